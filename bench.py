@@ -1,0 +1,223 @@
+"""Benchmark: GiB/s of masked WebSocket payload unmasked, device-resident, 64 KiB-frame batch.
+
+One step = one full batched decode (libwscodec wsc_decode: header walk -> scan -> record emit ->
+XOR unmask in place -> utf8 pass) of a device-resident batch of 16,384 masked 64 KiB BIN frames
+(1 GiB of payload, 14-byte headers, 4 frames per connection segment) per GPU.  Multi-GPU: one
+process per GPU (torchrun), each rank decodes its own independent shard (seed + rank) -- the path
+shards by connection with no collective; torch.distributed is used only for the barrier and the
+max-over-ranks time.  Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+FRAMES = 16384
+FRAME_BYTES = 65536
+FRAMES_PER_SEG = 4
+RECORD_BYTES = 32          # sizeof(wsc_frame)
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--frames", type=int, default=FRAMES)
+    ap.add_argument("--frame-bytes", type=int, default=FRAME_BYTES)
+    ap.add_argument("--frames-per-seg", type=int, default=FRAMES_PER_SEG)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-host-inclusive", action="store_true")
+    ap.add_argument("--window", type=int, default=0, help="unmask window bytes (0 = library default)")
+    ap.add_argument("--waves-per-cu", type=int, default=0)
+    return ap.parse_args()
+
+
+def cpu_baseline(cfg, seconds, threads):
+    """The reference's hot loop (websocket_frame.go:33-42) ported to C (oracle/go_unmask_port.c),
+    on a bounded sample of the same frames: repeated passes over the first 256 frames (16 MiB)
+    until `seconds` of wall time have elapsed."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_ref as O
+    lib = O.goport()
+    ns = min(256, cfg["n_frames"])
+    wire = cfg["wire"]
+    off = np.ascontiguousarray(cfg["payload_off"][:ns], dtype=np.uint64)
+    ln = np.ascontiguousarray(cfg["plen"][:ns], dtype=np.uint32)
+    mk = np.ascontiguousarray(cfg["mask"][:ns], dtype=np.uint32)
+    args = (wire.ctypes.data, off.ctypes.data, ln.ctypes.data, mk.ctypes.data, ns)
+    passes, t0 = 0, time.perf_counter()
+    while True:
+        if threads == 1:
+            lib.goport_unmask_frames(*args)
+        else:
+            lib.goport_unmask_frames_mt(*args, threads)
+        passes += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    gib = passes * int(ln.sum()) / 2**30
+    return gib / el, passes, el
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    from netman_amd import codec as K
+    from netman_amd import synth
+
+    seed = synth.SEED_BASE + 1 + 1000 * rank
+    cfg = synth.uniform_batch(a.frames, a.frame_bytes, a.frames_per_seg, seed=seed)
+    n_bytes = len(cfg["wire"])
+    n_segs = len(cfg["seg_off"]) - 1
+    over = dict(max_batch_bytes=n_bytes + 4096, max_segs=n_segs, max_frames=a.frames + 16)
+    if a.window:
+        over["unmask_window"] = a.window
+    if a.waves_per_cu:
+        over["unmask_waves_per_cu"] = a.waves_per_cu
+    codec = K.Codec(local, **over)
+
+    wire = torch.from_numpy(cfg["wire"]).to(dev)
+    seg_off = torch.from_numpy(cfg["seg_off"].view(np.int64)).to(dev)
+    st_out = torch.zeros(n_segs * 16, dtype=torch.uint8, device=dev)
+    seg_out = torch.zeros(n_segs * 32, dtype=torch.uint8, device=dev)
+    frames = torch.zeros((a.frames + 16) * 32, dtype=torch.uint8, device=dev)
+    summ = torch.zeros(32, dtype=torch.uint8, device=dev)
+    batch = codec.make_batch(wire, seg_off, None, st_out, seg_out, frames, summ)
+
+    # correctness gate on the real workload before timing (size-independent property: the first
+    # decode must equal the numpy restatement on a sample of frames)
+    codec.decode(batch)
+    codec.sync()
+    host = wire[: min(n_bytes, 64 * (a.frame_bytes + 14))].cpu().numpy()
+    k = int(np.searchsorted(cfg["payload_off"] + cfg["plen"], len(host), side="right"))
+    ref = synth.unmask_reference(cfg["wire"][: len(host)], cfg["payload_off"][:k], cfg["plen"][:k], cfg["mask"][:k])
+    ok = bool(np.array_equal(host[: int(cfg["payload_off"][k - 1] + cfg["plen"][k - 1])],
+                             ref[: int(cfg["payload_off"][k - 1] + cfg["plen"][k - 1])]))
+    summ_h = summ.cpu().numpy().view(K.SUMMARY_DTYPE)[0]
+    ok = ok and int(summ_h["n_frames"]) == a.frames and int(summ_h["n_spans"]) == a.frames
+
+    for _ in range(a.warmup):
+        codec.decode(batch)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        codec.decode(batch)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+        okt = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+        ok = bool(okt.item())
+
+    # per-kernel device time (hipEvents on the codec's launch stream)
+    prof = codec.profile(batch, max(5, min(a.steps, 20)))
+
+    payload = cfg["payload_bytes"]
+    value = payload * world * a.steps / el / 2**30
+    hdr = 14 if a.frame_bytes > 65535 else (8 if a.frame_bytes > 125 else 6)
+    alg_bytes = a.frames * (2 * a.frame_bytes + hdr + RECORD_BYTES)
+    unmask_ms = prof["unmask"]
+    achieved = alg_bytes / (unmask_ms * 1e-3) / 1e9
+    traffic = None
+    if os.path.exists(PMC_FILE):
+        try:
+            pm = json.load(open(PMC_FILE))
+            if pm.get("frames") == a.frames and pm.get("frame_bytes") == a.frame_bytes:
+                traffic = pm.get("unmask_hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    out = {
+        "metric": "GiB/s masked WebSocket payload unmasked, device-resident, 64 KiB-frame batch",
+        "value": round(value, 2),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(el / a.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (seeded masked BIN frames, uniform random payload and masks)",
+        "config": {"workload": f"{a.frames} x {a.frame_bytes} B masked BIN frames per GPU "
+                               f"({payload / 2**30:.3f} GiB payload, {hdr} B headers, "
+                               f"{a.frames_per_seg} frames per connection segment), in-place unmask",
+                   "frames_per_gpu": a.frames, "frame_bytes": a.frame_bytes,
+                   "segments_per_gpu": n_segs, "parallelism": f"shard{world}"},
+        "parity_ok": ok,
+        "kernel_ms": {k: round(v, 5) for k, v in prof.items()},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "kernel": "k_unmask", "alg_bytes_per_launch": alg_bytes},
+    }
+    if rank == 0 and not a.no_host_inclusive:
+        out["host_inclusive"] = host_inclusive(codec, cfg, K)
+    if rank == 0 and not a.no_cpu and a.cpu_seconds > 0:
+        threads = min(16, len(os.sched_getaffinity(0)))
+        v1, p1, e1 = cpu_baseline(cfg, a.cpu_seconds / 2, 1)
+        vm, pm_, em = cpu_baseline(cfg, a.cpu_seconds / 2, threads)
+        out["cpu_baseline"] = {"value": round(vm, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+                               "sample": f"first 256 frames (16 MiB payload) of the same batch, {pm_} passes "
+                                         f"in {em:.1f} s; C port of websocket_frame.go:33-42 (Go absent)",
+                               "value_1core": round(v1, 3)}
+    if rank == 0:
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+    codec.close()
+
+
+def host_inclusive(codec, cfg, K):
+    """wsc_decode_host on pinned host buffers: H2D of the wire, decode, D2H of the unmasked wire
+    and the records (reported in DESIGN.md, never as `value`)."""
+    lib = K.load_library()
+    n = len(cfg["wire"])
+    p = C.c_void_p()
+    if lib.wsc_host_alloc(n, C.byref(p)) != 0:
+        return None
+    try:
+        buf = np.frombuffer((C.c_uint8 * n).from_address(p.value), dtype=np.uint8)
+        buf[:] = cfg["wire"]
+        t0 = time.perf_counter()
+        iters = 3
+        for _ in range(iters):
+            codec.decode_host(buf, cfg["seg_off"])
+        el = (time.perf_counter() - t0) / iters
+        return {"gib_s": round(cfg["payload_bytes"] / el / 2**30, 2), "ms_per_batch": round(el * 1e3, 2),
+                "note": "pinned host wire -> H2D -> decode -> D2H wire+records, synchronous"}
+    finally:
+        lib.wsc_host_free(p)
+
+
+if __name__ == "__main__":
+    main()

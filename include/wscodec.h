@@ -1,0 +1,223 @@
+/*
+ * wscodec.h -- C ABI of the MI355X WebSocket frame codec (libwscodec.so).
+ *
+ * This is the drop-in boundary for netman's websocket DECODE path.  In the
+ * reference (pure Go) the path sits behind the internal interface
+ *     iface.IConnectEvent.DecodePacket() (IMessage, error)          iface/iconnect.go:38-39
+ * implemented by websocketProtocol.DecodePacket                       server/websocket.go:82-212
+ *   -> parseHeadBytes / parsePayloadLength                            server/websocket.go:214-302
+ *   -> nextFrame (XOR unmask at :35-39, reassembly, utf8, Message)    server/websocket_frame.go:13-103
+ * and its results reach the public iface.IWebsocketHandler.Message    iface/iwebsockethandler.go:4-8
+ * with the error -> close-code mapping of eventloop/epoll.go:106-129.
+ *
+ * The ABI replaces that per-frame, per-read decode with ONE batched call over many connections'
+ * bulk socket reads ("segments"), run as hand-written gfx950 kernels:
+ *   wsc_decode()        device-resident batch (the hot path)        replaces websocket.go:82-302 +
+ *                                                                   websocket_frame.go:13-103
+ *   wsc_decode_host()   host buffers in/out through pinned staging  same, plus the readData copy
+ *   wsc_session_*       per-connection DecodePacket() mirror        replaces IConnectEvent.DecodePacket
+ *                       (pending-message queue, carry-over)         (iface/iconnect.go:38-39)
+ * Plain pointers and sizes only; no exceptions cross the ABI; every function returns WSC_OK (0)
+ * or a negative WSC_E_* code.  INTEGRATION.md shows the cgo binding a netman maintainer would add.
+ */
+#ifndef WSCODEC_H
+#define WSCODEC_H
+#include <stddef.h>
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define WSC_ABI_VERSION 1
+
+/* ---- return codes --------------------------------------------------------------------------- */
+#define WSC_OK 0
+#define WSC_E_INVAL (-1)     /* bad argument / shape */
+#define WSC_E_DEVICE (-2)    /* HIP runtime error (wsc_last_error() has the text) */
+#define WSC_E_NOMEM (-3)     /* allocation failed */
+#define WSC_E_CAPACITY (-4)  /* batch exceeds the context's configured capacity */
+#define WSC_E_NODEVICE (-5)  /* no usable gfx950 device */
+#define WSC_E_STATE (-6)     /* session misuse (unknown / closed connection) */
+
+/* ---- per-frame error sentinels: util/errors.go:9-14 (same order/values as the oracle) -------- */
+#define WSC_ERR_NONE 0
+#define WSC_ERR_OPCODE_FAIL 1            /* WebsocketOpcodeFail                     -> 1002 */
+#define WSC_ERR_RSV_FAIL 2               /* WebsocketRsvFail                        -> 1002 */
+#define WSC_ERR_PING_PAYLOAD_OVERSIZE 3  /* WebsocketPingPayloadOversize            -> 1002 */
+#define WSC_ERR_CTRL_FRAGMENTED 4        /* WebsocketCtrlMessageMustNotFragmented   -> 1002 */
+#define WSC_ERR_MUST_UTF8 5              /* WebsocketMustUtf8                       -> 1007 */
+#define WSC_ERR_PROTOCOL_ERROR 6         /* WebsocketProtocolError                  -> 1002 */
+#define WSC_ERR_TOO_LARGE 7              /* payload > max_frame_len (reference would panic, Q4) -> 1002 */
+
+/* ---- what the decoder did with a frame (websocket.go:136-208 / websocket_frame.go:52-102) --- */
+#define WSC_FK_FRAG 0        /* FIN=0 through nextFrame: payload appended to continueBuffer      */
+#define WSC_FK_MESSAGE 1     /* FIN=1 data frame: util.Message{MsgID=msg_id, Opcode=mode}        */
+#define WSC_FK_PING 2        /* PING: reply PONG echoing the payload (websocket_ctrl.go:128-153) */
+#define WSC_FK_PONG 3        /* PONG with payload: consumed                                      */
+#define WSC_FK_CLOSE 4       /* CLOSE frame: reply CloseCode(1000) and close                     */
+#define WSC_FK_PONG_EMPTY 5  /* PONG without payload: Close() (websocket.go:198-201)             */
+#define WSC_FK_ERROR 6       /* sentinel `err` at this frame: CloseCode(1002|1007)               */
+#define WSC_FK_STALL 7       /* unmasked client frame: reference returns EAGAIN forever (Q3)     */
+
+/* wsc_frame.flags */
+#define WSC_FF_UNMASKED 0x01  /* payload went through nextFrame and was XOR-unmasked             */
+#define WSC_FF_CONT_MSG 0x02  /* MESSAGE whose data = continueBuffer || this payload (:62-68)    */
+#define WSC_FF_U8_PART 0x04   /* internal: FRAG of a TEXT chain (utf8 state carried)            */
+#define WSC_FF_U8_SELF 0x08   /* internal: payload alone must be valid utf8                     */
+#define WSC_FF_U8_CHAIN 0x10  /* internal: continueBuffer || payload must be valid utf8          */
+#define WSC_FF_U8_REASON 0x20 /* internal: CLOSE reason payload[2:] must be valid utf8          */
+#define WSC_FF_CTRL_ARENA 0x40 /* COMPACT: payload placed in the control region of the arena    */
+
+/* ---- per-connection terminal status ---------------------------------------------------------- */
+#define WSC_SEG_OPEN 0      /* connection continues; bytes [consumed, len) are carried over        */
+#define WSC_SEG_CLOSED 1    /* CLOSE frame or empty PONG: CloseCode(1000, "")                       */
+#define WSC_SEG_ERROR 2     /* protocol error: CloseCode(close_code = 1002 | 1007), see err        */
+#define WSC_SEG_STALLED 3   /* unmasked frame: nothing more is ever delivered (Q3)                  */
+
+/* batch flags */
+#define WSC_F_COMPACT 0x1   /* write unmasked payloads compacted into `arena` (messages contiguous)
+                               instead of unmasking the wire buffer in place                       */
+
+/* Decoder state carried between batches for one connection (subset of websocket.go:38-56).   */
+typedef struct wsc_conn_state {
+    uint64_t cont_len;     /* continueBuffer length (bytes of an unfinished fragmented message)  */
+    uint32_t msg_id;       /* msgID: next Message.MsgID                                          */
+    uint8_t message_mode;  /* messageMode: 0, 1 (text) or 2 (binary)                             */
+    uint8_t cont_utf8;     /* utf8 DFA state after continueBuffer (0 = complete characters)      */
+    uint8_t status;        /* WSC_SEG_*; a connection that is not OPEN decodes nothing           */
+    uint8_t pad;
+} wsc_conn_state;          /* 16 B */
+
+/* One record per frame whose header was parsed and acted on, in stream order.                  */
+typedef struct wsc_frame {
+    uint64_t hdr_off;      /* batch offset of the frame's first header byte                      */
+    uint32_t payload_len;  /* fragmentLength                                                     */
+    uint32_t mask;         /* the 4 mask bytes, wire byte 0 in bits 0..7                         */
+    uint32_t seg;          /* segment (connection slot) index                                    */
+    uint32_t msg_id;       /* msgID before this frame (Message.MsgID for WSC_FK_MESSAGE)         */
+    uint8_t opcode;        /* header opcode                                                      */
+    uint8_t fin;           /* header FIN bit                                                     */
+    uint8_t kind;          /* WSC_FK_*                                                           */
+    uint8_t mode;          /* messageMode after this header (Message.Opcode for MESSAGE)        */
+    uint8_t err;           /* WSC_ERR_* for WSC_FK_ERROR                                         */
+    uint8_t hdr_len;       /* 6 / 8 / 14 for complete masked headers; payload_off = hdr_off+hdr_len */
+    uint8_t flags;         /* WSC_FF_*                                                           */
+    uint8_t pad;
+} wsc_frame;               /* 32 B */
+
+/* Per-segment result.                                                                          */
+typedef struct wsc_seg_result {
+    uint64_t consumed;     /* bytes of the segment fully decoded (carry = [consumed, seg_len))   */
+    uint32_t frame_begin;  /* index of the segment's first wsc_frame                             */
+    uint32_t frame_count;
+    uint32_t status;       /* WSC_SEG_*                                                          */
+    uint32_t close_code;   /* 1000 / 1002 / 1007 when status is CLOSED or ERROR                  */
+    uint32_t err;          /* WSC_ERR_* when status == WSC_SEG_ERROR                             */
+    uint32_t pad;
+} wsc_seg_result;          /* 32 B */
+
+/* Batch totals written by the device.                                                          */
+typedef struct wsc_summary {
+    uint64_t data_bytes;   /* COMPACT: bytes in the data region of the arena                      */
+    uint64_t ctrl_bytes;   /* COMPACT: bytes in the control region (starts at data_bytes)         */
+    uint32_t n_frames;     /* frames in `frames`                                                  */
+    uint32_t n_spans;      /* payload spans unmasked                                              */
+    uint32_t overflow;     /* 1 if n_frames > frames_cap (records beyond the cap were dropped)    */
+    uint32_t pad;
+} wsc_summary;
+
+typedef struct wsc_batch {
+    uint8_t* wire;                   /* device: n_bytes, all segments back to back               */
+    uint64_t n_bytes;
+    const uint64_t* seg_off;         /* device: n_segs+1 offsets, [0]=0, [n_segs]=n_bytes        */
+    uint32_t n_segs;
+    uint32_t flags;                  /* WSC_F_*                                                  */
+    const wsc_conn_state* state_in;  /* device: n_segs (NULL = fresh connections)               */
+    wsc_conn_state* state_out;       /* device: n_segs                                           */
+    wsc_seg_result* seg_out;         /* device: n_segs                                           */
+    wsc_frame* frames;               /* device: frames_cap                                       */
+    uint32_t frames_cap;
+    uint32_t pad;
+    uint8_t* arena;                  /* device, COMPACT only: >= n_bytes + 64 bytes              */
+    uint64_t* frame_dst;             /* device, COMPACT only: per-frame arena offset             */
+    wsc_summary* summary;            /* device: 1                                                */
+} wsc_batch;
+
+typedef struct wsc_config {
+    uint64_t max_batch_bytes;  /* largest n_bytes a batch may have                               */
+    uint32_t max_segs;         /* largest n_segs                                                 */
+    uint32_t max_frames;       /* largest number of frames in one batch                          */
+    uint64_t max_frame_len;    /* payloads above this -> WSC_ERR_TOO_LARGE (<= 0xFFFFFFFF)       */
+    uint32_t unmask_window;    /* bytes per wave-window in the unmask kernel (0 = default)       */
+    uint32_t unmask_waves_per_cu; /* unmask grid sizing (0 = default)                            */
+    uint32_t unmask_nt;        /* bit0: non-temporal payload loads, bit1: non-temporal stores     */
+    uint32_t pad;
+} wsc_config;
+
+typedef struct wsc_ctx wsc_ctx;
+
+int wsc_abi_version(void);
+const char* wsc_last_error(void);
+int wsc_config_default(wsc_config* cfg);
+
+int wsc_create(int device, const wsc_config* cfg, wsc_ctx** out);
+int wsc_destroy(wsc_ctx* ctx);
+
+int wsc_dev_alloc(wsc_ctx* ctx, uint64_t bytes, void** out);
+int wsc_dev_free(wsc_ctx* ctx, void* p);
+int wsc_host_alloc(uint64_t bytes, void** out);   /* pinned (hipHostMalloc) */
+int wsc_host_free(void* p);
+
+/* Enqueue the decode of one device-resident batch on `hip_stream` (hipStream_t, NULL = the
+ * context's own stream).  Asynchronous: results are valid once the stream is synchronised. */
+int wsc_decode(wsc_ctx* ctx, const wsc_batch* batch, void* hip_stream);
+int wsc_sync(wsc_ctx* ctx, void* hip_stream);
+
+/* Host-buffer path: copies wire/offsets/state to the device through the context's pinned
+ * staging, decodes, and copies results back (synchronous).  In-place mode rewrites `wire`;
+ * COMPACT mode fills `arena` (host, >= n_bytes + 64).  `frames` has room for `frames_cap`. */
+int wsc_decode_host(wsc_ctx* ctx, uint8_t* wire, uint64_t n_bytes, const uint64_t* seg_off,
+                    uint32_t n_segs, uint32_t flags, const wsc_conn_state* state_in,
+                    wsc_conn_state* state_out, wsc_seg_result* seg_out, wsc_frame* frames,
+                    uint32_t frames_cap, uint8_t* arena, uint64_t* frame_dst, wsc_summary* summary);
+
+/* Timing helper for the benchmark: run `iters` back-to-back decodes of a device batch and
+ * return the per-kernel average device time (ms) measured with hipEvents on the launch stream.
+ * out_ms[0..4] = walk(count), scan, walk(emit), unmask, utf8;  out_ms[5] = whole decode. */
+int wsc_profile(wsc_ctx* ctx, const wsc_batch* batch, int iters, double* out_ms);
+
+/* ---- session: the per-connection DecodePacket() mirror (C++ host side above the ABI) --------- */
+typedef struct wsc_session wsc_session;
+
+/* events popped by wsc_session_next(); mirrors what DecodePacket + epoll.go:104-140 produce   */
+#define WSC_EV_NONE 0      /* (nil, EAGAIN): nothing pending for this connection               */
+#define WSC_EV_MESSAGE 1   /* (Message, nil): deliver to IWebsocketHandler.Message             */
+#define WSC_EV_PONG 2      /* PING answered: send a PONG frame with `data`                     */
+#define WSC_EV_CLOSE 3     /* CloseCode(close_code); err = sentinel (0 for a normal close)      */
+#define WSC_EV_STALL 4     /* unmasked frame: nothing more will be delivered (Q3)              */
+
+typedef struct wsc_event {
+    uint32_t type;        /* WSC_EV_* */
+    uint32_t msg_id;      /* MESSAGE: Message.MsgID */
+    uint32_t opcode;      /* MESSAGE: Message.Opcode (1 text, 2 binary) */
+    uint32_t close_code;  /* CLOSE */
+    uint32_t err;         /* CLOSE: WSC_ERR_* */
+    uint32_t pad;
+    const uint8_t* data;  /* MESSAGE / PONG payload, owned by the session until the next
+                             wsc_session_decode() */
+    uint64_t len;
+} wsc_event;
+
+int wsc_session_create(int device, const wsc_config* cfg, uint32_t flags, wsc_session** out);
+int wsc_session_destroy(wsc_session* s);
+int wsc_session_open(wsc_session* s, uint32_t* conn_out);            /* newWebsocketProtocol */
+int wsc_session_remove(wsc_session* s, uint32_t conn);               /* remove() */
+int wsc_session_feed(wsc_session* s, uint32_t conn, const uint8_t* bytes, uint64_t n);
+int wsc_session_decode(wsc_session* s);                              /* one batched device pass */
+int wsc_session_next(wsc_session* s, uint32_t conn, wsc_event* ev);  /* DecodePacket() */
+int wsc_session_state(wsc_session* s, uint32_t conn, wsc_conn_state* st, uint64_t* carry_bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* WSCODEC_H */

@@ -1,0 +1,46 @@
+"""Build recipes for the in-tree native libraries (gfx950 only).
+
+libwscodec.so  <- netman_amd/csrc/{wsc_kernels.hip, wsc_api.cpp, wsc_session.cpp}   (hipcc)
+The oracle (test infrastructure) has its own recipe in oracle/Makefile; __graft_entry__.build()
+drives both.
+"""
+import os
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+LIB = os.path.join(HERE, "libwscodec.so")
+SOURCES = ["wsc_kernels.hip", "wsc_api.cpp", "wsc_session.cpp"]
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+
+
+def _newest(paths):
+    return max(os.path.getmtime(p) for p in paths)
+
+
+def build_codec(force=False, verbose=False):
+    srcs = [os.path.join(CSRC, s) for s in SOURCES]
+    deps = srcs + [os.path.join(CSRC, "wsc_kernels.hpp"), os.path.join(ROOT, "include", "wscodec.h")]
+    if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= _newest(deps):
+        return LIB
+    objs = []
+    for s in srcs:
+        o = os.path.join("/tmp", "wsc_" + os.path.basename(s) + ".o")
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
+               "-x", "hip", "-c", s, "-o", o]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.run(cmd, check=True)
+        objs.append(o)
+    tmp = LIB + ".tmp"
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, LIB)
+    return LIB
+
+
+def build_oracle(force=False):
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")] + (["-B"] if force else []),
+                   check=True)

@@ -1,0 +1,379 @@
+"""ctypes binding of libwscodec.so (include/wscodec.h) and the Python mirror of netman's
+websocket decode surface.
+
+Reference surface mirrored here (ikilobyte/netman, Go):
+  util/message.go:4-53      Message{MsgID, DataLen, Data, IsWebSocket, Opcode} + ID/Bytes/String/...
+  util/errors.go:9-14       websocket error sentinels (same texts)
+  iface/iconnect.go:38-39   IConnectEvent.DecodePacket() (IMessage, error)   -> Session.DecodePacket
+  eventloop/epoll.go:106-129 sentinel -> close code                          -> close_code_for()
+
+The product path is the HIP library: if libwscodec.so cannot be loaded, or no gfx950 device is
+present, every entry point raises.  There is no CPU fallback in this package.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libwscodec.so")
+
+# ---- constants (include/wscodec.h) -------------------------------------------------------------
+WSC_OK = 0
+WSC_E_INVAL, WSC_E_DEVICE, WSC_E_NOMEM, WSC_E_CAPACITY, WSC_E_NODEVICE, WSC_E_STATE = -1, -2, -3, -4, -5, -6
+
+ERR_NONE, ERR_OPCODE_FAIL, ERR_RSV_FAIL, ERR_PING_PAYLOAD_OVERSIZE = 0, 1, 2, 3
+ERR_CTRL_FRAGMENTED, ERR_MUST_UTF8, ERR_PROTOCOL_ERROR, ERR_TOO_LARGE = 4, 5, 6, 7
+
+FK_FRAG, FK_MESSAGE, FK_PING, FK_PONG, FK_CLOSE, FK_PONG_EMPTY, FK_ERROR, FK_STALL = range(8)
+FF_UNMASKED, FF_CONT_MSG, FF_CTRL_ARENA = 0x01, 0x02, 0x40
+
+SEG_OPEN, SEG_CLOSED, SEG_ERROR, SEG_STALLED = 0, 1, 2, 3
+F_COMPACT = 0x1
+
+EV_NONE, EV_MESSAGE, EV_PONG, EV_CLOSE, EV_STALL = 0, 1, 2, 3, 4
+
+# ---- numpy views of the ABI records ------------------------------------------------------------
+CONN_STATE_DTYPE = np.dtype([("cont_len", "<u8"), ("msg_id", "<u4"), ("message_mode", "u1"),
+                             ("cont_utf8", "u1"), ("status", "u1"), ("pad", "u1")])
+FRAME_DTYPE = np.dtype([("hdr_off", "<u8"), ("payload_len", "<u4"), ("mask", "<u4"), ("seg", "<u4"),
+                        ("msg_id", "<u4"), ("opcode", "u1"), ("fin", "u1"), ("kind", "u1"),
+                        ("mode", "u1"), ("err", "u1"), ("hdr_len", "u1"), ("flags", "u1"),
+                        ("pad", "u1")])
+SEG_RESULT_DTYPE = np.dtype([("consumed", "<u8"), ("frame_begin", "<u4"), ("frame_count", "<u4"),
+                             ("status", "<u4"), ("close_code", "<u4"), ("err", "<u4"), ("pad", "<u4")])
+SUMMARY_DTYPE = np.dtype([("data_bytes", "<u8"), ("ctrl_bytes", "<u8"), ("n_frames", "<u4"),
+                          ("n_spans", "<u4"), ("overflow", "<u4"), ("pad", "<u4")])
+assert CONN_STATE_DTYPE.itemsize == 16 and FRAME_DTYPE.itemsize == 32
+assert SEG_RESULT_DTYPE.itemsize == 32 and SUMMARY_DTYPE.itemsize == 32
+
+
+class WscConfig(C.Structure):
+    _fields_ = [("max_batch_bytes", C.c_uint64), ("max_segs", C.c_uint32), ("max_frames", C.c_uint32),
+                ("max_frame_len", C.c_uint64), ("unmask_window", C.c_uint32),
+                ("unmask_waves_per_cu", C.c_uint32), ("unmask_nt", C.c_uint32), ("pad", C.c_uint32)]
+
+
+class WscBatch(C.Structure):
+    _fields_ = [("wire", C.c_void_p), ("n_bytes", C.c_uint64), ("seg_off", C.c_void_p),
+                ("n_segs", C.c_uint32), ("flags", C.c_uint32), ("state_in", C.c_void_p),
+                ("state_out", C.c_void_p), ("seg_out", C.c_void_p), ("frames", C.c_void_p),
+                ("frames_cap", C.c_uint32), ("pad", C.c_uint32), ("arena", C.c_void_p),
+                ("frame_dst", C.c_void_p), ("summary", C.c_void_p)]
+
+
+class WscEvent(C.Structure):
+    _fields_ = [("type", C.c_uint32), ("msg_id", C.c_uint32), ("opcode", C.c_uint32),
+                ("close_code", C.c_uint32), ("err", C.c_uint32), ("pad", C.c_uint32),
+                ("data", C.POINTER(C.c_uint8)), ("len", C.c_uint64)]
+
+
+class WscConnState(C.Structure):
+    _fields_ = [("cont_len", C.c_uint64), ("msg_id", C.c_uint32), ("message_mode", C.c_uint8),
+                ("cont_utf8", C.c_uint8), ("status", C.c_uint8), ("pad", C.c_uint8)]
+
+
+# every function include/wscodec.h declares, with its ctypes signature
+_P, _U32, _U64, _I = C.c_void_p, C.c_uint32, C.c_uint64, C.c_int
+SIGNATURES = {
+    "wsc_abi_version": (_I, []),
+    "wsc_last_error": (C.c_char_p, []),
+    "wsc_config_default": (_I, [C.POINTER(WscConfig)]),
+    "wsc_create": (_I, [_I, C.POINTER(WscConfig), C.POINTER(_P)]),
+    "wsc_destroy": (_I, [_P]),
+    "wsc_dev_alloc": (_I, [_P, _U64, C.POINTER(_P)]),
+    "wsc_dev_free": (_I, [_P, _P]),
+    "wsc_host_alloc": (_I, [_U64, C.POINTER(_P)]),
+    "wsc_host_free": (_I, [_P]),
+    "wsc_decode": (_I, [_P, C.POINTER(WscBatch), _P]),
+    "wsc_sync": (_I, [_P, _P]),
+    "wsc_decode_host": (_I, [_P, _P, _U64, _P, _U32, _U32, _P, _P, _P, _P, _U32, _P, _P, _P]),
+    "wsc_profile": (_I, [_P, C.POINTER(WscBatch), _I, C.POINTER(C.c_double)]),
+    "wsc_session_create": (_I, [_I, C.POINTER(WscConfig), _U32, C.POINTER(_P)]),
+    "wsc_session_destroy": (_I, [_P]),
+    "wsc_session_open": (_I, [_P, C.POINTER(_U32)]),
+    "wsc_session_remove": (_I, [_P, _U32]),
+    "wsc_session_feed": (_I, [_P, _U32, _P, _U64]),
+    "wsc_session_decode": (_I, [_P]),
+    "wsc_session_next": (_I, [_P, _U32, C.POINTER(WscEvent)]),
+    "wsc_session_state": (_I, [_P, _U32, C.POINTER(WscConnState), C.POINTER(_U64)]),
+}
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH):
+    """Load libwscodec.so (raises OSError if it is missing: there is no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise OSError(f"libwscodec.so not built ({path}); run __graft_entry__.build()")
+    lib = C.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+class WscError(RuntimeError):
+    def __init__(self, rc: int, where: str):
+        lib = load_library()
+        super().__init__(f"{where} failed: rc={rc} ({lib.wsc_last_error().decode(errors='replace')})")
+        self.rc = rc
+
+
+def _check(rc: int, where: str):
+    if rc != WSC_OK:
+        raise WscError(rc, where)
+
+
+def default_config(**over) -> WscConfig:
+    lib = load_library()
+    cfg = WscConfig()
+    _check(lib.wsc_config_default(C.byref(cfg)), "wsc_config_default")
+    for k, v in over.items():
+        setattr(cfg, k, v)
+    return cfg
+
+
+def _ptr(a) -> int:
+    """device/host address of a numpy array or torch tensor (None -> NULL)"""
+    if a is None:
+        return 0
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data
+    return a.data_ptr()
+
+
+@dataclass
+class DecodeResult:
+    seg: np.ndarray          # SEG_RESULT_DTYPE [n_segs]
+    state: np.ndarray        # CONN_STATE_DTYPE [n_segs]
+    frames: np.ndarray       # FRAME_DTYPE [n_frames]
+    summary: np.ndarray      # SUMMARY_DTYPE scalar
+    frame_dst: np.ndarray | None = None
+    arena: np.ndarray | None = None
+
+
+class Codec:
+    """One device context (wsc_ctx)."""
+
+    def __init__(self, device: int = 0, **cfg_over):
+        self.lib = load_library()
+        self.cfg = default_config(**cfg_over)
+        h = C.c_void_p()
+        _check(self.lib.wsc_create(device, C.byref(self.cfg), C.byref(h)), "wsc_create")
+        self.h = h
+
+    def close(self):
+        if self.h:
+            self.lib.wsc_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # device-resident batch: all arguments are torch CUDA tensors (or None)
+    def make_batch(self, wire, seg_off, state_in, state_out, seg_out, frames, summary,
+                   compact=False, arena=None, frame_dst=None, n_bytes=None) -> WscBatch:
+        b = WscBatch()
+        b.wire = _ptr(wire)
+        b.n_bytes = int(wire.numel() if n_bytes is None else n_bytes)
+        b.seg_off = _ptr(seg_off)
+        b.n_segs = int(seg_off.numel() - 1)
+        b.flags = F_COMPACT if compact else 0
+        b.state_in = _ptr(state_in)
+        b.state_out = _ptr(state_out)
+        b.seg_out = _ptr(seg_out)
+        b.frames = _ptr(frames)
+        b.frames_cap = int(frames.numel() // FRAME_DTYPE.itemsize)
+        b.arena = _ptr(arena)
+        b.frame_dst = _ptr(frame_dst)
+        b.summary = _ptr(summary)
+        return b
+
+    def decode(self, batch: WscBatch, stream=None):
+        _check(self.lib.wsc_decode(self.h, C.byref(batch), stream), "wsc_decode")
+
+    def sync(self, stream=None):
+        _check(self.lib.wsc_sync(self.h, stream), "wsc_sync")
+
+    def profile(self, batch: WscBatch, iters: int):
+        out = (C.c_double * 6)()
+        _check(self.lib.wsc_profile(self.h, C.byref(batch), iters, out), "wsc_profile")
+        return dict(zip(["walk_count", "scan", "walk_emit", "unmask", "utf8", "total"], list(out)))
+
+    def decode_host(self, wire: np.ndarray, seg_off: np.ndarray, state_in: np.ndarray | None = None,
+                    compact: bool = False, frames_cap: int | None = None) -> DecodeResult:
+        """Host-buffer path (H2D, decode, D2H).  In-place mode rewrites `wire`."""
+        assert wire.dtype == np.uint8 and wire.flags.c_contiguous
+        seg_off = np.ascontiguousarray(seg_off, dtype=np.uint64)
+        n = len(seg_off) - 1
+        cap = int(frames_cap or self.cfg.max_frames)
+        state_out = np.zeros(n, CONN_STATE_DTYPE)
+        seg = np.zeros(n, SEG_RESULT_DTYPE)
+        frames = np.zeros(cap, FRAME_DTYPE)
+        summary = np.zeros(1, SUMMARY_DTYPE)
+        arena = np.zeros(len(wire) + 64, np.uint8) if compact else None
+        frame_dst = np.zeros(cap, np.uint64) if compact else None
+        if state_in is not None:
+            state_in = np.ascontiguousarray(state_in, dtype=CONN_STATE_DTYPE)
+        rc = self.lib.wsc_decode_host(self.h, _ptr(wire), len(wire), _ptr(seg_off), n,
+                                      F_COMPACT if compact else 0, _ptr(state_in), _ptr(state_out),
+                                      _ptr(seg), _ptr(frames), cap, _ptr(arena), _ptr(frame_dst),
+                                      _ptr(summary))
+        _check(rc, "wsc_decode_host")
+        nf = int(summary[0]["n_frames"])
+        return DecodeResult(seg=seg, state=state_out, frames=frames[:nf].copy(), summary=summary[0],
+                            frame_dst=None if frame_dst is None else frame_dst[:nf].copy(),
+                            arena=arena)
+
+
+# ---- netman's message / error surface ----------------------------------------------------------
+class Message:
+    """util.Message (util/message.go:4-53)."""
+    __slots__ = ("MsgID", "DataLen", "Data", "IsWebSocket", "Opcode")
+
+    def __init__(self, MsgID: int, Data: bytes, Opcode: int, IsWebSocket: bool = True):
+        self.MsgID = MsgID
+        self.Data = Data
+        self.DataLen = len(Data)
+        self.IsWebSocket = IsWebSocket
+        self.Opcode = Opcode
+
+    def ID(self): return self.MsgID
+    def String(self): return self.Data.decode("utf-8", errors="replace")
+    def Bytes(self): return self.Data
+    def Len(self): return self.DataLen
+    def SetData(self, b: bytes): self.Data, self.DataLen = b, len(b)
+    def GetOpcode(self): return self.Opcode
+    def IsWebsocket(self): return self.IsWebSocket
+    def IsText(self): return self.Opcode == 1
+    def IsBinary(self): return self.Opcode == 2
+
+    def __repr__(self):
+        return f"Message(MsgID={self.MsgID}, Opcode={self.Opcode}, DataLen={self.DataLen})"
+
+
+class NetmanError(Exception):
+    pass
+
+
+# util/errors.go:9-14 (texts verbatim) + syscall.EAGAIN + io.EOF
+WebsocketOpcodeFail = NetmanError("websocket opcode fail")
+WebsocketRsvFail = NetmanError("websocket RSV must be 0")
+WebsocketPingPayloadOversize = NetmanError("websocket ping payload oversize")
+WebsocketCtrlMessageMustNotFragmented = NetmanError("websocket control message MUST NOT be fragmented")
+WebsocketMustUtf8 = NetmanError("websocket text message must utf-8")
+WebsocketProtocolError = NetmanError("websocket protocol error")
+WebsocketFrameTooLarge = NetmanError("websocket frame exceeds max_frame_len")  # Q4 divergence
+EAGAIN = NetmanError("resource temporarily unavailable")
+
+SENTINELS = {
+    ERR_OPCODE_FAIL: WebsocketOpcodeFail,
+    ERR_RSV_FAIL: WebsocketRsvFail,
+    ERR_PING_PAYLOAD_OVERSIZE: WebsocketPingPayloadOversize,
+    ERR_CTRL_FRAGMENTED: WebsocketCtrlMessageMustNotFragmented,
+    ERR_MUST_UTF8: WebsocketMustUtf8,
+    ERR_PROTOCOL_ERROR: WebsocketProtocolError,
+    ERR_TOO_LARGE: WebsocketFrameTooLarge,
+}
+
+
+def close_code_for(err) -> int | None:
+    """eventloop/epoll.go:106-129: which CloseCode the poller sends for a DecodePacket error."""
+    if err in (WebsocketOpcodeFail, WebsocketRsvFail, WebsocketCtrlMessageMustNotFragmented,
+               WebsocketProtocolError, WebsocketPingPayloadOversize, WebsocketFrameTooLarge):
+        return 1002
+    if err is WebsocketMustUtf8:
+        return 1007
+    return None
+
+
+@dataclass
+class Event:
+    type: int
+    msg_id: int = 0
+    opcode: int = 0
+    close_code: int = 0
+    err: int = 0
+    data: bytes = b""
+
+
+class Session:
+    """Many connections decoded in batches on one device (wsc_session_*)."""
+
+    def __init__(self, device: int = 0, compact: bool = False, **cfg_over):
+        self.lib = load_library()
+        self.cfg = default_config(**cfg_over)
+        h = C.c_void_p()
+        _check(self.lib.wsc_session_create(device, C.byref(self.cfg), F_COMPACT if compact else 0,
+                                           C.byref(h)), "wsc_session_create")
+        self.h = h
+
+    def close(self):
+        if self.h:
+            self.lib.wsc_session_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def open(self) -> int:
+        cid = C.c_uint32()
+        _check(self.lib.wsc_session_open(self.h, C.byref(cid)), "wsc_session_open")
+        return cid.value
+
+    def remove(self, conn: int):
+        _check(self.lib.wsc_session_remove(self.h, conn), "wsc_session_remove")
+
+    def feed(self, conn: int, data: bytes):
+        buf = (C.c_uint8 * len(data)).from_buffer_copy(data) if data else None
+        _check(self.lib.wsc_session_feed(self.h, conn, buf, len(data)), "wsc_session_feed")
+
+    def decode(self):
+        _check(self.lib.wsc_session_decode(self.h), "wsc_session_decode")
+
+    def next_event(self, conn: int) -> Event:
+        ev = WscEvent()
+        _check(self.lib.wsc_session_next(self.h, conn, C.byref(ev)), "wsc_session_next")
+        data = C.string_at(ev.data, ev.len) if ev.len else b""
+        return Event(ev.type, ev.msg_id, ev.opcode, ev.close_code, ev.err, data)
+
+    def events(self, conn: int) -> list[Event]:
+        out = []
+        while True:
+            e = self.next_event(conn)
+            if e.type == EV_NONE:
+                return out
+            out.append(e)
+
+    def DecodePacket(self, conn: int):
+        """IConnectEvent.DecodePacket() for an already-fed-and-decoded connection:
+        (Message, None) | (None, None) after a PONG reply / close | (None, sentinel) | (None, EAGAIN)."""
+        e = self.next_event(conn)
+        if e.type == EV_MESSAGE:
+            return Message(e.msg_id, e.data, e.opcode), None
+        if e.type == EV_CLOSE:
+            return None, (SENTINELS.get(e.err) if e.err else None)
+        if e.type == EV_PONG:
+            return None, None
+        return None, EAGAIN
+
+    def state(self, conn: int):
+        st = WscConnState()
+        carry = C.c_uint64()
+        _check(self.lib.wsc_session_state(self.h, conn, C.byref(st), C.byref(carry)), "wsc_session_state")
+        return st, carry.value

@@ -1,0 +1,377 @@
+// wsc_api.cpp -- host side of libwscodec: context, launch sequence, host-staged path, timing.
+// Compiled by hipcc together with wsc_kernels.hip (gfx950 only; no CPU fallback anywhere: a
+// missing device is an error, WSC_E_NODEVICE).
+#include <hip/hip_runtime.h>
+#include <rocprim/device/device_scan.hpp>
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "wsc_kernels.hpp"
+
+namespace wsc {
+template <bool EMIT, bool COMPACT> __global__ void k_walk(WalkArgs);
+template <bool COMPACT, int P, int NT>
+__global__ void k_unmask(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*,
+                         const wsc_summary*);
+template <bool COMPACT> __global__ void k_utf8(Utf8Args);
+}  // namespace wsc
+
+using namespace wsc;
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+#define HIP_TRY(expr)                                                                    \
+    do {                                                                                 \
+        hipError_t e_ = (expr);                                                          \
+        if (e_ != hipSuccess)                                                            \
+            return fail(WSC_E_DEVICE, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+uint32_t ilog2(uint32_t x) {
+    uint32_t r = 0;
+    while ((1u << (r + 1)) <= x) ++r;
+    return r;
+}
+}  // namespace
+
+struct wsc_ctx {
+    int device = 0;
+    int n_cu = 256;
+    hipStream_t stream = nullptr;
+    wsc_config cfg{};
+    uint32_t pieces = 8;          // 16 B pieces per lane -> window = pieces KiB
+    SegCount* counts = nullptr;
+    SegCount* bases = nullptr;
+    void* scan_tmp = nullptr;
+    size_t scan_tmp_bytes = 0;
+    Span* spans = nullptr;
+    uint32_t* tile = nullptr;
+    uint64_t tile_entries = 0;
+    // host-staged path buffers (lazily allocated)
+    uint8_t* d_wire = nullptr;
+    uint8_t* d_arena = nullptr;
+    uint64_t* d_seg_off = nullptr;
+    wsc_conn_state* d_state_in = nullptr;
+    wsc_conn_state* d_state_out = nullptr;
+    wsc_seg_result* d_seg_out = nullptr;
+    wsc_frame* d_frames = nullptr;
+    uint64_t* d_frame_dst = nullptr;
+    wsc_summary* d_summary = nullptr;
+};
+
+extern "C" {
+
+int wsc_abi_version(void) { return WSC_ABI_VERSION; }
+const char* wsc_last_error(void) { return g_err.c_str(); }
+
+int wsc_config_default(wsc_config* cfg) {
+    if (!cfg) return fail(WSC_E_INVAL, "cfg is NULL");
+    std::memset(cfg, 0, sizeof(*cfg));
+    cfg->max_batch_bytes = 64ull << 20;
+    cfg->max_segs = 1u << 16;
+    cfg->max_frames = 1u << 20;
+    cfg->max_frame_len = 0x7FFFFFFFull;
+    cfg->unmask_window = 4096;       // tools/tune_unmask.py, profiles/r01_tune_*.log
+    cfg->unmask_waves_per_cu = 0;    // 0: one window per wave (grid = windows)
+    cfg->unmask_nt = 3;              // non-temporal loads and stores
+    return WSC_OK;
+}
+
+static int alloc_host_path(wsc_ctx* c) {
+    if (c->d_wire) return WSC_OK;
+    const wsc_config& g = c->cfg;
+    HIP_TRY(hipMalloc(&c->d_wire, g.max_batch_bytes + 64));
+    HIP_TRY(hipMalloc(&c->d_arena, g.max_batch_bytes + 64));
+    HIP_TRY(hipMalloc(&c->d_seg_off, (g.max_segs + 1) * sizeof(uint64_t)));
+    HIP_TRY(hipMalloc(&c->d_state_in, g.max_segs * sizeof(wsc_conn_state)));
+    HIP_TRY(hipMalloc(&c->d_state_out, g.max_segs * sizeof(wsc_conn_state)));
+    HIP_TRY(hipMalloc(&c->d_seg_out, g.max_segs * sizeof(wsc_seg_result)));
+    HIP_TRY(hipMalloc(&c->d_frames, (uint64_t)g.max_frames * sizeof(wsc_frame)));
+    HIP_TRY(hipMalloc(&c->d_frame_dst, (uint64_t)g.max_frames * sizeof(uint64_t)));
+    HIP_TRY(hipMalloc(&c->d_summary, sizeof(wsc_summary)));
+    return WSC_OK;
+}
+
+int wsc_create(int device, const wsc_config* cfg_in, wsc_ctx** out) {
+    if (!out) return fail(WSC_E_INVAL, "out is NULL");
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+        return fail(WSC_E_NODEVICE, "no HIP device visible");
+    if (device < 0 || device >= ndev) return fail(WSC_E_INVAL, "device index out of range");
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(WSC_E_NODEVICE, std::string("libwscodec is built for gfx950, device is ") + prop.gcnArchName);
+    wsc_config cfg;
+    if (cfg_in) cfg = *cfg_in; else wsc_config_default(&cfg);
+    if (cfg.max_segs == 0 || cfg.max_frames == 0 || cfg.max_batch_bytes == 0)
+        return fail(WSC_E_INVAL, "zero capacity in config");
+    if (cfg.max_frame_len > 0xFFFFFFFFull) return fail(WSC_E_INVAL, "max_frame_len > 2^32-1");
+    uint32_t win = cfg.unmask_window ? cfg.unmask_window : 4096;
+    if (win != 4096 && win != 8192 && win != 16384) return fail(WSC_E_INVAL, "unmask_window must be 4096/8192/16384");
+    cfg.unmask_window = win;
+
+    HIP_TRY(hipSetDevice(device));
+    wsc_ctx* c = new wsc_ctx();
+    c->device = device;
+    c->n_cu = prop.multiProcessorCount;
+    c->cfg = cfg;
+    c->pieces = win / 1024;
+    int rc = WSC_OK;
+    auto chk = [&](hipError_t e, const char* what) {
+        if (e != hipSuccess && rc == WSC_OK) rc = fail(WSC_E_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
+    };
+    chk(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate");
+    chk(hipMalloc(&c->counts, cfg.max_segs * sizeof(SegCount)), "hipMalloc counts");
+    chk(hipMalloc(&c->bases, cfg.max_segs * sizeof(SegCount)), "hipMalloc bases");
+    chk(hipMalloc(&c->spans, (uint64_t)cfg.max_frames * sizeof(Span)), "hipMalloc spans");
+    c->tile_entries = cfg.max_batch_bytes / 1024 + 2;
+    chk(hipMalloc(&c->tile, c->tile_entries * sizeof(uint32_t)), "hipMalloc tile");
+    if (rc == WSC_OK) {
+        size_t bytes = 0;
+        SegCount init{};
+        chk(rocprim::exclusive_scan(nullptr, bytes, c->counts, c->bases, init, cfg.max_segs, SegCountAdd(),
+                                    c->stream),
+            "rocprim::exclusive_scan(size)");
+        c->scan_tmp_bytes = bytes;
+        chk(hipMalloc(&c->scan_tmp, bytes ? bytes : 16), "hipMalloc scan tmp");
+    }
+    if (rc != WSC_OK) {
+        wsc_destroy(c);
+        return rc;
+    }
+    *out = c;
+    return WSC_OK;
+}
+
+int wsc_destroy(wsc_ctx* c) {
+    if (!c) return WSC_OK;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    void* ptrs[] = {c->counts, c->bases, c->scan_tmp, c->spans, c->tile, c->d_wire, c->d_arena,
+                    c->d_seg_off, c->d_state_in, c->d_state_out, c->d_seg_out, c->d_frames,
+                    c->d_frame_dst, c->d_summary};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    return WSC_OK;
+}
+
+int wsc_dev_alloc(wsc_ctx* c, uint64_t bytes, void** out) {
+    if (!c || !out) return fail(WSC_E_INVAL, "NULL argument");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipMalloc(out, bytes ? bytes : 16));
+    return WSC_OK;
+}
+int wsc_dev_free(wsc_ctx* c, void* p) {
+    if (!c) return fail(WSC_E_INVAL, "NULL ctx");
+    HIP_TRY(hipSetDevice(c->device));
+    if (p) HIP_TRY(hipFree(p));
+    return WSC_OK;
+}
+int wsc_host_alloc(uint64_t bytes, void** out) {
+    if (!out) return fail(WSC_E_INVAL, "NULL out");
+    HIP_TRY(hipHostMalloc(out, bytes ? bytes : 16, hipHostMallocDefault));
+    return WSC_OK;
+}
+int wsc_host_free(void* p) {
+    if (p) HIP_TRY(hipHostFree(p));
+    return WSC_OK;
+}
+
+// The launch sequence.  `ev` (optional, 6 pairs) brackets each stage for wsc_profile.
+static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev) {
+    const bool compact = (b->flags & WSC_F_COMPACT) != 0;
+    const uint32_t n = b->n_segs;
+    if (n == 0) return fail(WSC_E_INVAL, "n_segs == 0");
+    if (n > c->cfg.max_segs) return fail(WSC_E_CAPACITY, "n_segs > max_segs");
+    if (b->n_bytes > c->cfg.max_batch_bytes) return fail(WSC_E_CAPACITY, "n_bytes > max_batch_bytes");
+    if (!b->wire || !b->seg_off || !b->state_out || !b->seg_out || !b->frames || !b->summary)
+        return fail(WSC_E_INVAL, "NULL batch pointer");
+    if (reinterpret_cast<uintptr_t>(b->wire) & 15) return fail(WSC_E_INVAL, "wire must be 16-byte aligned");
+    if (compact && (!b->arena || !b->frame_dst)) return fail(WSC_E_INVAL, "COMPACT needs arena + frame_dst");
+    if (compact && (reinterpret_cast<uintptr_t>(b->arena) & 15)) return fail(WSC_E_INVAL, "arena must be 16-byte aligned");
+
+    WalkArgs wa{};
+    wa.wire = b->wire;
+    wa.seg_off = b->seg_off;
+    wa.n_segs = n;
+    wa.frames_cap = b->frames_cap;
+    wa.state_in = b->state_in;
+    wa.max_frame_len = c->cfg.max_frame_len;
+    wa.counts = c->counts;
+    wa.bases = c->bases;
+    wa.frames = b->frames;
+    wa.spans = c->spans;
+    wa.spans_cap = c->cfg.max_frames;
+    wa.win_shift = ilog2(c->pieces * 1024);
+    wa.tile_first = c->tile;
+    wa.frame_dst = b->frame_dst;
+    wa.state_out = b->state_out;
+    wa.seg_out = b->seg_out;
+    wa.summary = b->summary;
+
+    const dim3 wblk(256), wgrid((n + 255) / 256);
+    auto rec = [&](int i) {
+        if (ev) (void)hipEventRecord(ev[i], st);
+    };
+    rec(0);
+    if (compact) hipLaunchKernelGGL((k_walk<false, true>), wgrid, wblk, 0, st, wa);
+    else hipLaunchKernelGGL((k_walk<false, false>), wgrid, wblk, 0, st, wa);
+    HIP_TRY(hipGetLastError());
+    rec(1);
+    size_t tb = c->scan_tmp_bytes;
+    SegCount init{};
+    HIP_TRY(rocprim::exclusive_scan(c->scan_tmp, tb, c->counts, c->bases, init, n, SegCountAdd(), st));
+    rec(2);
+    if (compact) hipLaunchKernelGGL((k_walk<true, true>), wgrid, wblk, 0, st, wa);
+    else hipLaunchKernelGGL((k_walk<true, false>), wgrid, wblk, 0, st, wa);
+    HIP_TRY(hipGetLastError());
+    rec(3);
+
+    uint8_t* udst = compact ? b->arena : b->wire;
+    const uint64_t udst_bytes = compact ? 0 : b->n_bytes;
+    const uint64_t wb = (uint64_t)c->pieces * 1024;
+    const uint64_t n_win = (b->n_bytes + wb - 1) / wb;
+    uint64_t waves = c->cfg.unmask_waves_per_cu ? (uint64_t)c->n_cu * c->cfg.unmask_waves_per_cu : n_win;
+    if (waves > n_win) waves = n_win;
+    if (waves == 0) waves = 1;
+    const dim3 ublk(256), ugrid((uint32_t)((waves + 3) / 4));
+    using UK = void (*)(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*,
+                        const wsc_summary*);
+    // [compact][pieces 4/8/16][nt 0..3]
+    static const UK table[2][3][4] = {
+        {{k_unmask<false, 4, 0>, k_unmask<false, 4, 1>, k_unmask<false, 4, 2>, k_unmask<false, 4, 3>},
+         {k_unmask<false, 8, 0>, k_unmask<false, 8, 1>, k_unmask<false, 8, 2>, k_unmask<false, 8, 3>},
+         {k_unmask<false, 16, 0>, k_unmask<false, 16, 1>, k_unmask<false, 16, 2>, k_unmask<false, 16, 3>}},
+        {{k_unmask<true, 4, 0>, k_unmask<true, 4, 1>, k_unmask<true, 4, 2>, k_unmask<true, 4, 3>},
+         {k_unmask<true, 8, 0>, k_unmask<true, 8, 1>, k_unmask<true, 8, 2>, k_unmask<true, 8, 3>},
+         {k_unmask<true, 16, 0>, k_unmask<true, 16, 1>, k_unmask<true, 16, 2>, k_unmask<true, 16, 3>}}};
+    const int pi = c->pieces == 4 ? 0 : (c->pieces == 8 ? 1 : 2);
+    const UK kern = table[compact ? 1 : 0][pi][c->cfg.unmask_nt & 3];
+    hipLaunchKernelGGL(kern, ugrid, ublk, 0, st, udst, (const uint8_t*)b->wire, b->n_bytes, udst_bytes,
+                       (const Span*)c->spans, (const uint32_t*)c->tile, (const wsc_summary*)b->summary);
+    HIP_TRY(hipGetLastError());
+    rec(4);
+
+    Utf8Args u8{};
+    u8.wire = b->wire;
+    u8.arena = b->arena;
+    u8.frame_dst = b->frame_dst;
+    u8.seg_off = b->seg_off;
+    u8.n_segs = n;
+    u8.counts = c->counts;
+    u8.state_in = b->state_in;
+    u8.frames = b->frames;
+    u8.state_out = b->state_out;
+    u8.seg_out = b->seg_out;
+    if (compact) hipLaunchKernelGGL((k_utf8<true>), wgrid, wblk, 0, st, u8);
+    else hipLaunchKernelGGL((k_utf8<false>), wgrid, wblk, 0, st, u8);
+    HIP_TRY(hipGetLastError());
+    rec(5);
+    return WSC_OK;
+}
+
+int wsc_decode(wsc_ctx* c, const wsc_batch* b, void* hip_stream) {
+    if (!c || !b) return fail(WSC_E_INVAL, "NULL argument");
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
+    return launch(c, b, st, nullptr);
+}
+
+int wsc_sync(wsc_ctx* c, void* hip_stream) {
+    if (!c) return fail(WSC_E_INVAL, "NULL ctx");
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
+    HIP_TRY(hipStreamSynchronize(st));
+    return WSC_OK;
+}
+
+int wsc_decode_host(wsc_ctx* c, uint8_t* wire, uint64_t n_bytes, const uint64_t* seg_off,
+                    uint32_t n_segs, uint32_t flags, const wsc_conn_state* state_in,
+                    wsc_conn_state* state_out, wsc_seg_result* seg_out, wsc_frame* frames,
+                    uint32_t frames_cap, uint8_t* arena, uint64_t* frame_dst, wsc_summary* summary) {
+    if (!c || !wire || !seg_off || !state_out || !seg_out || !frames || !summary)
+        return fail(WSC_E_INVAL, "NULL argument");
+    const bool compact = (flags & WSC_F_COMPACT) != 0;
+    if (compact && (!arena || !frame_dst)) return fail(WSC_E_INVAL, "COMPACT needs arena + frame_dst");
+    if (n_segs == 0 || n_segs > c->cfg.max_segs) return fail(WSC_E_CAPACITY, "n_segs out of range");
+    if (n_bytes > c->cfg.max_batch_bytes) return fail(WSC_E_CAPACITY, "n_bytes > max_batch_bytes");
+    HIP_TRY(hipSetDevice(c->device));
+    int rc = alloc_host_path(c);
+    if (rc) return rc;
+    const uint32_t cap = frames_cap < c->cfg.max_frames ? frames_cap : c->cfg.max_frames;
+    hipStream_t st = c->stream;
+    HIP_TRY(hipMemcpyAsync(c->d_wire, wire, n_bytes, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(c->d_seg_off, seg_off, (n_segs + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+    if (state_in)
+        HIP_TRY(hipMemcpyAsync(c->d_state_in, state_in, n_segs * sizeof(wsc_conn_state), hipMemcpyHostToDevice, st));
+    wsc_batch b{};
+    b.wire = c->d_wire;
+    b.n_bytes = n_bytes;
+    b.seg_off = c->d_seg_off;
+    b.n_segs = n_segs;
+    b.flags = flags;
+    b.state_in = state_in ? c->d_state_in : nullptr;
+    b.state_out = c->d_state_out;
+    b.seg_out = c->d_seg_out;
+    b.frames = c->d_frames;
+    b.frames_cap = cap;
+    b.arena = compact ? c->d_arena : nullptr;
+    b.frame_dst = compact ? c->d_frame_dst : nullptr;
+    b.summary = c->d_summary;
+    rc = launch(c, &b, st, nullptr);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(summary, c->d_summary, sizeof(wsc_summary), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    const uint32_t nf = summary->n_frames < cap ? summary->n_frames : cap;
+    HIP_TRY(hipMemcpyAsync(state_out, c->d_state_out, n_segs * sizeof(wsc_conn_state), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(seg_out, c->d_seg_out, n_segs * sizeof(wsc_seg_result), hipMemcpyDeviceToHost, st));
+    if (nf) HIP_TRY(hipMemcpyAsync(frames, c->d_frames, (uint64_t)nf * sizeof(wsc_frame), hipMemcpyDeviceToHost, st));
+    if (compact) {
+        const uint64_t ab = summary->data_bytes + summary->ctrl_bytes;
+        if (ab) HIP_TRY(hipMemcpyAsync(arena, c->d_arena, ab, hipMemcpyDeviceToHost, st));
+        if (nf) HIP_TRY(hipMemcpyAsync(frame_dst, c->d_frame_dst, (uint64_t)nf * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    } else if (n_bytes) {
+        HIP_TRY(hipMemcpyAsync(wire, c->d_wire, n_bytes, hipMemcpyDeviceToHost, st));
+    }
+    HIP_TRY(hipStreamSynchronize(st));
+    if (summary->overflow) return fail(WSC_E_CAPACITY, "frame capacity exceeded");
+    return WSC_OK;
+}
+
+int wsc_profile(wsc_ctx* c, const wsc_batch* b, int iters, double* out_ms) {
+    if (!c || !b || !out_ms || iters <= 0) return fail(WSC_E_INVAL, "bad argument");
+    HIP_TRY(hipSetDevice(c->device));
+    hipEvent_t ev[6];
+    for (auto& e : ev) HIP_TRY(hipEventCreate(&e));
+    double acc[6] = {0, 0, 0, 0, 0, 0};
+    int rc = WSC_OK;
+    for (int it = 0; it < iters && rc == WSC_OK; ++it) {
+        rc = launch(c, b, c->stream, ev);
+        if (rc) break;
+        if (hipStreamSynchronize(c->stream) != hipSuccess) { rc = fail(WSC_E_DEVICE, "sync"); break; }
+        for (int k = 0; k < 5; ++k) {
+            float ms = 0;
+            (void)hipEventElapsedTime(&ms, ev[k], ev[k + 1]);
+            acc[k] += ms;
+        }
+        float tot = 0;
+        (void)hipEventElapsedTime(&tot, ev[0], ev[5]);
+        acc[5] += tot;
+    }
+    for (auto& e : ev) (void)hipEventDestroy(e);
+    for (int k = 0; k < 6; ++k) out_ms[k] = acc[k] / iters;
+    return rc;
+}
+
+}  // extern "C"

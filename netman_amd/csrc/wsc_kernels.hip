@@ -1,0 +1,679 @@
+// wsc_kernels.hip -- gfx950 kernels of the WebSocket frame decoder.
+//
+//   k_walk<EMIT,COMPACT>  header walk + per-frame decode state machine, one lane per segment
+//                         (server/websocket.go:82-302, server/websocket_frame.go:13-103 minus the
+//                         byte loops).  Pass 1 counts, pass 2 (after an exclusive scan) emits
+//                         frame records, payload spans and the window->span index.
+//   k_unmask<COMPACT,P,NT> the hot loop (websocket_frame.go:35-39): XOR-unmask every payload span,
+//                         byte-tile decomposed, 16 B per lane access, 1 KiB per wave instruction.
+//   k_utf8                utf8.Valid for TEXT messages / control payloads / close reasons
+//                         (websocket_frame.go:71-73, websocket.go:170-172) and the fix-up of a
+//                         connection whose text turns out invalid (CloseCode 1007).
+#include "wsc_kernels.hpp"
+
+namespace wsc {
+
+__device__ __forceinline__ uint32_t rotr32(uint32_t x, uint32_t r) {
+    r &= 31;
+    return r ? (x >> r) | (x << (32 - r)) : x;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Header walk
+// ---------------------------------------------------------------------------------------------
+
+// close-code validity, websocket_ctrl.go:160-177 (+ reservedCode, websocket.go:31)
+__device__ __forceinline__ bool close_code_ok(uint32_t code) {
+    if (code < 1000 || code >= 5000) return false;
+    if (code >= 1016 && code <= 2999) return false;
+    if (code == 1004 || code == 1005 || code == 1006 || code == 1015) return false;
+    return true;
+}
+
+template <bool EMIT, bool COMPACT>
+__global__ __launch_bounds__(256) void k_walk(WalkArgs a) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= a.n_segs) return;
+    const uint8_t* __restrict__ w = a.wire;
+    const uint64_t seg_start = a.seg_off[s];
+    const uint64_t seg_end = a.seg_off[s + 1];
+
+    wsc_conn_state st = {};
+    if (a.state_in) st = a.state_in[s];
+    uint64_t cont = st.cont_len;
+    uint32_t msg = st.msg_id;
+    uint32_t mode = st.message_mode;
+    uint32_t status = st.status;
+    uint32_t close_code = 0, err_out = 0;
+
+    SegCount base = {}, tot = {};
+    if constexpr (EMIT) {
+        base = a.bases[s];
+        tot = SegCountAdd()(a.bases[a.n_segs - 1], a.counts[a.n_segs - 1]);
+    }
+    uint32_t nf = 0, ns0 = 0, ns1 = 0, sflags = 0;
+    uint64_t nb0 = 0, nb1 = 0;
+
+    // window->span index bookkeeping (EMIT): next window start not yet assigned, per region
+    const uint64_t W = 1ull << a.win_shift;
+    uint64_t nx0 = 0, nx1 = 0;
+    if constexpr (EMIT) {
+        if constexpr (COMPACT) {
+            nx0 = (base.bytes0 + W - 1) & ~(W - 1);
+            nx1 = (tot.bytes0 + base.bytes1 + W - 1) & ~(W - 1);
+        } else {
+            nx0 = (seg_start + W - 1) & ~(W - 1);
+        }
+    }
+
+    uint64_t pos = seg_start;
+    while (status == WSC_SEG_OPEN) {
+        const uint64_t avail = seg_end - pos;
+        if (avail < 2) break;
+        // speculative header read: the longest masked header is 14 bytes
+        uint32_t h[14];
+#pragma unroll
+        for (int k = 0; k < 14; ++k) h[k] = (k < (int64_t)avail) ? (uint32_t)w[pos + k] : 0u;
+        const uint32_t fin = h[0] >> 7;
+        const uint32_t rsv = (h[0] >> 4) & 7;
+        const uint32_t op = h[0] & 0xF;
+        const uint32_t masked = h[1] >> 7;
+        const uint32_t len7 = h[1] & 0x7F;
+
+        wsc_frame fr;
+        fr.hdr_off = pos;
+        fr.payload_len = 0;
+        fr.mask = 0;
+        fr.seg = s;
+        fr.msg_id = msg;
+        fr.opcode = (uint8_t)op;
+        fr.fin = (uint8_t)fin;
+        fr.kind = WSC_FK_ERROR;
+        fr.mode = (uint8_t)mode;
+        fr.err = 0;
+        fr.hdr_len = 2;
+        fr.flags = 0;
+        fr.pad = 0;
+
+        bool emit_rec = true;
+        uint64_t next = pos;
+        bool have_span = false;
+        uint32_t region = 0;
+        uint64_t plen = 0;
+
+        if (rsv) {  // websocket.go:229-231, checked as soon as the 2 bytes are in
+            fr.err = WSC_ERR_RSV_FAIL;
+            status = WSC_SEG_ERROR; close_code = 1002; err_out = WSC_ERR_RSV_FAIL;
+            next = pos + 2;
+        } else {
+            const uint32_t mode_h = (op == 1 || op == 2) ? op : mode;   // :234-236
+            fr.mode = (uint8_t)mode_h;
+            const uint32_t ext = len7 == 126 ? 2 : (len7 == 127 ? 8 : 0);
+            if (avail < 2 + ext) break;                                  // wait for the length
+            if (ext == 2) plen = (h[2] << 8) | h[3];
+            else if (ext == 8) {
+                plen = 0;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) plen = (plen << 8) | h[2 + k];
+            } else plen = len7;
+            if (!masked) {  // Q3: the reference never completes this header
+                fr.kind = WSC_FK_STALL;
+                fr.hdr_len = (uint8_t)(2 + ext);
+                status = WSC_SEG_STALLED;
+                next = pos + 2 + ext;
+            } else {
+                const uint32_t hl = 2 + ext + 4;
+                if (avail < hl) break;                                   // wait for the mask
+                uint32_t mask = 0;
+                if (ext == 0) mask = h[2] | h[3] << 8 | h[4] << 16 | h[5] << 24;
+                else if (ext == 2) mask = h[4] | h[5] << 8 | h[6] << 16 | h[7] << 24;
+                else mask = h[10] | h[11] << 8 | h[12] << 16 | h[13] << 24;
+                fr.hdr_len = (uint8_t)hl;
+                fr.mask = mask;
+                fr.payload_len = (uint32_t)plen;
+                const uint64_t pstart = pos + hl;
+
+                // opcode switch, websocket.go:136-208
+                uint32_t e = 0, kind = WSC_FK_ERROR;
+                bool payload = false;
+                if (op == 0) {
+                    if (mode_h < 1) e = WSC_ERR_OPCODE_FAIL;
+                    else { payload = true; kind = fin ? WSC_FK_MESSAGE : WSC_FK_FRAG; }
+                } else if (op == 1 || op == 2) {
+                    if (cont >= 1) e = WSC_ERR_PING_PAYLOAD_OVERSIZE;
+                    else { payload = true; kind = fin ? WSC_FK_MESSAGE : WSC_FK_FRAG; }
+                } else if (op == 8) {
+                    if (!(plen == 0 || plen >= 2) || plen > 125) e = WSC_ERR_PROTOCOL_ERROR;
+                    else if (plen == 0) kind = WSC_FK_CLOSE;
+                    else { payload = true; kind = fin ? WSC_FK_CLOSE : WSC_FK_FRAG; }
+                } else if (op == 9) {
+                    if (fin != 1) e = WSC_ERR_CTRL_FRAGMENTED;
+                    else if (plen > 125) e = WSC_ERR_PING_PAYLOAD_OVERSIZE;     // ctrl.go:130-132
+                    else { payload = true; kind = WSC_FK_PING; }
+                } else if (op == 10) {
+                    if (fin != 1) e = WSC_ERR_CTRL_FRAGMENTED;
+                    else if (plen == 0) kind = WSC_FK_PONG_EMPTY;
+                    else { payload = true; kind = WSC_FK_PONG; }
+                } else {
+                    e = WSC_ERR_OPCODE_FAIL;
+                }
+                if (payload && !e) {
+                    if (plen > a.max_frame_len) e = WSC_ERR_TOO_LARGE;          // Q4
+                    else if (avail < hl + plen) break;                           // wait for payload
+                }
+                next = pstart + (payload && !e ? plen : 0);
+                if (e) {
+                    fr.err = (uint8_t)e;
+                    status = WSC_SEG_ERROR; close_code = 1002; err_out = e;
+                    next = pstart;
+                } else {
+                    fr.kind = (uint8_t)kind;
+                    if (payload) fr.flags |= WSC_FF_UNMASKED;
+                    const bool text = mode_h == 1;
+                    if (kind == WSC_FK_MESSAGE) {                                // frame.go:52-91
+                        const bool cmsg = (op == 0 && cont >= 1);
+                        if (cmsg) { fr.flags |= WSC_FF_CONT_MSG; cont = 0; }
+                        if (text) fr.flags |= cmsg ? WSC_FF_U8_CHAIN : WSC_FF_U8_SELF;
+                        mode = 0;                                                // op is 0/1/2
+                        msg += 1;
+                    } else if (kind == WSC_FK_FRAG) {                            // frame.go:92-99
+                        if (text) fr.flags |= WSC_FF_U8_PART;
+                        cont += plen;
+                        mode = mode_h;
+                    } else if (kind == WSC_FK_PING || kind == WSC_FK_PONG) {
+                        if (text) fr.flags |= WSC_FF_U8_SELF;                    // Q6
+                        msg += 1;                                                // Q5
+                        region = 1;
+                    } else if (kind == WSC_FK_CLOSE) {                           // :153-183
+                        region = 1;
+                        if (payload) {
+                            if (plen > 2) fr.flags |= WSC_FF_U8_REASON;
+                            const uint32_t code = (((uint32_t)w[pstart] ^ (mask & 0xFF)) << 8) |
+                                                  ((uint32_t)w[pstart + 1] ^ ((mask >> 8) & 0xFF));
+                            if (!close_code_ok(code)) {
+                                fr.kind = WSC_FK_ERROR;
+                                fr.err = WSC_ERR_PROTOCOL_ERROR;
+                                status = WSC_SEG_ERROR; close_code = 1002;
+                                err_out = WSC_ERR_PROTOCOL_ERROR;
+                            }
+                        }
+                        if (status == WSC_SEG_OPEN) { status = WSC_SEG_CLOSED; close_code = 1000; }
+                    } else if (kind == WSC_FK_PONG_EMPTY) {
+                        status = WSC_SEG_CLOSED; close_code = 1000;
+                    }
+                    have_span = payload && plen > 0;
+                }
+            }
+        }
+
+        if (fr.flags & (WSC_FF_U8_PART | WSC_FF_U8_SELF | WSC_FF_U8_CHAIN | WSC_FF_U8_REASON))
+            sflags |= SEGF_UTF8;
+        if constexpr (COMPACT) if (region) fr.flags |= WSC_FF_CTRL_ARENA;
+
+        if (emit_rec) {
+            if constexpr (EMIT) {
+                const uint32_t fi = base.frames + nf;
+                if (fi < a.frames_cap) {
+                    a.frames[fi] = fr;
+                    if constexpr (COMPACT) {
+                        uint64_t d = ~0ull;
+                        if (fr.flags & WSC_FF_UNMASKED)
+                            d = region ? tot.bytes0 + base.bytes1 + nb1 : base.bytes0 + nb0;
+                        a.frame_dst[fi] = d;
+                    }
+                }
+                if (have_span) {
+                    Span sp;
+                    sp.src = pos + fr.hdr_len;
+                    sp.len = (uint32_t)plen;
+                    uint32_t idx;
+                    if constexpr (COMPACT) {
+                        if (region) {
+                            sp.dst = tot.bytes0 + base.bytes1 + nb1;
+                            idx = tot.spans0 + base.spans1 + ns1;
+                        } else {
+                            sp.dst = base.bytes0 + nb0;
+                            idx = base.spans0 + ns0;
+                        }
+                    } else {
+                        sp.dst = sp.src;
+                        idx = base.spans0 + ns0;
+                    }
+                    sp.key = rotr32(fr.mask, 8u * ((uint32_t)(0u - (uint32_t)sp.dst) & 3u));
+                    if (idx < a.spans_cap) a.spans[idx] = sp;
+                    const uint64_t dend = sp.dst + plen;
+                    uint64_t& nx = (COMPACT && region) ? nx1 : nx0;
+                    while (nx < dend) {
+                        a.tile_first[nx >> a.win_shift] = idx;
+                        nx += W;
+                    }
+                }
+            }
+            nf += 1;
+            if (have_span) {
+                if (COMPACT && region) { ns1 += 1; nb1 += plen; }
+                else { ns0 += 1; nb0 += plen; }
+            }
+        }
+        pos = next;
+    }
+
+    if constexpr (!EMIT) {
+        SegCount c;
+        c.frames = nf; c.spans0 = ns0; c.spans1 = ns1; c.flags = sflags;
+        c.bytes0 = nb0; c.bytes1 = nb1;
+        a.counts[s] = c;
+    } else {
+        // windows that start in this segment's region(s) after its last span
+        if constexpr (COMPACT) {
+            const uint64_t e0 = base.bytes0 + nb0, e1 = tot.bytes0 + base.bytes1 + nb1;
+            for (; nx0 < e0; nx0 += W) a.tile_first[nx0 >> a.win_shift] = base.spans0 + ns0;
+            for (; nx1 < e1; nx1 += W) a.tile_first[nx1 >> a.win_shift] = tot.spans0 + base.spans1 + ns1;
+        } else {
+            for (; nx0 < seg_end; nx0 += W) a.tile_first[nx0 >> a.win_shift] = base.spans0 + ns0;
+        }
+        wsc_seg_result r;
+        r.consumed = pos - seg_start;
+        r.frame_begin = base.frames;
+        r.frame_count = nf;
+        r.status = status;
+        r.close_code = close_code;
+        r.err = err_out;
+        r.pad = 0;
+        a.seg_out[s] = r;
+        wsc_conn_state o;
+        o.cont_len = cont;
+        o.msg_id = msg;
+        o.message_mode = (uint8_t)mode;
+        o.cont_utf8 = cont ? st.cont_utf8 : 0;   // k_utf8 recomputes it for TEXT chains
+        o.status = (uint8_t)status;
+        o.pad = 0;
+        a.state_out[s] = o;
+        if (s == a.n_segs - 1) {
+            wsc_summary sm;
+            sm.data_bytes = COMPACT ? tot.bytes0 : 0;
+            sm.ctrl_bytes = COMPACT ? tot.bytes1 : 0;
+            sm.n_frames = tot.frames;
+            sm.n_spans = tot.spans0 + tot.spans1;
+            sm.overflow = (tot.frames > a.frames_cap || tot.spans0 + tot.spans1 > a.spans_cap) ? 1u : 0u;
+            sm.pad = 0;
+            *a.summary = sm;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Unmask: the hot loop.  The destination byte range is cut into windows of P KiB; wave w owns
+// window w (grid-stride).  tile_first[w] names the first span whose destination ends after the
+// window start, so the wave walks only the spans that overlap its window (scalar loads).  Each
+// lane holds P pieces of 16 B at dst + w*W + k*1024 + lane*16: every wave instruction touches
+// 1 KiB contiguous.  For each overlapping span a lane ORs the span's rotated mask word into the
+// bytes of its pieces that the span covers, then XORs and stores once.
+// ---------------------------------------------------------------------------------------------
+
+__device__ __forceinline__ uint32_t bytes_to_mask(uint32_t lo, uint32_t hi) {
+    // byte lanes [lo, hi) of a dword, lo <= hi <= 4
+    const uint32_t a = lo >= 4 ? 0u : (0xFFFFFFFFu << (8 * lo));
+    const uint32_t b = hi >= 4 ? 0xFFFFFFFFu : ~(0xFFFFFFFFu << (8 * hi));
+    return a & b;
+}
+
+// 16 bytes starting at src + off (off may be unaligned); bytes outside [0, n) read as 0
+__device__ __forceinline__ uint4 load16_unaligned(const uint8_t* __restrict__ src, int64_t off,
+                                                  uint64_t n) {
+    const int64_t c0 = off & ~(int64_t)15;
+    const uint32_t sh = (uint32_t)(off - c0);
+    uint4 v0 = make_uint4(0, 0, 0, 0), v1 = make_uint4(0, 0, 0, 0);
+    if (c0 >= 0 && (uint64_t)c0 + 16 <= n) v0 = *reinterpret_cast<const uint4*>(src + c0);
+    else {
+        uint32_t t[4] = {0, 0, 0, 0};
+        for (int j = 0; j < 16; ++j) {
+            const int64_t q = c0 + j;
+            if (q >= 0 && (uint64_t)q < n) t[j >> 2] |= (uint32_t)src[q] << (8 * (j & 3));
+        }
+        v0 = make_uint4(t[0], t[1], t[2], t[3]);
+    }
+    if (sh == 0) return v0;
+    const int64_t c1 = c0 + 16;
+    if (c1 >= 0 && (uint64_t)c1 + 16 <= n) v1 = *reinterpret_cast<const uint4*>(src + c1);
+    else {
+        uint32_t t[4] = {0, 0, 0, 0};
+        for (int j = 0; j < 16; ++j) {
+            const int64_t q = c1 + j;
+            if (q >= 0 && (uint64_t)q < n) t[j >> 2] |= (uint32_t)src[q] << (8 * (j & 3));
+        }
+        v1 = make_uint4(t[0], t[1], t[2], t[3]);
+    }
+    const uint32_t d[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+    const uint32_t q = sh >> 2, rb = sh & 3;
+    uint32_t o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        // select dwords q+j and q+j+1 without dynamic register indexing
+        uint32_t lo = d[j], hi = d[j + 1];
+        if (q == 1) { lo = d[j + 1]; hi = d[j + 2]; }
+        else if (q == 2) { lo = d[j + 2]; hi = d[j + 3]; }
+        else if (q == 3) { lo = d[j + 3]; hi = d[j + 4]; }
+        o[j] = __builtin_amdgcn_alignbyte(hi, lo, rb);
+    }
+    return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+template <int NT>
+__device__ __forceinline__ u32x4 ld16v(const uint8_t* p) {
+    if constexpr (NT & 1) return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    else return *reinterpret_cast<const u32x4*>(p);
+}
+template <int NT>
+__device__ __forceinline__ void st16v(uint8_t* p, u32x4 v) {
+    if constexpr (NT & 2) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
+    else *reinterpret_cast<u32x4*>(p) = v;
+}
+template <int NT>
+__device__ __forceinline__ uint4 ld16(const uint8_t* p) {
+    const u32x4 t = ld16v<NT>(p);
+    return make_uint4(t.x, t.y, t.z, t.w);
+}
+template <int NT>
+__device__ __forceinline__ void st16(uint8_t* p, uint4 v) {
+    u32x4 t = {v.x, v.y, v.z, v.w};
+    st16v<NT>(p, t);
+}
+
+// General window: several spans overlap it (small frames), or it is the last, partial window.
+// Builds a per-byte key from every span that overlaps each 16-byte piece.
+template <bool COMPACT, int P, int NT>
+__device__ __attribute__((noinline)) void unmask_window_general(
+    uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, uint64_t src_bytes, uint64_t total,
+    const Span* __restrict__ spans, uint32_t n_spans, uint32_t r, uint64_t wbase, uint32_t lofs) {
+    constexpr uint32_t WB = 1024u * P;
+    uint4 v[P], key[P];
+    uint32_t cov[P];
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+        key[k] = make_uint4(0, 0, 0, 0);
+        cov[k] = 0;
+        v[k] = make_uint4(0, 0, 0, 0);
+        if constexpr (!COMPACT) {
+            const uint64_t addr = wbase + k * 1024u + lofs;
+            if (addr + 16 <= total) v[k] = ld16<NT>(dst + addr);
+        }
+    }
+    for (; r < n_spans; ++r) {
+        const Span sp = spans[r];
+        if (sp.dst >= wbase + WB) break;
+        const uint64_t d0 = sp.dst, d1 = sp.dst + sp.len;
+#pragma unroll
+        for (int k = 0; k < P; ++k) {
+            const uint64_t pa = wbase + k * 1024u + lofs;
+            const uint64_t lo = d0 > pa ? d0 : pa;
+            const uint64_t hi = d1 < pa + 16 ? d1 : pa + 16;
+            if (lo < hi) {
+                const uint32_t bl = (uint32_t)(lo - pa), bh = (uint32_t)(hi - pa);
+                uint32_t m[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const uint32_t l = bl > 4u * j ? bl - 4u * j : 0u;
+                    const uint32_t hh = bh > 4u * j ? bh - 4u * j : 0u;
+                    m[j] = l < hh ? bytes_to_mask(l, hh > 4 ? 4 : hh) : 0u;
+                }
+                key[k].x |= sp.key & m[0];
+                key[k].y |= sp.key & m[1];
+                key[k].z |= sp.key & m[2];
+                key[k].w |= sp.key & m[3];
+                cov[k] |= 1u;
+                if constexpr (COMPACT) {
+                    const int64_t so = (int64_t)sp.src + ((int64_t)pa - (int64_t)sp.dst);
+                    const uint4 sv = load16_unaligned(src, so, src_bytes);
+                    v[k].x |= sv.x & m[0];
+                    v[k].y |= sv.y & m[1];
+                    v[k].z |= sv.z & m[2];
+                    v[k].w |= sv.w & m[3];
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+        if (!cov[k]) continue;
+        const uint64_t addr = wbase + k * 1024u + lofs;
+        uint4 o = v[k];
+        o.x ^= key[k].x; o.y ^= key[k].y; o.z ^= key[k].z; o.w ^= key[k].w;
+        if (COMPACT || addr + 16 <= total) {
+            st16<NT>(dst + addr, o);
+        } else {
+            // in-place tail piece past the last full 16 B of the buffer: byte stores
+            const uint32_t kd[4] = {key[k].x, key[k].y, key[k].z, key[k].w};
+            for (uint32_t j = 0; addr + j < total; ++j)
+                dst[addr + j] ^= (uint8_t)(kd[j >> 2] >> (8 * (j & 3)));
+        }
+    }
+}
+
+// NT bit 0: non-temporal loads, bit 1: non-temporal stores.  In place, `src` is unused (dst is
+// both source and destination) so the two restrict pointers never alias in an access.
+template <bool COMPACT, int P, int NT>
+__global__ __launch_bounds__(256) void k_unmask(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src,
+                                                uint64_t src_bytes, uint64_t dst_bytes_host,
+                                                const Span* __restrict__ spans,
+                                                const uint32_t* __restrict__ tile_first,
+                                                const wsc_summary* __restrict__ summary) {
+    constexpr uint32_t WB = 1024u * P;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t waves_per_block = blockDim.x >> 6;
+    const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * waves_per_block + (threadIdx.x >> 6));
+    const uint32_t nw = gridDim.x * waves_per_block;
+    const uint64_t total = COMPACT ? summary->data_bytes + summary->ctrl_bytes : dst_bytes_host;
+    const uint32_t n_spans = summary->n_spans;
+    const uint64_t n_win = (total + WB - 1) / WB;
+    const uint32_t lofs = lane * 16u;
+    if (n_spans == 0) return;
+
+    for (uint64_t win = gw; win < n_win; win += nw) {
+        const uint64_t wbase = win * WB;
+        if (wbase + WB > total) {   // the last, partial window
+            const uint32_t r = tile_first[win];
+            unmask_window_general<COMPACT, P, NT>(dst, src, src_bytes, total, spans, n_spans, r, wbase, lofs);
+            continue;
+        }
+        u32x4 v[P];
+        if constexpr (!COMPACT) {
+            // in place the loads do not depend on the span lookup: issue them first
+#pragma unroll
+            for (int k = 0; k < P; ++k) v[k] = ld16v<NT>(dst + wbase + k * 1024u + lofs);
+        }
+        uint32_t r = tile_first[win];
+        Span sp = spans[r < n_spans ? r : n_spans - 1];
+        if (r >= n_spans) sp.dst = ~0ull;   // no span starts before the window's end
+        if (sp.dst <= wbase && sp.dst + sp.len >= wbase + WB) {
+            // fast path: one span covers the whole window -> one rotated key for every dword
+            if constexpr (COMPACT) {
+                const int64_t so = (int64_t)sp.src - (int64_t)sp.dst;
+#pragma unroll
+                for (int k = 0; k < P; ++k) {
+                    const uint4 t = load16_unaligned(src, so + (int64_t)(wbase + k * 1024u + lofs), src_bytes);
+                    v[k] = u32x4{t.x, t.y, t.z, t.w};
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < P; ++k) {
+                v[k] ^= sp.key;
+                st16v<NT>(dst + wbase + k * 1024u + lofs, v[k]);
+            }
+            continue;
+        }
+        // several spans overlap the window (small frames) or it holds a frame edge
+        u32x4 key[P];
+        uint32_t cov = 0;
+#pragma unroll
+        for (int k = 0; k < P; ++k) {
+            key[k] = u32x4{0, 0, 0, 0};
+            if constexpr (COMPACT) v[k] = u32x4{0, 0, 0, 0};
+        }
+        while (sp.dst < wbase + WB) {
+            const uint64_t d0 = sp.dst, d1 = sp.dst + sp.len;
+#pragma unroll
+            for (int k = 0; k < P; ++k) {
+                const uint64_t pa = wbase + k * 1024u + lofs;
+                const uint64_t lo = d0 > pa ? d0 : pa;
+                const uint64_t hi = d1 < pa + 16 ? d1 : pa + 16;
+                if (lo < hi) {
+                    const uint32_t bl = (uint32_t)(lo - pa), bh = (uint32_t)(hi - pa);
+                    uint32_t m[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const uint32_t l = bl > 4u * j ? bl - 4u * j : 0u;
+                        const uint32_t hh = bh > 4u * j ? bh - 4u * j : 0u;
+                        m[j] = l < hh ? bytes_to_mask(l, hh > 4 ? 4 : hh) : 0u;
+                    }
+                    key[k].x |= sp.key & m[0];
+                    key[k].y |= sp.key & m[1];
+                    key[k].z |= sp.key & m[2];
+                    key[k].w |= sp.key & m[3];
+                    cov |= 1u << k;
+                    if constexpr (COMPACT) {
+                        const int64_t so = (int64_t)sp.src + ((int64_t)pa - (int64_t)sp.dst);
+                        const uint4 sv = load16_unaligned(src, so, src_bytes);
+                        v[k].x |= sv.x & m[0];
+                        v[k].y |= sv.y & m[1];
+                        v[k].z |= sv.z & m[2];
+                        v[k].w |= sv.w & m[3];
+                    }
+                }
+            }
+            if (++r >= n_spans) break;
+            sp = spans[r];
+        }
+#pragma unroll
+        for (int k = 0; k < P; ++k)
+            if (cov & (1u << k)) st16v<NT>(dst + wbase + k * 1024u + lofs, v[k] ^ key[k]);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// UTF-8 (Go utf8.Valid semantics): a 9-state DFA, state 0 = between characters, 8 = reject.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t u8_step(uint32_t s, uint32_t b) {
+    switch (s) {
+    case 0:
+        if (b < 0x80) return 0;
+        if (b >= 0xC2 && b <= 0xDF) return 1;
+        if (b == 0xE0) return 4;
+        if (b == 0xED) return 5;
+        if (b >= 0xE1 && b <= 0xEF) return 2;
+        if (b == 0xF0) return 6;
+        if (b >= 0xF1 && b <= 0xF3) return 3;
+        if (b == 0xF4) return 7;
+        return 8;
+    case 1: return (b >= 0x80 && b <= 0xBF) ? 0 : 8;
+    case 2: return (b >= 0x80 && b <= 0xBF) ? 1 : 8;
+    case 3: return (b >= 0x80 && b <= 0xBF) ? 2 : 8;
+    case 4: return (b >= 0xA0 && b <= 0xBF) ? 1 : 8;
+    case 5: return (b >= 0x80 && b <= 0x9F) ? 1 : 8;
+    case 6: return (b >= 0x90 && b <= 0xBF) ? 2 : 8;
+    case 7: return (b >= 0x80 && b <= 0x8F) ? 2 : 8;
+    default: return 8;
+    }
+}
+
+__device__ uint32_t u8_run(uint32_t s, const uint8_t* p, uint64_t n) {
+    uint64_t i = 0;
+    while (i < n && s != 8) {
+        if (s == 0 && (((uintptr_t)(p + i)) & 3) == 0 && i + 4 <= n) {
+            const uint32_t wv = *reinterpret_cast<const uint32_t*>(p + i);
+            if ((wv & 0x80808080u) == 0) { i += 4; continue; }
+        }
+        s = u8_step(s, p[i]);
+        ++i;
+    }
+    return s;
+}
+
+template <bool COMPACT>
+__global__ __launch_bounds__(256) void k_utf8(Utf8Args a) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= a.n_segs) return;
+    if (!(a.counts[s].flags & SEGF_UTF8)) return;
+    wsc_seg_result r = a.seg_out[s];
+    uint32_t dfa = 0;
+    if (a.state_in && a.state_in[s].cont_len) dfa = a.state_in[s].cont_utf8;
+    int64_t fail = -1;
+    for (uint32_t i = r.frame_begin; i < r.frame_begin + r.frame_count; ++i) {
+        const wsc_frame f = a.frames[i];
+        const uint8_t* p = COMPACT ? a.arena + a.frame_dst[i] : a.wire + f.hdr_off + f.hdr_len;
+        bool ok = true;
+        if (f.flags & WSC_FF_U8_PART) {
+            dfa = u8_run(dfa, p, f.payload_len);
+        } else if (f.flags & WSC_FF_U8_CHAIN) {
+            ok = u8_run(dfa, p, f.payload_len) == 0;
+        } else if (f.flags & WSC_FF_U8_SELF) {
+            ok = u8_run(0, p, f.payload_len) == 0;
+        } else if (f.flags & WSC_FF_U8_REASON) {
+            ok = u8_run(0, p + 2, f.payload_len - 2) == 0;
+        }
+        if (f.flags & WSC_FF_CONT_MSG) dfa = 0;   // continueBuffer consumed (frame.go:62-68)
+        if (!ok) { fail = i; break; }
+    }
+    wsc_conn_state o = a.state_out[s];
+    if (fail >= 0) {
+        wsc_frame f = a.frames[fail];
+        f.kind = WSC_FK_ERROR;
+        f.err = WSC_ERR_MUST_UTF8;
+        a.frames[fail] = f;
+        const uint32_t end = r.frame_begin + r.frame_count;
+        if constexpr (!COMPACT) {
+            // frames after the failing one were never reached by the reference: re-mask them
+            for (uint32_t j = (uint32_t)fail + 1; j < end; ++j) {
+                const wsc_frame g = a.frames[j];
+                if (!(g.flags & WSC_FF_UNMASKED)) continue;
+                uint8_t* q = a.wire + g.hdr_off + g.hdr_len;
+                for (uint32_t b = 0; b < g.payload_len; ++b) q[b] ^= (uint8_t)(g.mask >> (8 * (b & 3)));
+            }
+        }
+        r.frame_count = (uint32_t)fail - r.frame_begin + 1;
+        r.consumed = f.hdr_off + f.hdr_len + f.payload_len - a.seg_off[s];
+        r.status = WSC_SEG_ERROR;
+        r.close_code = 1007;
+        r.err = WSC_ERR_MUST_UTF8;
+        a.seg_out[s] = r;
+        o.status = WSC_SEG_ERROR;
+    } else {
+        o.cont_utf8 = o.cont_len ? (uint8_t)dfa : 0;
+    }
+    a.state_out[s] = o;
+}
+
+// explicit instantiations used by the host code
+template __global__ void k_walk<false, false>(WalkArgs);
+template __global__ void k_walk<true, false>(WalkArgs);
+template __global__ void k_walk<false, true>(WalkArgs);
+template __global__ void k_walk<true, true>(WalkArgs);
+template __global__ void k_unmask<false, 4, 0>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*);
+template __global__ void k_unmask<false, 4, 1>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*);
+template __global__ void k_unmask<false, 4, 2>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*);
+template __global__ void k_unmask<false, 4, 3>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*);
+template __global__ void k_unmask<false, 8, 0>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*);
+template __global__ void k_unmask<false, 8, 1>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*);
+template __global__ void k_unmask<false, 8, 2>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*);
+template __global__ void k_unmask<false, 8, 3>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*);
+template __global__ void k_unmask<false, 16, 0>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*);
+template __global__ void k_unmask<false, 16, 1>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*);
+template __global__ void k_unmask<false, 16, 2>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*);
+template __global__ void k_unmask<false, 16, 3>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*);
+template __global__ void k_unmask<true, 4, 0>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*);
+template __global__ void k_unmask<true, 4, 1>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*);
+template __global__ void k_unmask<true, 4, 2>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*);
+template __global__ void k_unmask<true, 4, 3>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*);
+template __global__ void k_unmask<true, 8, 0>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*);
+template __global__ void k_unmask<true, 8, 1>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*);
+template __global__ void k_unmask<true, 8, 2>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*);
+template __global__ void k_unmask<true, 8, 3>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*);
+template __global__ void k_unmask<true, 16, 0>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*);
+template __global__ void k_unmask<true, 16, 1>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*);
+template __global__ void k_unmask<true, 16, 2>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*);
+template __global__ void k_unmask<true, 16, 3>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*);
+template __global__ void k_utf8<false>(Utf8Args);
+template __global__ void k_utf8<true>(Utf8Args);
+
+}  // namespace wsc

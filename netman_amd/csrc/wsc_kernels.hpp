@@ -1,0 +1,80 @@
+// wsc_kernels.hpp -- device-side types shared by the gfx950 kernels and the host launch code.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "../../include/wscodec.h"
+
+namespace wsc {
+
+// Per-segment counts produced by the header walk; the exclusive scan of these gives each
+// segment its slice of every output array.  In-place mode uses only frames/spans0/flags.
+struct SegCount {
+    uint32_t frames;   // frame records
+    uint32_t spans0;   // payload spans (in-place: all; COMPACT: data region)
+    uint32_t spans1;   // COMPACT: control-region spans
+    uint32_t flags;    // SEGF_*
+    uint64_t bytes0;   // COMPACT: data-region bytes
+    uint64_t bytes1;   // COMPACT: control-region bytes
+};
+
+struct SegCountAdd {
+    __host__ __device__ SegCount operator()(const SegCount& a, const SegCount& b) const {
+        SegCount r;
+        r.frames = a.frames + b.frames;
+        r.spans0 = a.spans0 + b.spans0;
+        r.spans1 = a.spans1 + b.spans1;
+        r.flags = a.flags | b.flags;
+        r.bytes0 = a.bytes0 + b.bytes0;
+        r.bytes1 = a.bytes1 + b.bytes1;
+        return r;
+    }
+};
+
+enum : uint32_t { SEGF_UTF8 = 1u };
+
+// One contiguous run of masked payload bytes to XOR: source in the wire, destination either the
+// same bytes (in place) or the arena (COMPACT).  `key` is the mask word rotated so that it XORs
+// 4-byte-aligned destination dwords directly: key = rotr(mask, 8 * ((-dst) & 3)).
+struct Span {
+    uint64_t src;
+    uint64_t dst;
+    uint32_t len;
+    uint32_t key;
+};
+static_assert(sizeof(Span) == 24, "span layout");
+
+struct WalkArgs {
+    const uint8_t* wire;
+    const uint64_t* seg_off;
+    uint32_t n_segs;
+    uint32_t frames_cap;
+    const wsc_conn_state* state_in;
+    uint64_t max_frame_len;
+    SegCount* counts;
+    const SegCount* bases;
+    wsc_frame* frames;
+    Span* spans;
+    uint32_t spans_cap;
+    uint32_t win_shift;          // log2(unmask window bytes)
+    uint32_t* tile_first;        // per window: first span whose dst end > window start
+    uint64_t* frame_dst;         // COMPACT
+    wsc_conn_state* state_out;
+    wsc_seg_result* seg_out;
+    wsc_summary* summary;
+};
+
+
+struct Utf8Args {
+    uint8_t* wire;
+    const uint8_t* arena;        // COMPACT
+    const uint64_t* frame_dst;   // COMPACT
+    const uint64_t* seg_off;
+    uint32_t n_segs;
+    const SegCount* counts;
+    const wsc_conn_state* state_in;
+    wsc_frame* frames;
+    wsc_conn_state* state_out;
+    wsc_seg_result* seg_out;
+};
+
+}  // namespace wsc

@@ -1,0 +1,132 @@
+"""Seeded random client->server streams for parity tests (test infrastructure).
+
+Each stream is one connection's post-handshake bytes: mostly well-formed traffic (single-frame
+text/binary, fragmented chains incl. 0-length fragments and multi-byte characters split across
+fragments, PING/PONG interleaved) with a small per-frame chance of the things the reference
+rejects or mishandles (RSV bits, reserved opcodes, CONT without a start, TEXT inside a chain,
+oversize/fragmented control frames, bad close codes / reasons, invalid UTF-8, unmasked frames,
+non-minimal length encodings, empty PONG).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from netman_amd.synth import frame, OP_CONT, OP_TEXT, OP_BIN, OP_CLOSE, OP_PING, OP_PONG
+
+_SAMPLE_TEXT = ["hello", "netman", "Grüße", "日本語テキスト", "emoji 😀🎉", "ασδφ", "a" * 40,
+                "mixed ✓ ✗ ← → ß", ""]
+
+
+def _rand_text(rng, n_max=200):
+    parts = []
+    while sum(len(p.encode()) for p in parts) < rng.integers(0, n_max + 1):
+        parts.append(_SAMPLE_TEXT[rng.integers(len(_SAMPLE_TEXT))])
+        if len(parts) > 50:
+            break
+    return "".join(parts).encode("utf-8")
+
+
+def _bad_utf8(rng):
+    bads = [b"\xff", b"\xc0\x80", b"\xed\xa0\x80", b"\xe2\x82", b"\xf4\x90\x80\x80", b"\x80", b"\xf8\x88\x80\x80\x80"]
+    good = _rand_text(rng, 40)
+    cut = int(rng.integers(0, len(good) + 1))
+    # keep the cut on a character boundary so the only error is the injected one
+    while cut < len(good) and (good[cut] & 0xC0) == 0x80:
+        cut += 1
+    return good[:cut] + bads[rng.integers(len(bads))] + good[cut:]
+
+
+def _payload(rng, big_p=0.02):
+    r = rng.random()
+    if r < big_p:
+        n = int(rng.choice([65535, 65536, 70000]))
+    elif r < 0.1:
+        n = int(rng.choice([0, 1, 2, 3, 4, 5, 125, 126, 127, 255, 256]))
+    else:
+        n = int(rng.integers(0, 300))
+    return rng.bytes(n)
+
+
+def _ctrl_payload(rng, hi):
+    """control payloads: mostly ASCII (valid utf8, so Q6 rarely fires), sometimes random bytes"""
+    n = int(rng.integers(0, hi))
+    if rng.random() < 0.85:
+        return bytes(rng.integers(0x20, 0x7F, n, dtype=np.uint8))
+    return rng.bytes(n)
+
+
+def _ext_for(rng, n):
+    """mostly minimal; sometimes a non-minimal (but legal to the reference) length encoding"""
+    if rng.random() < 0.05:
+        return 8 if n > 125 or rng.random() < 0.5 else 2
+    return None
+
+
+def random_stream(seed: int, n_units: int = 20, err_p: float = 0.03, big_p: float = 0.02,
+                  text_p: float = 0.3) -> bytes:
+    rng = np.random.default_rng(seed)
+    out = bytearray()
+
+    def F(op, payload=b"", fin=True, masked=True, rsv=0, ext=None):
+        if ext is None:
+            ext = _ext_for(rng, len(payload))
+            if ext == 2 and len(payload) > 65535:
+                ext = 8
+        out.extend(frame(op, payload, fin=fin, mask=int(rng.integers(0, 2**32)), masked=masked,
+                         rsv=rsv, ext=ext))
+
+    for _ in range(n_units):
+        r = rng.random()
+        if r < err_p:  # something the reference rejects / mishandles
+            kind = int(rng.integers(0, 12))
+            if kind == 0: F(OP_BIN, b"x", rsv=int(rng.integers(1, 8)))
+            elif kind == 1: F(int(rng.choice([3, 4, 5, 6, 7, 11, 12, 13, 14, 15])), b"zz")
+            elif kind == 2: F(OP_CONT, b"orphan")
+            elif kind == 3: F(OP_PING, rng.bytes(126))
+            elif kind == 4: F(OP_PING, b"p", fin=False)
+            elif kind == 5: F(OP_CLOSE, b"\x03")
+            elif kind == 6: F(OP_CLOSE, (int(rng.choice([999, 1004, 1005, 1006, 1015, 1016, 2999, 5000]))).to_bytes(2, "big") + b"bye")
+            elif kind == 7: F(OP_CLOSE, (1000).to_bytes(2, "big") + _bad_utf8(rng))
+            elif kind == 8: F(OP_TEXT, _bad_utf8(rng))
+            elif kind == 9: F(OP_BIN, b"unmasked", masked=False)
+            elif kind == 10: F(OP_PONG, b"")
+            else: F(OP_PONG, b"x", fin=False)
+            continue
+        if r < 0.10:
+            F(OP_PING, _ctrl_payload(rng, 126))
+        elif r < 0.15:
+            F(OP_PONG, _ctrl_payload(rng, 200) or b"x")
+        elif r < 0.45:  # fragmented message
+            text = rng.random() < text_p
+            if text:
+                body = _rand_text(rng, 300)
+                if rng.random() < 0.02:
+                    body = _bad_utf8(rng)
+            else:
+                body = _payload(rng, big_p)
+            nfr = int(rng.integers(2, 6))
+            cuts = sorted(int(x) for x in rng.integers(0, len(body) + 1, nfr - 1))
+            pieces = [body[a:b] for a, b in zip([0] + cuts, cuts + [len(body)])]
+            for i, pc in enumerate(pieces):
+                F(OP_TEXT if (i == 0 and text) else (OP_BIN if i == 0 else OP_CONT), pc,
+                  fin=(i == len(pieces) - 1))
+                if i < len(pieces) - 1 and rng.random() < 0.15:
+                    F(OP_PING, _ctrl_payload(rng, 20))
+                if i < len(pieces) - 1 and rng.random() < 0.01:
+                    F(OP_CLOSE, (1000).to_bytes(2, "big") + b"frag", fin=False)   # Q7 quirk
+        else:
+            if rng.random() < text_p:
+                F(OP_TEXT, _rand_text(rng, 200))
+            else:
+                F(OP_BIN, _payload(rng, big_p))
+        if rng.random() < 0.005:
+            F(OP_CLOSE, b"" if rng.random() < 0.5 else (1000).to_bytes(2, "big") + b"done")
+    return bytes(out)
+
+
+def random_splits(rng, n: int, k: int):
+    """k random cut points in (0, n) -> increasing chunk ends ending at n"""
+    if n == 0:
+        return [0]
+    cuts = sorted(set(int(x) for x in rng.integers(1, max(n, 2), k))) if k else []
+    return [c for c in cuts if 0 < c < n] + [n]

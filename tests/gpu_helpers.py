@@ -1,0 +1,70 @@
+"""Shared checks for the GPU parity tests: device records vs the oracle's frame log."""
+from __future__ import annotations
+
+import numpy as np
+
+import oracle_ref as O
+from netman_amd import codec as K
+
+
+def pack_streams(streams):
+    """concatenate streams as segments (16 B-aligned buffer start)"""
+    lens = [len(s) for s in streams]
+    off = np.zeros(len(streams) + 1, dtype=np.uint64)
+    np.cumsum(lens, out=off[1:])
+    wire = np.frombuffer(b"".join(streams), dtype=np.uint8).copy() if sum(lens) else np.zeros(0, np.uint8)
+    return wire, off
+
+
+def compare_segment(si, stream, seg_start, res: K.DecodeResult, ora: O.OracleOut, wire_after=None,
+                    compact=False, check_state=True):
+    sr = res.seg[si]
+    fb, fc = int(sr["frame_begin"]), int(sr["frame_count"])
+    fr = res.frames[fb:fb + fc]
+    of = ora.frames
+    assert fc == len(of), f"seg {si}: {fc} device frames vs {len(of)} oracle frames\n{fr}\n{of}"
+    for i in range(fc):
+        d, o = fr[i], of[i]
+        ctx = f"seg {si} frame {i}: dev={d} ora={o}"
+        assert int(d["hdr_off"]) - seg_start == int(o["hdr_off"]), ctx
+        for f in ("kind", "opcode", "fin", "mode", "msg_id"):
+            assert int(d[f]) == int(o[f]), f + " " + ctx
+        assert int(d["err"]) == int(o["err"]), "err " + ctx
+        if int(d["kind"]) != K.FK_STALL and int(d["err"]) != K.ERR_RSV_FAIL:
+            assert int(d["payload_len"]) == int(o["payload_len"]), ctx
+            assert int(d["mask"]) == int(o["mask"]), ctx
+            assert int(d["hdr_off"]) + int(d["hdr_len"]) - seg_start == int(o["payload_off"]), ctx
+    # terminal status
+    r = ora.res
+    if r["closed"]:
+        assert int(sr["status"]) in (K.SEG_CLOSED, K.SEG_ERROR), f"seg {si} status {sr}"
+        assert int(sr["close_code"]) == r["close_code"], f"seg {si} {sr} vs {r}"
+        assert int(sr["err"]) == r["err"], f"seg {si} {sr} vs {r}"
+    elif r["stalled"]:
+        assert int(sr["status"]) == K.SEG_STALLED, f"seg {si} {sr}"
+    else:
+        assert int(sr["status"]) == K.SEG_OPEN, f"seg {si} {sr} vs {r}"
+        if check_state and int(sr["consumed"]) == len(stream):   # no partial frame pending
+            st = res.state[si]
+            assert int(st["msg_id"]) == r["msg_id"], f"seg {si} {st} vs {r}"
+            assert int(st["message_mode"]) == r["message_mode"], f"seg {si} {st} vs {r}"
+            assert int(st["cont_len"]) == r["cont_len"], f"seg {si} {st} vs {r}"
+    # payload bytes
+    ref = np.frombuffer(ora.inplace, dtype=np.uint8)
+    if not compact:
+        got = wire_after[seg_start:seg_start + len(stream)]
+        if not np.array_equal(got, ref):
+            bad = np.nonzero(got != ref)[0]
+            raise AssertionError(f"seg {si}: in-place bytes differ at {bad[:10]} (n={len(bad)})")
+    else:
+        for i in range(fc):
+            d = fr[i]
+            if int(d["flags"]) & K.FF_UNMASKED and int(d["payload_len"]):
+                p = int(d["hdr_off"]) + int(d["hdr_len"]) - seg_start
+                L = int(d["payload_len"])
+                dst = int(res.frame_dst[fb + i])
+                assert np.array_equal(res.arena[dst:dst + L], ref[p:p + L]), f"seg {si} frame {i} arena"
+
+
+def events_of_session(sess, conn):
+    return [(e.type, e.msg_id, e.opcode, e.close_code, e.err, e.data) for e in sess.events(conn)]

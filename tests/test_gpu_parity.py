@@ -1,0 +1,160 @@
+"""GPU parity: libwscodec (HIP, gfx950) against the CPU oracle on the same inputs.
+
+Bit-exact for everything (integer/byte work): frame records, unmasked payload bytes, statuses,
+carried state, delivered events.
+"""
+import numpy as np
+import pytest
+
+import oracle_ref as O
+from fuzz_streams import random_stream, random_splits
+from gpu_helpers import pack_streams, compare_segment, events_of_session
+from netman_amd import codec as K
+from netman_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+HELLO = bytes.fromhex("818537fa213d7f9f4d5158")        # RFC 6455 §5.7 masked "Hello"
+PONG_HELLO = bytes.fromhex("8a8537fa213d7f9f4d5158")   # RFC 6455 §5.7 masked Pong "Hello"
+
+
+@pytest.fixture(scope="module")
+def codec(codec_lib):
+    c = K.Codec(0, max_batch_bytes=64 << 20, max_segs=1 << 14, max_frames=1 << 18)
+    yield c
+    c.close()
+
+
+def _check_batch(codec, streams, compact=False, max_frame_len=0x7FFFFFFF):
+    wire, off = pack_streams(streams)
+    orig = wire.copy()
+    res = codec.decode_host(wire, off, compact=compact)
+    assert int(res.summary["overflow"]) == 0
+    for i, s in enumerate(streams):
+        ora = O.run(s, max_frame_len=max_frame_len)
+        compare_segment(i, s, int(off[i]), res, ora, wire_after=wire, compact=compact)
+    if compact:
+        assert np.array_equal(wire, orig), "COMPACT mode must not modify the wire"
+    return res
+
+
+def test_rfc6455_known_answers(codec):
+    streams = [HELLO, PONG_HELLO + HELLO, HELLO * 3]
+    wire, off = pack_streams(streams)
+    res = _check_batch(codec, streams)
+    f = res.frames
+    assert int(f[0]["kind"]) == K.FK_MESSAGE and int(f[0]["payload_len"]) == 5
+    assert int(f[0]["mask"]) == 0x3D21FA37 and int(f[0]["mode"]) == 1
+    # frame 2 (after the masked PONG, which takes msgID 0 -- Q5) is MsgID 1
+    assert int(f[1]["kind"]) == K.FK_PONG and int(f[2]["msg_id"]) == 1
+
+
+def test_rfc6455_unmasked_examples_stall(codec):
+    # §5.7 single-frame unmasked text and fragmented unmasked text: netman never completes them (Q3)
+    res = _check_batch(codec, [bytes.fromhex("810548656c6c6f"), bytes.fromhex("010348656c80026c6f")])
+    assert [int(x) for x in res.seg["status"]] == [K.SEG_STALLED, K.SEG_STALLED]
+
+
+@pytest.mark.parametrize("compact", [False, True])
+def test_fuzz_single_batch(codec, compact):
+    streams = [random_stream(1000 + i, n_units=int(5 + i % 40)) for i in range(400)]
+    _check_batch(codec, streams, compact=compact)
+
+
+def test_fuzz_text_heavy(codec):
+    streams = [random_stream(5000 + i, n_units=30, text_p=0.9, err_p=0.02) for i in range(300)]
+    _check_batch(codec, streams)
+
+
+def test_edge_lengths(codec):
+    streams = []
+    for n in [0, 1, 2, 3, 4, 5, 15, 16, 17, 125, 126, 127, 1023, 1024, 1025, 65535, 65536, 65537, 1 << 20]:
+        streams.append(synth.frame(2, bytes(np.random.default_rng(n).bytes(n)), mask=0xDEADBEEF))
+        streams.append(synth.frame(2, b"\x00" * n, mask=0))
+        streams.append(synth.frame(2, b"\xff" * n, mask=0xFFFFFFFF, ext=8))
+    streams.append(b"")
+    streams.append(b"\x82")                         # incomplete header
+    streams.append(synth.frame(2, b"abc")[:-1])     # incomplete payload
+    _check_batch(codec, streams)
+
+
+def test_max_frame_len(codec_lib):
+    c = K.Codec(0, max_batch_bytes=8 << 20, max_segs=64, max_frames=4096, max_frame_len=1000)
+    streams = [synth.frame(2, b"a" * 1000), synth.frame(2, b"a" * 1001), synth.frame(10, b"b" * 5000),
+               synth.frame(1, b"ok") + synth.frame(2, b"c" * 70000)]
+    wire, off = pack_streams(streams)
+    res = c.decode_host(wire, off)
+    for i, s in enumerate(streams):
+        compare_segment(i, s, int(off[i]), res, O.run(s, max_frame_len=1000), wire_after=wire)
+    assert int(res.seg[1]["err"]) == K.ERR_TOO_LARGE
+    c.close()
+
+
+@pytest.mark.parametrize("compact", [False, True])
+def test_session_carry_over(codec_lib, compact):
+    """streams fed in random chunks across several batched decodes == oracle on the whole stream"""
+    rng = np.random.default_rng(7)
+    sess = K.Session(0, compact=compact, max_batch_bytes=16 << 20, max_segs=1024, max_frames=1 << 16)
+    streams = [random_stream(9000 + i, n_units=25) for i in range(120)]
+    conns = [sess.open() for _ in streams]
+    splits = [random_splits(rng, len(s), int(rng.integers(0, 6))) for s in streams]
+    got = {c: [] for c in conns}
+    rounds = max(len(sp) for sp in splits)
+    prev = [0] * len(streams)
+    for r in range(rounds):
+        for i, (c, s, sp) in enumerate(zip(conns, streams, splits)):
+            if r < len(sp):
+                sess.feed(c, s[prev[i]:sp[r]])
+                prev[i] = sp[r]
+        sess.decode()
+        for c in conns:
+            got[c].extend(events_of_session(sess, c))
+    for i, (c, s) in enumerate(zip(conns, streams)):
+        ref = [e.key() for e in O.run(s).events]
+        assert got[c] == ref, f"stream {i}: {got[c][:5]} vs {ref[:5]}"
+    sess.close()
+
+
+def test_decode_packet_mirror(codec_lib):
+    sess = K.Session(0, max_batch_bytes=1 << 20, max_segs=16, max_frames=1024)
+    c = sess.open()
+    sess.feed(c, HELLO + synth.frame(9, b"ping!") + synth.frame(0x2, b"\x01\x02", fin=True)
+              + synth.frame(1, b"\xff"))
+    sess.decode()
+    m, err = sess.DecodePacket(c)
+    assert err is None and m.IsText() and m.Bytes() == b"Hello" and m.ID() == 0
+    m, err = sess.DecodePacket(c)          # PING answered -> (nil, nil)
+    assert m is None and err is None
+    m, err = sess.DecodePacket(c)
+    assert m.IsBinary() and m.ID() == 2    # the PING consumed msgID 1 (Q5)
+    m, err = sess.DecodePacket(c)
+    assert m is None and err is K.WebsocketMustUtf8 and K.close_code_for(err) == 1007
+    m, err = sess.DecodePacket(c)
+    assert err is K.EAGAIN
+    sess.close()
+
+
+def test_device_resident_uniform_64k(codec_lib):
+    torch = pytest.importorskip("torch")
+    cfg = synth.uniform_batch(1024, 65536, 4, seed=synth.SEED_BASE + 99)
+    c = K.Codec(0, max_batch_bytes=128 << 20, max_segs=4096, max_frames=1 << 16)
+    dev = torch.device("cuda:0")
+    wire = torch.from_numpy(cfg["wire"]).to(dev)
+    seg_off = torch.from_numpy(cfg["seg_off"].view(np.int64)).to(dev)
+    n = len(cfg["seg_off"]) - 1
+    st_out = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
+    seg_out = torch.zeros(n * 32, dtype=torch.uint8, device=dev)
+    frames = torch.zeros((1 << 16) * 32, dtype=torch.uint8, device=dev)
+    summ = torch.zeros(32, dtype=torch.uint8, device=dev)
+    b = c.make_batch(wire, seg_off, None, st_out, seg_out, frames, summ)
+    c.decode(b)
+    c.sync()
+    ref = synth.unmask_reference(cfg["wire"], cfg["payload_off"], cfg["plen"], cfg["mask"])
+    assert np.array_equal(wire.cpu().numpy(), ref)
+    # XOR is an involution: a second decode restores the masked bytes exactly
+    c.decode(b)
+    c.sync()
+    assert np.array_equal(wire.cpu().numpy(), cfg["wire"])
+    fr = frames.cpu().numpy().view(K.FRAME_DTYPE)[:1024]
+    assert (fr["kind"] == K.FK_MESSAGE).all() and (fr["msg_id"] == np.tile(np.arange(4), 256)).all()
+    c.close()
