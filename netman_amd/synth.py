@@ -177,3 +177,19 @@ def frame(op, payload: bytes = b"", fin=True, mask=None, masked=True, rsv=0, ext
     else:
         out += payload
     return bytes(out)
+
+
+def unmask_uniform(cfg):
+    """vectorised websocket_frame.go:35-39 for batches whose frames all have one payload size"""
+    plen = cfg["plen"]
+    P = int(plen[0])
+    assert (plen == P).all() and P % 4 == 0
+    n = len(plen)
+    wire = cfg["wire"]
+    stride = len(wire) // n
+    hdr = stride - P
+    out = wire.copy().reshape(n, stride)
+    mb = cfg["mask"].view(np.uint8).reshape(n, 1, 4)
+    pay = out[:, hdr:].reshape(n, P // 4, 4)
+    pay ^= mb
+    return out.reshape(-1)

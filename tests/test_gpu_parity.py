@@ -158,3 +158,120 @@ def test_device_resident_uniform_64k(codec_lib):
     fr = frames.cpu().numpy().view(K.FRAME_DTYPE)[:1024]
     assert (fr["kind"] == K.FK_MESSAGE).all() and (fr["msg_id"] == np.tile(np.arange(4), 256)).all()
     c.close()
+
+
+# ---- golden fixtures through the device path --------------------------------------------------
+def test_golden_known_answers_gpu(codec_lib):
+    from golden_io import kat_cases, event_matches
+    cases = kat_cases()
+    sess = K.Session(0, max_batch_bytes=4 << 20, max_segs=64, max_frames=4096)
+    conns = []
+    for _, stream, _ in cases:
+        c = sess.open()
+        sess.feed(c, stream)
+        conns.append(c)
+    sess.decode()
+    for (name, _, expect), c in zip(cases, conns):
+        evs = sess.events(c)
+        assert len(evs) == len(expect), (name, evs)
+        for e, ev in zip(expect, evs):
+            assert event_matches(e, ev), (name, e, ev)
+    sess.close()
+
+
+@pytest.mark.parametrize("compact", [False, True])
+def test_golden_aiohttp_streams_gpu(codec, compact):
+    from golden_io import aiohttp_cases
+    streams = [s for _, s, _ in aiohttp_cases()]
+    _check_batch(codec, streams, compact=compact)
+
+
+# ---- BASELINE.json configs at full size (size-independent properties + vectorised reference) --
+def _device_batch(c, cfg, torch, compact=False):
+    dev = torch.device("cuda:0")
+    n = len(cfg["seg_off"]) - 1
+    t = dict(wire=torch.from_numpy(cfg["wire"]).to(dev),
+             seg_off=torch.from_numpy(cfg["seg_off"].view(np.int64)).to(dev),
+             st_out=torch.zeros(n * 16, dtype=torch.uint8, device=dev),
+             seg_out=torch.zeros(n * 32, dtype=torch.uint8, device=dev),
+             frames=torch.zeros((cfg["n_frames"] + 16) * 32, dtype=torch.uint8, device=dev),
+             summ=torch.zeros(32, dtype=torch.uint8, device=dev))
+    if compact:
+        t["arena"] = torch.zeros(len(cfg["wire"]) + 64, dtype=torch.uint8, device=dev)
+        t["frame_dst"] = torch.zeros(cfg["n_frames"] + 16, dtype=torch.int64, device=dev)
+    b = c.make_batch(t["wire"], t["seg_off"], None, t["st_out"], t["seg_out"], t["frames"], t["summ"],
+                     compact=compact, arena=t.get("arena"), frame_dst=t.get("frame_dst"))
+    return b, t
+
+
+def test_config1_1m_x_1k_frames(codec_lib):
+    torch = pytest.importorskip("torch")
+    cfg = synth.uniform_batch(1 << 20, 1024, 16, seed=synth.SEED_BASE + 1)
+    c = K.Codec(0, max_batch_bytes=len(cfg["wire"]) + 4096, max_segs=1 << 16, max_frames=(1 << 20) + 16)
+    b, t = _device_batch(c, cfg, torch)
+    c.decode(b)
+    c.sync()
+    assert np.array_equal(t["wire"].cpu().numpy(), synth.unmask_uniform(cfg))
+    fr = t["frames"].cpu().numpy().view(K.FRAME_DTYPE)[: 1 << 20]
+    assert (fr["kind"] == K.FK_MESSAGE).all() and (fr["hdr_len"] == 8).all()
+    c.close()
+
+
+def test_config2_mixed_power_law(codec_lib):
+    torch = pytest.importorskip("torch")
+    cfg = synth.mixed_batch()
+    c = K.Codec(0, max_batch_bytes=len(cfg["wire"]) + 4096, max_segs=1 << 15, max_frames=cfg["n_frames"] + 16)
+    b, t = _device_batch(c, cfg, torch)
+    c.decode(b)
+    c.sync()
+    ref = synth.unmask_reference(cfg["wire"], cfg["payload_off"], cfg["plen"], cfg["mask"])
+    assert np.array_equal(t["wire"].cpu().numpy(), ref)
+    c.close()
+
+
+def test_config3_shard_1m_x_4k_frames(codec_lib):
+    """one GPU's shard of configs[3] (8M x 4 KiB over 8 GPUs): 1M frames, 4 GiB payload"""
+    torch = pytest.importorskip("torch")
+    from netman_amd import shard
+    cfg = synth.uniform_batch(1 << 20, 4096, 16, seed=shard.shard_seed(synth.SEED_BASE + 3, 0))
+    c = K.Codec(0, max_batch_bytes=len(cfg["wire"]) + 4096, max_segs=1 << 16, max_frames=(1 << 20) + 16)
+    b, t = _device_batch(c, cfg, torch)
+    c.decode(b)
+    c.sync()
+    assert np.array_equal(t["wire"].cpu().numpy(), synth.unmask_uniform(cfg))
+    c.decode(b)                      # involution: decoding again restores the masked wire
+    c.sync()
+    assert np.array_equal(t["wire"].cpu().numpy(), cfg["wire"])
+    c.close()
+
+
+@pytest.mark.parametrize("ping_p", [0.0, 0.1])
+def test_config4_fragmented_reassembly(codec_lib, ping_p):
+    """configs[4]: 64k connections x one fragmented message, reassembled contiguously (COMPACT)"""
+    torch = pytest.importorskip("torch")
+    cfg = synth.fragmented_batch(n_conns=65536, seed=synth.SEED_BASE + 4, ping_p=ping_p)
+    c = K.Codec(0, max_batch_bytes=len(cfg["wire"]) + 4096, max_segs=1 << 16, max_frames=cfg["n_frames"] + 16)
+    b, t = _device_batch(c, cfg, torch, compact=True)
+    c.decode(b)
+    c.sync()
+    assert np.array_equal(t["wire"].cpu().numpy(), cfg["wire"])      # COMPACT leaves the wire alone
+    fr = t["frames"].cpu().numpy().view(K.FRAME_DTYPE)[: cfg["n_frames"]]
+    dst = t["frame_dst"].cpu().numpy()[: cfg["n_frames"]].view(np.uint64)
+    arena = t["arena"].cpu().numpy()
+    segr = t["seg_out"].cpu().numpy().view(K.SEG_RESULT_DTYPE)
+    ref = synth.unmask_reference(cfg["wire"], cfg["payload_off"], cfg["plen"], cfg["mask"])
+    data_frames = fr["kind"] != K.FK_PING
+    assert (segr["status"] == K.SEG_OPEN).all() and (fr["kind"][data_frames] != K.FK_ERROR).all()
+    # each connection's message is contiguous in the data region, in connection order
+    msg_end = np.nonzero(fr["kind"] == K.FK_MESSAGE)[0]
+    assert len(msg_end) == 65536
+    expect = np.concatenate([ref[int(p):int(p) + int(L)] for p, L, k in
+                             zip(cfg["payload_off"], cfg["plen"], fr["kind"]) if k != K.FK_PING])
+    sm = t["summ"].cpu().numpy().view(K.SUMMARY_DTYPE)[0]
+    assert int(sm["data_bytes"]) == len(expect)
+    assert np.array_equal(arena[: len(expect)], expect)
+    # control payloads (PINGs) land in the control region, unmasked
+    for i in np.nonzero(fr["kind"] == K.FK_PING)[0][:2000]:
+        p, L = int(cfg["payload_off"][i]), int(cfg["plen"][i])
+        assert np.array_equal(arena[int(dst[i]):int(dst[i]) + L], ref[p:p + L])
+    c.close()

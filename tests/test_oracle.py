@@ -1,0 +1,113 @@
+"""CPU tests of the oracle: pinned against the golden vectors, and the reference quirks it must
+reproduce.  No GPU."""
+import numpy as np
+import pytest
+
+import oracle_ref as O
+from fuzz_streams import random_stream
+from golden_io import kat_cases, aiohttp_cases, event_matches, data_matches
+from netman_amd.synth import frame
+
+
+@pytest.mark.parametrize("name,stream,expect", kat_cases(), ids=[c[0] for c in kat_cases()])
+def test_rfc6455_known_answers(name, stream, expect):
+    evs = O.run(stream).events
+    assert len(evs) == len(expect), (name, evs)
+    for e, ev in zip(expect, evs):
+        assert event_matches(e, ev), (name, e, ev)
+
+
+@pytest.mark.parametrize("seed,stream,expect", aiohttp_cases(), ids=[str(c[0]) for c in aiohttp_cases()])
+def test_against_aiohttp_reader(seed, stream, expect):
+    """independent decoder (aiohttp 3.14.3 reader_py) on valid streams: same data messages and
+    PING payloads (netman answers each PING with a PONG echo), in order; MsgIDs follow Q5"""
+    evs = O.run(stream).events
+    got = [(("MESSAGE", e.opcode) if e.type == O.EV_MESSAGE else ("PONG", None), e.data)
+           for e in evs if e.type in (O.EV_MESSAGE, O.EV_PONG)]
+    assert len(got) == len(expect)
+    for (k, op, enc), ((gk, gop), data) in zip(expect, got):
+        assert k == gk and (op is None or op == gop) and data_matches(enc, data)
+    # msgID counts every FIN frame that passed nextFrame (data messages and PINGs here)
+    assert [e.msg_id for e in evs if e.type == O.EV_MESSAGE] == sorted(e.msg_id for e in evs if e.type == O.EV_MESSAGE)
+
+
+def test_utf8_valid_matches_python():
+    rng = np.random.default_rng(3)
+    samples = [b"", b"abc", "Grüße 日本 😀".encode(), b"\xed\xa0\x80", b"\xc0\x80", b"\xf4\x90\x80\x80",
+               b"\xf4\x8f\xbf\xbf", b"\xe0\x9f\xbf", b"\xe0\xa0\x80", b"\xef\xbf\xbf", b"\xc2", b"\xf0\x90\x80"]
+    for _ in range(3000):
+        n = int(rng.integers(0, 12))
+        samples.append(bytes(rng.integers(0x80, 0x100, n, dtype=np.uint8)) if rng.random() < 0.5 else rng.bytes(n))
+    for b in samples:
+        try:
+            b.decode("utf-8")
+            py = True
+        except UnicodeDecodeError:
+            py = False
+        assert O.utf8_valid(b) == py, b
+
+
+def test_chunking_without_split_headers_is_invisible():
+    """level-triggered re-reads: any chunking that never cuts a header gives the same events"""
+    rng = np.random.default_rng(11)
+    for i in range(60):
+        s = random_stream(300 + i, n_units=20)
+        full = O.run(s)
+        # chunk ends inside payloads only: frame boundaries + payload offsets from the frame log
+        cands = []
+        for f in full.frames:
+            if f["payload_len"] > 1:
+                cands.append(int(f["payload_off"]) + int(rng.integers(1, int(f["payload_len"]))))
+        ends = sorted(set(cands)) + [len(s)]
+        part = O.run(s, chunk_ends=ends)
+        assert [e.key() for e in part.events] == [e.key() for e in full.events]
+
+
+def test_q1_split_extended_length_desyncs():
+    """Q1 (websocket.go:282-284): a 1-byte read of a 16-bit length returns nil and the stream
+    desyncs -- the batched codec instead waits for the whole header (documented divergence)"""
+    s = frame(2, b"x" * 200, mask=0x01020304) + frame(2, b"y", mask=5)
+    whole = O.run(s)
+    split = O.run(s, chunk_ends=[3, len(s)])   # cut inside the 2-byte extended length
+    assert [e.type for e in whole.events] == [O.EV_MESSAGE, O.EV_MESSAGE]
+    assert [e.key() for e in split.events] != [e.key() for e in whole.events]
+
+
+def test_q5_msgid_counts_control_frames():
+    s = frame(9, b"a", mask=1) + frame(10, b"b", mask=2) + frame(2, b"c", mask=3)
+    evs = O.run(s).events
+    assert [(e.type, e.msg_id) for e in evs] == [(O.EV_PONG, 0), (O.EV_MESSAGE, 2)]
+
+
+def test_q6_ping_payload_utf8_checked_inside_text_message():
+    s = frame(1, b"ab", fin=False, mask=1) + frame(9, b"\xff", mask=2) + frame(0, b"c", mask=3)
+    evs = O.run(s).events
+    assert [(e.type, e.close_code) for e in evs] == [(O.EV_CLOSE, 1007)]
+
+
+def test_q7_fragmented_close_joins_message():
+    s = (frame(2, b"ab", fin=False, mask=1) + frame(8, b"\x03\xe8zz", fin=False, mask=2) +
+         frame(0, b"c", mask=3))
+    evs = O.run(s).events
+    assert evs[0].type == O.EV_MESSAGE and evs[0].data == b"ab\x03\xe8zzc"
+
+
+def test_q8_empty_fragment_escapes_data_check():
+    s = frame(1, b"", fin=False, mask=1) + frame(2, b"bin", mask=2)
+    evs = O.run(s).events
+    assert [(e.type, e.opcode, e.data) for e in evs] == [(O.EV_MESSAGE, 2, b"bin")]
+
+
+def test_q3_unmasked_stalls_forever():
+    s = frame(2, b"ok", mask=1) + frame(2, b"nomask", masked=False) + frame(2, b"after", mask=2)
+    out = O.run(s)
+    assert [e.type for e in out.events] == [O.EV_MESSAGE, O.EV_STALL]
+    assert out.res["stalled"] == 1 and out.res["closed"] == 0
+
+
+def test_inplace_unmask_matches_restatement():
+    rng = np.random.default_rng(5)
+    data = rng.bytes(1000)
+    s = frame(2, data, mask=0xA1B2C3D4)
+    out = O.run(s)
+    assert out.inplace[8:] == data and out.inplace[:8] == s[:8]
