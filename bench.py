@@ -111,12 +111,12 @@ def main():
     # decode must equal the numpy restatement on a sample of frames)
     codec.decode(batch)
     codec.sync()
-    host = wire[: min(n_bytes, 64 * (a.frame_bytes + 14))].cpu().numpy()
+    host = wire[: min(n_bytes, 64 * (a.frame_bytes + 14))].cpu().numpy().copy()
     k = int(np.searchsorted(cfg["payload_off"] + cfg["plen"], len(host), side="right"))
     ref = synth.unmask_reference(cfg["wire"][: len(host)], cfg["payload_off"][:k], cfg["plen"][:k], cfg["mask"][:k])
     ok = bool(np.array_equal(host[: int(cfg["payload_off"][k - 1] + cfg["plen"][k - 1])],
                              ref[: int(cfg["payload_off"][k - 1] + cfg["plen"][k - 1])]))
-    summ_h = summ.cpu().numpy().view(K.SUMMARY_DTYPE)[0]
+    summ_h = summ.cpu().numpy().copy().view(K.SUMMARY_DTYPE)[0]
     ok = ok and int(summ_h["n_frames"]) == a.frames and int(summ_h["n_spans"]) == a.frames
 
     for _ in range(a.warmup):

@@ -75,8 +75,10 @@ extern "C" {
 #define WSC_SEG_STALLED 3   /* unmasked frame: nothing more is ever delivered (Q3)                  */
 
 /* batch flags */
-#define WSC_F_COMPACT 0x1   /* write unmasked payloads compacted into `arena` (messages contiguous)
-                               instead of unmasking the wire buffer in place                       */
+#define WSC_F_COMPACT 0x1   /* write unmasked payloads compacted into `arena` instead of unmasking
+                               the wire buffer in place.  Arena layout: segments in order, each as
+                               [data payloads (continuation chains contiguous)][control payloads]; a
+                               frame's payload is at frame_dst[i]                                  */
 
 /* Decoder state carried between batches for one connection (subset of websocket.go:38-56).   */
 typedef struct wsc_conn_state {
@@ -118,11 +120,12 @@ typedef struct wsc_seg_result {
 
 /* Batch totals written by the device.                                                          */
 typedef struct wsc_summary {
-    uint64_t data_bytes;   /* COMPACT: bytes in the data region of the arena                      */
-    uint64_t ctrl_bytes;   /* COMPACT: bytes in the control region (starts at data_bytes)         */
+    uint64_t data_bytes;   /* COMPACT: data payload bytes in the arena (all segments)            */
+    uint64_t ctrl_bytes;   /* COMPACT: control payload bytes in the arena                         */
     uint32_t n_frames;     /* frames in `frames`                                                  */
     uint32_t n_spans;      /* payload spans unmasked                                              */
-    uint32_t overflow;     /* 1 if n_frames > frames_cap (records beyond the cap were dropped)    */
+    uint32_t overflow;     /* bit0: n_frames > frames_cap (records beyond the cap were dropped);
+                              bit1: internal look-back timeout (results invalid)                  */
     uint32_t pad;
 } wsc_summary;
 
@@ -168,8 +171,9 @@ int wsc_dev_free(wsc_ctx* ctx, void* p);
 int wsc_host_alloc(uint64_t bytes, void** out);   /* pinned (hipHostMalloc) */
 int wsc_host_free(void* p);
 
-/* Enqueue the decode of one device-resident batch on `hip_stream` (hipStream_t, NULL = the
- * context's own stream).  Asynchronous: results are valid once the stream is synchronised. */
+/* Enqueue the decode of one device-resident batch on `hip_stream` (a hipStream_t; NULL = the
+ * default stream, as everywhere in HIP).  Asynchronous: results are valid once the stream is
+ * synchronised (wsc_sync with the same stream).  Inputs must be ready on that stream. */
 int wsc_decode(wsc_ctx* ctx, const wsc_batch* batch, void* hip_stream);
 int wsc_sync(wsc_ctx* ctx, void* hip_stream);
 
@@ -183,7 +187,8 @@ int wsc_decode_host(wsc_ctx* ctx, uint8_t* wire, uint64_t n_bytes, const uint64_
 
 /* Timing helper for the benchmark: run `iters` back-to-back decodes of a device batch and
  * return the per-kernel average device time (ms) measured with hipEvents on the launch stream.
- * out_ms[0..4] = walk(count), scan, walk(emit), unmask, utf8;  out_ms[5] = whole decode. */
+ * out_ms[0] = fused header walk, [1], [2] = 0 (reserved), [3] = unmask, [4] = utf8 pass,
+ * [5] = whole decode.  A context runs one decode at a time (its scratch is shared). */
 int wsc_profile(wsc_ctx* ctx, const wsc_batch* batch, int iters, double* out_ms);
 
 /* ---- session: the per-connection DecodePacket() mirror (C++ host side above the ABI) --------- */

@@ -112,6 +112,14 @@ def load_library(path: str = LIB_PATH):
         return _lib
     if not os.path.exists(path):
         raise OSError(f"libwscodec.so not built ({path}); run __graft_entry__.build()")
+    # One HIP runtime per process: torch wheels bundle their own libamdhip64.so (SONAME
+    # libamdhip64.so.7, the same as /opt/rocm's).  Loading torch first lets our DT_NEEDED resolve
+    # to that already-loaded runtime, so torch tensors and our kernels share one HIP/ROCr
+    # instance; without torch (C/Go hosts) the library uses /opt/rocm's runtime.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = C.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)
@@ -201,16 +209,33 @@ class Codec:
         b.summary = _ptr(summary)
         return b
 
+    @staticmethod
+    def _stream(stream):
+        """default to torch's current stream (0 = the null stream), so launches are ordered after
+        the torch ops that produced the batch tensors (fills, copies)"""
+        if stream is not None:
+            return stream
+        import sys
+        torch = sys.modules.get("torch")
+        if torch is not None and torch.cuda.is_initialized():
+            return torch.cuda.current_stream().cuda_stream or None
+        return None
+
     def decode(self, batch: WscBatch, stream=None):
-        _check(self.lib.wsc_decode(self.h, C.byref(batch), stream), "wsc_decode")
+        _check(self.lib.wsc_decode(self.h, C.byref(batch), self._stream(stream)), "wsc_decode")
 
     def sync(self, stream=None):
-        _check(self.lib.wsc_sync(self.h, stream), "wsc_sync")
+        _check(self.lib.wsc_sync(self.h, self._stream(stream)), "wsc_sync")
 
     def profile(self, batch: WscBatch, iters: int):
+        import sys
+        torch = sys.modules.get("torch")
+        if torch is not None and torch.cuda.is_initialized():
+            torch.cuda.synchronize()     # the profile runs on the context's own stream
         out = (C.c_double * 6)()
         _check(self.lib.wsc_profile(self.h, C.byref(batch), iters, out), "wsc_profile")
-        return dict(zip(["walk_count", "scan", "walk_emit", "unmask", "utf8", "total"], list(out)))
+        v = list(out)
+        return {"walk": v[0], "unmask": v[3], "utf8": v[4], "total": v[5]}
 
     def decode_host(self, wire: np.ndarray, seg_off: np.ndarray, state_in: np.ndarray | None = None,
                     compact: bool = False, frames_cap: int | None = None) -> DecodeResult:

@@ -2,7 +2,6 @@
 // Compiled by hipcc together with wsc_kernels.hip (gfx950 only; no CPU fallback anywhere: a
 // missing device is an error, WSC_E_NODEVICE).
 #include <hip/hip_runtime.h>
-#include <rocprim/device/device_scan.hpp>
 
 #include <cstdio>
 #include <cstring>
@@ -11,7 +10,7 @@
 #include "wsc_kernels.hpp"
 
 namespace wsc {
-template <bool EMIT, bool COMPACT> __global__ void k_walk(WalkArgs);
+template <bool COMPACT> __global__ void k_walk_fused(WalkArgs);
 template <bool COMPACT, int P, int NT>
 __global__ void k_unmask(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*,
                          const wsc_summary*);
@@ -48,9 +47,10 @@ struct wsc_ctx {
     wsc_config cfg{};
     uint32_t pieces = 8;          // 16 B pieces per lane -> window = pieces KiB
     SegCount* counts = nullptr;
-    SegCount* bases = nullptr;
-    void* scan_tmp = nullptr;
-    size_t scan_tmp_bytes = 0;
+    uint32_t* lb_ticket = nullptr;   // [0] ticket, [1] spin-timeout flag
+    uint32_t* lb_flag = nullptr;
+    uint64_t* lb_agg = nullptr;
+    uint64_t* lb_incl = nullptr;
     Span* spans = nullptr;
     uint32_t* tile = nullptr;
     uint64_t tile_entries = 0;
@@ -131,19 +131,19 @@ int wsc_create(int device, const wsc_config* cfg_in, wsc_ctx** out) {
     };
     chk(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate");
     chk(hipMalloc(&c->counts, cfg.max_segs * sizeof(SegCount)), "hipMalloc counts");
-    chk(hipMalloc(&c->bases, cfg.max_segs * sizeof(SegCount)), "hipMalloc bases");
+    const uint64_t max_blocks = (cfg.max_segs + 255) / 256 + 1;
+    chk(hipMalloc(&c->lb_ticket, 16), "hipMalloc lb_ticket");
+    chk(hipMalloc(&c->lb_flag, max_blocks * sizeof(uint32_t)), "hipMalloc lb_flag");
+    chk(hipMalloc(&c->lb_agg, max_blocks * 4 * sizeof(uint64_t)), "hipMalloc lb_agg");
+    chk(hipMalloc(&c->lb_incl, max_blocks * 4 * sizeof(uint64_t)), "hipMalloc lb_incl");
+    if (rc == WSC_OK) {
+        chk(hipMemsetAsync(c->lb_ticket, 0, 16, c->stream), "hipMemset lb_ticket");
+        chk(hipMemsetAsync(c->lb_flag, 0, max_blocks * sizeof(uint32_t), c->stream), "hipMemset lb_flag");
+        chk(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+    }
     chk(hipMalloc(&c->spans, (uint64_t)cfg.max_frames * sizeof(Span)), "hipMalloc spans");
     c->tile_entries = cfg.max_batch_bytes / 1024 + 2;
     chk(hipMalloc(&c->tile, c->tile_entries * sizeof(uint32_t)), "hipMalloc tile");
-    if (rc == WSC_OK) {
-        size_t bytes = 0;
-        SegCount init{};
-        chk(rocprim::exclusive_scan(nullptr, bytes, c->counts, c->bases, init, cfg.max_segs, SegCountAdd(),
-                                    c->stream),
-            "rocprim::exclusive_scan(size)");
-        c->scan_tmp_bytes = bytes;
-        chk(hipMalloc(&c->scan_tmp, bytes ? bytes : 16), "hipMalloc scan tmp");
-    }
     if (rc != WSC_OK) {
         wsc_destroy(c);
         return rc;
@@ -156,7 +156,7 @@ int wsc_destroy(wsc_ctx* c) {
     if (!c) return WSC_OK;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    void* ptrs[] = {c->counts, c->bases, c->scan_tmp, c->spans, c->tile, c->d_wire, c->d_arena,
+    void* ptrs[] = {c->counts, c->lb_ticket, c->lb_flag, c->lb_agg, c->lb_incl, c->spans, c->tile, c->d_wire, c->d_arena,
                     c->d_seg_off, c->d_state_in, c->d_state_out, c->d_seg_out, c->d_frames,
                     c->d_frame_dst, c->d_summary};
     for (void* p : ptrs)
@@ -209,7 +209,11 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     wa.state_in = b->state_in;
     wa.max_frame_len = c->cfg.max_frame_len;
     wa.counts = c->counts;
-    wa.bases = c->bases;
+    wa.lb_ticket = c->lb_ticket;
+    wa.lb_flag = c->lb_flag;
+    wa.lb_agg = c->lb_agg;
+    wa.lb_incl = c->lb_incl;
+    wa.lb_err = c->lb_ticket + 1;
     wa.frames = b->frames;
     wa.spans = c->spans;
     wa.spans_cap = c->cfg.max_frames;
@@ -225,17 +229,11 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
         if (ev) (void)hipEventRecord(ev[i], st);
     };
     rec(0);
-    if (compact) hipLaunchKernelGGL((k_walk<false, true>), wgrid, wblk, 0, st, wa);
-    else hipLaunchKernelGGL((k_walk<false, false>), wgrid, wblk, 0, st, wa);
+    if (compact) hipLaunchKernelGGL((k_walk_fused<true>), wgrid, wblk, 0, st, wa);
+    else hipLaunchKernelGGL((k_walk_fused<false>), wgrid, wblk, 0, st, wa);
     HIP_TRY(hipGetLastError());
     rec(1);
-    size_t tb = c->scan_tmp_bytes;
-    SegCount init{};
-    HIP_TRY(rocprim::exclusive_scan(c->scan_tmp, tb, c->counts, c->bases, init, n, SegCountAdd(), st));
     rec(2);
-    if (compact) hipLaunchKernelGGL((k_walk<true, true>), wgrid, wblk, 0, st, wa);
-    else hipLaunchKernelGGL((k_walk<true, false>), wgrid, wblk, 0, st, wa);
-    HIP_TRY(hipGetLastError());
     rec(3);
 
     uint8_t* udst = compact ? b->arena : b->wire;
@@ -274,6 +272,9 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     u8.frames = b->frames;
     u8.state_out = b->state_out;
     u8.seg_out = b->seg_out;
+    u8.lb_ticket = c->lb_ticket;
+    u8.lb_flag = c->lb_flag;
+    u8.lb_err = c->lb_ticket + 1;
     if (compact) hipLaunchKernelGGL((k_utf8<true>), wgrid, wblk, 0, st, u8);
     else hipLaunchKernelGGL((k_utf8<false>), wgrid, wblk, 0, st, u8);
     HIP_TRY(hipGetLastError());
@@ -284,15 +285,14 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
 int wsc_decode(wsc_ctx* c, const wsc_batch* b, void* hip_stream) {
     if (!c || !b) return fail(WSC_E_INVAL, "NULL argument");
     HIP_TRY(hipSetDevice(c->device));
-    hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
-    return launch(c, b, st, nullptr);
+    // like every HIP API: NULL is the default (null) stream
+    return launch(c, b, static_cast<hipStream_t>(hip_stream), nullptr);
 }
 
 int wsc_sync(wsc_ctx* c, void* hip_stream) {
     if (!c) return fail(WSC_E_INVAL, "NULL ctx");
     HIP_TRY(hipSetDevice(c->device));
-    hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
-    HIP_TRY(hipStreamSynchronize(st));
+    HIP_TRY(hipStreamSynchronize(static_cast<hipStream_t>(hip_stream)));
     return WSC_OK;
 }
 

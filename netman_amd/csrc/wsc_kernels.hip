@@ -1,9 +1,9 @@
 // wsc_kernels.hip -- gfx950 kernels of the WebSocket frame decoder.
 //
-//   k_walk<EMIT,COMPACT>  header walk + per-frame decode state machine, one lane per segment
+//   k_walk_fused<COMPACT> header walk + per-frame decode state machine, one lane per segment
 //                         (server/websocket.go:82-302, server/websocket_frame.go:13-103 minus the
-//                         byte loops).  Pass 1 counts, pass 2 (after an exclusive scan) emits
-//                         frame records, payload spans and the window->span index.
+//                         byte loops).  Count, block scan + decoupled look-back, then emit frame
+//                         records, payload spans and the window->span index, in one launch.
 //   k_unmask<COMPACT,P,NT> the hot loop (websocket_frame.go:35-39): XOR-unmask every payload span,
 //                         byte-tile decomposed, 16 B per lane access, 1 KiB per wave instruction.
 //   k_utf8                utf8.Valid for TEXT messages / control payloads / close reasons
@@ -30,10 +30,13 @@ __device__ __forceinline__ bool close_code_ok(uint32_t code) {
     return true;
 }
 
+// Walk one segment's frames (one lane).  Pass 1 (EMIT=false) only counts; pass 2 (EMIT=true)
+// writes frame records, payload spans, the window->span index and the segment's results at the
+// output offsets `base` (exclusive prefix over segments) for its counts `own` (pass 1 result).
+// COMPACT arena layout per segment: [data payloads][control payloads] at base.bytes0+base.bytes1.
 template <bool EMIT, bool COMPACT>
-__global__ __launch_bounds__(256) void k_walk(WalkArgs a) {
-    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= a.n_segs) return;
+__device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, const SegCount& base,
+                                                 const SegCount& own) {
     const uint8_t* __restrict__ w = a.wire;
     const uint64_t seg_start = a.seg_off[s];
     const uint64_t seg_end = a.seg_off[s + 1];
@@ -45,12 +48,8 @@ __global__ __launch_bounds__(256) void k_walk(WalkArgs a) {
     uint32_t mode = st.message_mode;
     uint32_t status = st.status;
     uint32_t close_code = 0, err_out = 0;
-
-    SegCount base = {}, tot = {};
-    if constexpr (EMIT) {
-        base = a.bases[s];
-        tot = SegCountAdd()(a.bases[a.n_segs - 1], a.counts[a.n_segs - 1]);
-    }
+    const uint64_t abase = base.bytes0 + base.bytes1;   // COMPACT: this segment's arena offset
+    const uint32_t sbase = base.spans0 + base.spans1;   // first span index of this segment
     uint32_t nf = 0, ns0 = 0, ns1 = 0, sflags = 0;
     uint64_t nb0 = 0, nb1 = 0;
 
@@ -59,8 +58,8 @@ __global__ __launch_bounds__(256) void k_walk(WalkArgs a) {
     uint64_t nx0 = 0, nx1 = 0;
     if constexpr (EMIT) {
         if constexpr (COMPACT) {
-            nx0 = (base.bytes0 + W - 1) & ~(W - 1);
-            nx1 = (tot.bytes0 + base.bytes1 + W - 1) & ~(W - 1);
+            nx0 = (abase + W - 1) & ~(W - 1);
+            nx1 = (abase + own.bytes0 + W - 1) & ~(W - 1);
         } else {
             nx0 = (seg_start + W - 1) & ~(W - 1);
         }
@@ -218,7 +217,7 @@ __global__ __launch_bounds__(256) void k_walk(WalkArgs a) {
                     if constexpr (COMPACT) {
                         uint64_t d = ~0ull;
                         if (fr.flags & WSC_FF_UNMASKED)
-                            d = region ? tot.bytes0 + base.bytes1 + nb1 : base.bytes0 + nb0;
+                            d = region ? abase + own.bytes0 + nb1 : abase + nb0;
                         a.frame_dst[fi] = d;
                     }
                 }
@@ -229,15 +228,15 @@ __global__ __launch_bounds__(256) void k_walk(WalkArgs a) {
                     uint32_t idx;
                     if constexpr (COMPACT) {
                         if (region) {
-                            sp.dst = tot.bytes0 + base.bytes1 + nb1;
-                            idx = tot.spans0 + base.spans1 + ns1;
+                            sp.dst = abase + own.bytes0 + nb1;
+                            idx = sbase + own.spans0 + ns1;
                         } else {
-                            sp.dst = base.bytes0 + nb0;
-                            idx = base.spans0 + ns0;
+                            sp.dst = abase + nb0;
+                            idx = sbase + ns0;
                         }
                     } else {
                         sp.dst = sp.src;
-                        idx = base.spans0 + ns0;
+                        idx = sbase + ns0;
                     }
                     sp.key = rotr32(fr.mask, 8u * ((uint32_t)(0u - (uint32_t)sp.dst) & 3u));
                     if (idx < a.spans_cap) a.spans[idx] = sp;
@@ -258,19 +257,17 @@ __global__ __launch_bounds__(256) void k_walk(WalkArgs a) {
         pos = next;
     }
 
-    if constexpr (!EMIT) {
-        SegCount c;
-        c.frames = nf; c.spans0 = ns0; c.spans1 = ns1; c.flags = sflags;
-        c.bytes0 = nb0; c.bytes1 = nb1;
-        a.counts[s] = c;
-    } else {
+    SegCount c;
+    c.frames = nf; c.spans0 = ns0; c.spans1 = ns1; c.flags = sflags;
+    c.bytes0 = nb0; c.bytes1 = nb1;
+    if constexpr (EMIT) {
         // windows that start in this segment's region(s) after its last span
         if constexpr (COMPACT) {
-            const uint64_t e0 = base.bytes0 + nb0, e1 = tot.bytes0 + base.bytes1 + nb1;
-            for (; nx0 < e0; nx0 += W) a.tile_first[nx0 >> a.win_shift] = base.spans0 + ns0;
-            for (; nx1 < e1; nx1 += W) a.tile_first[nx1 >> a.win_shift] = tot.spans0 + base.spans1 + ns1;
+            const uint64_t e0 = abase + nb0, e1 = e0 + nb1;
+            for (; nx0 < e0; nx0 += W) a.tile_first[nx0 >> a.win_shift] = sbase + ns0;
+            for (; nx1 < e1; nx1 += W) a.tile_first[nx1 >> a.win_shift] = sbase + ns0 + ns1;
         } else {
-            for (; nx0 < seg_end; nx0 += W) a.tile_first[nx0 >> a.win_shift] = base.spans0 + ns0;
+            for (; nx0 < seg_end; nx0 += W) a.tile_first[nx0 >> a.win_shift] = sbase + ns0;
         }
         wsc_seg_result r;
         r.consumed = pos - seg_start;
@@ -289,16 +286,138 @@ __global__ __launch_bounds__(256) void k_walk(WalkArgs a) {
         o.status = (uint8_t)status;
         o.pad = 0;
         a.state_out[s] = o;
-        if (s == a.n_segs - 1) {
-            wsc_summary sm;
-            sm.data_bytes = COMPACT ? tot.bytes0 : 0;
-            sm.ctrl_bytes = COMPACT ? tot.bytes1 : 0;
-            sm.n_frames = tot.frames;
-            sm.n_spans = tot.spans0 + tot.spans1;
-            sm.overflow = (tot.frames > a.frames_cap || tot.spans0 + tot.spans1 > a.spans_cap) ? 1u : 0u;
-            sm.pad = 0;
-            *a.summary = sm;
+    }
+    return c;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Fused walk: count -> block scan -> decoupled look-back across blocks -> emit, one launch.
+// Block ids come from a ticket counter in dispatch order, so every block a block waits for has
+// already started.  Look-back hand-off (MI355X_MICROARCH.md "Valid forms", row 1): one lane per
+// block stores its aggregate / inclusive prefix with agent-scope (sc1, write-through) stores,
+// drains them with s_waitcnt vmcnt(0), then publishes the flag with an agent-scope atomic; the
+// reader polls the flag and reads the payload with agent-scope atomic RMWs (fetch_add 0), which
+// are coherent across XCDs.  Spins are bounded; flags and the ticket are zeroed by k_utf8 at the
+// end of every decode (and at context creation).
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ SegCount sc_add(const SegCount& x, const SegCount& y) { return SegCountAdd()(x, y); }
+
+__device__ __forceinline__ SegCount sc_shfl_up(const SegCount& v, int d) {
+    SegCount o;
+    o.frames = __shfl_up(v.frames, d);
+    o.spans0 = __shfl_up(v.spans0, d);
+    o.spans1 = __shfl_up(v.spans1, d);
+    o.flags = __shfl_up(v.flags, d);
+    o.bytes0 = __shfl_up(v.bytes0, d);
+    o.bytes1 = __shfl_up(v.bytes1, d);
+    return o;
+}
+
+__device__ __forceinline__ void lb_store(uint64_t* p, const SegCount& v) {
+    const uint64_t w0 = (uint64_t)v.frames | ((uint64_t)v.spans0 << 32);
+    const uint64_t w1 = (uint64_t)v.spans1 | ((uint64_t)v.flags << 32);
+    __hip_atomic_store(p + 0, w0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(p + 1, w1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(p + 2, v.bytes0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(p + 3, v.bytes1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ SegCount lb_load(uint64_t* p) {
+    const uint64_t w0 = __hip_atomic_fetch_add(p + 0, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t w1 = __hip_atomic_fetch_add(p + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    SegCount v;
+    v.frames = (uint32_t)w0; v.spans0 = (uint32_t)(w0 >> 32);
+    v.spans1 = (uint32_t)w1; v.flags = (uint32_t)(w1 >> 32);
+    v.bytes0 = __hip_atomic_fetch_add(p + 2, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    v.bytes1 = __hip_atomic_fetch_add(p + 3, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return v;
+}
+
+template <bool COMPACT>
+__global__ __launch_bounds__(256) void k_walk_fused(WalkArgs a) {
+    __shared__ uint32_t sh_bid;
+    __shared__ SegCount sh_wave[4];
+    __shared__ SegCount sh_prefix;
+    if (threadIdx.x == 0)
+        sh_bid = __hip_atomic_fetch_add(a.lb_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const uint32_t bid = sh_bid;
+    const uint32_t n_blocks = (a.n_segs + 255) / 256;
+    const uint32_t s = bid * 256 + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const SegCount zero = {};
+
+    SegCount own = zero;
+    if (s < a.n_segs) {
+        own = walk_segment<false, COMPACT>(a, s, zero, zero);
+        a.counts[s] = own;
+    }
+    // block-wide scan (64-lane shuffles, then across the 4 waves)
+    SegCount inc = own;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const SegCount o = sc_shfl_up(inc, d);
+        if (lane >= (uint32_t)d) inc = sc_add(o, inc);
+    }
+    SegCount excl = sc_shfl_up(inc, 1);
+    if (lane == 0) excl = zero;
+    if (lane == 63) sh_wave[wave] = inc;
+    __syncthreads();
+    SegCount wpre = zero, btot = zero;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        if ((uint32_t)q < wave) wpre = sc_add(wpre, sh_wave[q]);
+        btot = sc_add(btot, sh_wave[q]);
+    }
+    if (threadIdx.x == 0) {
+        SegCount prefix = zero;
+        uint32_t* flag = a.lb_flag;
+        uint64_t* agg = a.lb_agg;      // [block][4]
+        uint64_t* incl = a.lb_incl;    // [block][4]
+        if (bid == 0) {
+            lb_store(incl, btot);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(flag, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            lb_store(agg + 4ull * bid, btot);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(flag + bid, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            int64_t j = (int64_t)bid - 1;
+            uint32_t spins = 0;
+            while (j >= 0) {
+                const uint32_t f = __hip_atomic_fetch_add(flag + j, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (f == 0) {
+                    if (++spins > (1u << 24)) {   // bounded: never hang the device
+                        __hip_atomic_fetch_or(a.lb_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                const SegCount v = lb_load((f == 2 ? incl : agg) + 4ull * j);
+                prefix = sc_add(v, prefix);
+                if (f == 2) break;
+                --j;
+            }
+            lb_store(incl + 4ull * bid, sc_add(prefix, btot));
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(flag + bid, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
+        sh_prefix = prefix;
+    }
+    __syncthreads();
+    const SegCount base = sc_add(sh_prefix, sc_add(wpre, excl));
+    if (s < a.n_segs) walk_segment<true, COMPACT>(a, s, base, own);
+    if (bid == n_blocks - 1 && threadIdx.x == 0) {
+        const SegCount tot = sc_add(sh_prefix, btot);
+        wsc_summary sm;
+        sm.data_bytes = COMPACT ? tot.bytes0 : 0;
+        sm.ctrl_bytes = COMPACT ? tot.bytes1 : 0;
+        sm.n_frames = tot.frames;
+        sm.n_spans = tot.spans0 + tot.spans1;
+        sm.overflow = (tot.frames > a.frames_cap || tot.spans0 + tot.spans1 > a.spans_cap) ? 1u : 0u;
+        if (__hip_atomic_load(a.lb_err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) sm.overflow |= 2u;
+        sm.pad = 0;
+        *a.summary = sm;
     }
 }
 
@@ -593,6 +712,9 @@ __device__ uint32_t u8_run(uint32_t s, const uint8_t* p, uint64_t n) {
 template <bool COMPACT>
 __global__ __launch_bounds__(256) void k_utf8(Utf8Args a) {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    // re-arm k_walk_fused's look-back state for the next decode (this launch is ordered after it)
+    if (s < (a.n_segs + 255) / 256) a.lb_flag[s] = 0;
+    if (s == 0) { *a.lb_ticket = 0; *a.lb_err = 0; }
     if (s >= a.n_segs) return;
     if (!(a.counts[s].flags & SEGF_UTF8)) return;
     wsc_seg_result r = a.seg_out[s];
@@ -645,10 +767,8 @@ __global__ __launch_bounds__(256) void k_utf8(Utf8Args a) {
 }
 
 // explicit instantiations used by the host code
-template __global__ void k_walk<false, false>(WalkArgs);
-template __global__ void k_walk<true, false>(WalkArgs);
-template __global__ void k_walk<false, true>(WalkArgs);
-template __global__ void k_walk<true, true>(WalkArgs);
+template __global__ void k_walk_fused<false>(WalkArgs);
+template __global__ void k_walk_fused<true>(WalkArgs);
 template __global__ void k_unmask<false, 4, 0>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*);
 template __global__ void k_unmask<false, 4, 1>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*);
 template __global__ void k_unmask<false, 4, 2>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*);

@@ -51,7 +51,6 @@ struct WalkArgs {
     const wsc_conn_state* state_in;
     uint64_t max_frame_len;
     SegCount* counts;
-    const SegCount* bases;
     wsc_frame* frames;
     Span* spans;
     uint32_t spans_cap;
@@ -61,6 +60,11 @@ struct WalkArgs {
     wsc_conn_state* state_out;
     wsc_seg_result* seg_out;
     wsc_summary* summary;
+    uint32_t* lb_ticket;         // look-back: dynamic block id counter
+    uint32_t* lb_flag;           // per block: 0 none, 1 aggregate, 2 inclusive prefix
+    uint64_t* lb_agg;            // per block: SegCount as 4 x u64
+    uint64_t* lb_incl;
+    uint32_t* lb_err;            // bounded-spin timeout
 };
 
 
@@ -75,6 +79,9 @@ struct Utf8Args {
     wsc_frame* frames;
     wsc_conn_state* state_out;
     wsc_seg_result* seg_out;
+    uint32_t* lb_ticket;
+    uint32_t* lb_flag;
+    uint32_t* lb_err;
 };
 
 }  // namespace wsc
