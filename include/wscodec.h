@@ -191,6 +191,10 @@ int wsc_decode_host(wsc_ctx* ctx, uint8_t* wire, uint64_t n_bytes, const uint64_
  * [5] = whole decode.  A context runs one decode at a time (its scratch is shared). */
 int wsc_profile(wsc_ctx* ctx, const wsc_batch* batch, int iters, double* out_ms);
 
+/* Diagnostics: with WSC_DEBUG_STAMPS=1 in the environment at wsc_create, the header-walk kernel
+ * records per block 4 s_memrealtime stamps (100 MHz): start, counted, look-back done, emitted. */
+int wsc_debug_stamps(wsc_ctx* ctx, uint64_t* out, uint32_t max_blocks);
+
 /* ---- session: the per-connection DecodePacket() mirror (C++ host side above the ABI) --------- */
 typedef struct wsc_session wsc_session;
 

@@ -92,6 +92,7 @@ SIGNATURES = {
     "wsc_sync": (_I, [_P, _P]),
     "wsc_decode_host": (_I, [_P, _P, _U64, _P, _U32, _U32, _P, _P, _P, _P, _U32, _P, _P, _P]),
     "wsc_profile": (_I, [_P, C.POINTER(WscBatch), _I, C.POINTER(C.c_double)]),
+    "wsc_debug_stamps": (_I, [_P, _P, _U32]),
     "wsc_session_create": (_I, [_I, C.POINTER(WscConfig), _U32, C.POINTER(_P)]),
     "wsc_session_destroy": (_I, [_P]),
     "wsc_session_open": (_I, [_P, C.POINTER(_U32)]),

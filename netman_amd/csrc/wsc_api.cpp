@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -51,6 +52,7 @@ struct wsc_ctx {
     uint32_t* lb_flag = nullptr;
     uint64_t* lb_agg = nullptr;
     uint64_t* lb_incl = nullptr;
+    uint64_t* dbg = nullptr;         // WSC_DEBUG_STAMPS=1: per-block walk timestamps
     Span* spans = nullptr;
     uint32_t* tile = nullptr;
     uint64_t tile_entries = 0;
@@ -136,6 +138,8 @@ int wsc_create(int device, const wsc_config* cfg_in, wsc_ctx** out) {
     chk(hipMalloc(&c->lb_flag, max_blocks * sizeof(uint32_t)), "hipMalloc lb_flag");
     chk(hipMalloc(&c->lb_agg, max_blocks * 4 * sizeof(uint64_t)), "hipMalloc lb_agg");
     chk(hipMalloc(&c->lb_incl, max_blocks * 4 * sizeof(uint64_t)), "hipMalloc lb_incl");
+    if (const char* e = std::getenv("WSC_DEBUG_STAMPS"); e && e[0] == '1')
+        chk(hipMalloc(&c->dbg, max_blocks * 4 * sizeof(uint64_t)), "hipMalloc dbg");
     if (rc == WSC_OK) {
         chk(hipMemsetAsync(c->lb_ticket, 0, 16, c->stream), "hipMemset lb_ticket");
         chk(hipMemsetAsync(c->lb_flag, 0, max_blocks * sizeof(uint32_t), c->stream), "hipMemset lb_flag");
@@ -156,7 +160,7 @@ int wsc_destroy(wsc_ctx* c) {
     if (!c) return WSC_OK;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    void* ptrs[] = {c->counts, c->lb_ticket, c->lb_flag, c->lb_agg, c->lb_incl, c->spans, c->tile, c->d_wire, c->d_arena,
+    void* ptrs[] = {c->dbg, c->counts, c->lb_ticket, c->lb_flag, c->lb_agg, c->lb_incl, c->spans, c->tile, c->d_wire, c->d_arena,
                     c->d_seg_off, c->d_state_in, c->d_state_out, c->d_seg_out, c->d_frames,
                     c->d_frame_dst, c->d_summary};
     for (void* p : ptrs)
@@ -203,6 +207,7 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
 
     WalkArgs wa{};
     wa.wire = b->wire;
+    wa.n_bytes = b->n_bytes;
     wa.seg_off = b->seg_off;
     wa.n_segs = n;
     wa.frames_cap = b->frames_cap;
@@ -214,6 +219,7 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     wa.lb_agg = c->lb_agg;
     wa.lb_incl = c->lb_incl;
     wa.lb_err = c->lb_ticket + 1;
+    wa.dbg = c->dbg;
     wa.frames = b->frames;
     wa.spans = c->spans;
     wa.spans_cap = c->cfg.max_frames;
@@ -372,6 +378,15 @@ int wsc_profile(wsc_ctx* c, const wsc_batch* b, int iters, double* out_ms) {
     for (auto& e : ev) (void)hipEventDestroy(e);
     for (int k = 0; k < 6; ++k) out_ms[k] = acc[k] / iters;
     return rc;
+}
+
+int wsc_debug_stamps(wsc_ctx* c, uint64_t* out, uint32_t max_blocks) {
+    if (!c || !out) return fail(WSC_E_INVAL, "NULL argument");
+    if (!c->dbg) return fail(WSC_E_STATE, "context created without WSC_DEBUG_STAMPS=1");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(out, c->dbg, (uint64_t)max_blocks * 4 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    return WSC_OK;
 }
 
 }  // extern "C"

@@ -34,6 +34,38 @@ __device__ __forceinline__ bool close_code_ok(uint32_t code) {
 // writes frame records, payload spans, the window->span index and the segment's results at the
 // output offsets `base` (exclusive prefix over segments) for its counts `own` (pass 1 result).
 // COMPACT arena layout per segment: [data payloads][control payloads] at base.bytes0+base.bytes1.
+// Header fetch: the longest masked header is 14 bytes.  Two aligned 16-byte loads cover
+// [pos, pos+16) -- one request per lane per load instead of 14 byte gathers.  Bytes past the
+// segment end are never used (every use is guarded by `avail`).
+__device__ __forceinline__ void hdr_issue(const uint8_t* __restrict__ w, uint64_t n, uint64_t pos,
+                                          uint4& c0, uint4& c1) {
+    const uint64_t a0 = pos & ~15ull;
+    if (a0 + 32 <= n) {
+        c0 = *reinterpret_cast<const uint4*>(w + a0);
+        c1 = *reinterpret_cast<const uint4*>(w + a0 + 16);
+    } else {   // the last 32 bytes of the buffer: byte loads, nothing read past n
+        uint32_t t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (uint32_t k = 0; k < 32 && a0 + k < n; ++k) t[k >> 2] |= (uint32_t)w[a0 + k] << (8 * (k & 3));
+        c0 = make_uint4(t[0], t[1], t[2], t[3]);
+        c1 = make_uint4(t[4], t[5], t[6], t[7]);
+    }
+}
+__device__ __forceinline__ void hdr_extract(const uint4& c0, const uint4& c1, uint64_t pos, uint32_t (&h)[14]) {
+    const uint32_t d[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+    const uint32_t sh = (uint32_t)(pos & 15), q = sh >> 2, rb = sh & 3;
+    uint32_t hd[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        uint32_t lo = d[j], hi = d[j + 1];
+        if (q == 1) { lo = d[j + 1]; hi = d[j + 2]; }
+        else if (q == 2) { lo = d[j + 2]; hi = d[j + 3]; }
+        else if (q == 3) { lo = d[j + 3]; hi = d[j + 4]; }
+        hd[j] = __builtin_amdgcn_alignbyte(hi, lo, rb);
+    }
+#pragma unroll
+    for (int k = 0; k < 14; ++k) h[k] = (hd[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+}
+
 template <bool EMIT, bool COMPACT>
 __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, const SegCount& base,
                                                  const SegCount& own) {
@@ -66,13 +98,16 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
     }
 
     uint64_t pos = seg_start;
+    // The header of the next frame is loaded as soon as its position is known, before this
+    // frame's record stores are issued: vmcnt counts loads and stores in order, so a load issued
+    // after the stores would also wait for them.
+    uint4 hc0 = make_uint4(0, 0, 0, 0), hc1 = make_uint4(0, 0, 0, 0);
+    if (status == WSC_SEG_OPEN && seg_end - pos >= 2) hdr_issue(w, a.n_bytes, pos, hc0, hc1);
     while (status == WSC_SEG_OPEN) {
         const uint64_t avail = seg_end - pos;
         if (avail < 2) break;
-        // speculative header read: the longest masked header is 14 bytes
         uint32_t h[14];
-#pragma unroll
-        for (int k = 0; k < 14; ++k) h[k] = (k < (int64_t)avail) ? (uint32_t)w[pos + k] : 0u;
+        hdr_extract(hc0, hc1, pos, h);
         const uint32_t fin = h[0] >> 7;
         const uint32_t rsv = (h[0] >> 4) & 7;
         const uint32_t op = h[0] & 0xF;
@@ -205,6 +240,7 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
             }
         }
 
+        if (status == WSC_SEG_OPEN && seg_end - next >= 2) hdr_issue(w, a.n_bytes, next, hc0, hc1);
         if (fr.flags & (WSC_FF_U8_PART | WSC_FF_U8_SELF | WSC_FF_U8_CHAIN | WSC_FF_U8_REASON))
             sflags |= SEGF_UTF8;
         if constexpr (COMPACT) if (region) fr.flags |= WSC_FF_CTRL_ARENA;
@@ -346,6 +382,8 @@ __global__ __launch_bounds__(256) void k_walk_fused(WalkArgs a) {
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const SegCount zero = {};
 
+    uint64_t t0 = 0, t1 = 0, t2 = 0;
+    if (a.dbg && threadIdx.x == 0) t0 = __builtin_amdgcn_s_memrealtime();
     SegCount own = zero;
     if (s < a.n_segs) {
         own = walk_segment<false, COMPACT>(a, s, zero, zero);
@@ -368,45 +406,75 @@ __global__ __launch_bounds__(256) void k_walk_fused(WalkArgs a) {
         if ((uint32_t)q < wave) wpre = sc_add(wpre, sh_wave[q]);
         btot = sc_add(btot, sh_wave[q]);
     }
-    if (threadIdx.x == 0) {
-        SegCount prefix = zero;
+    if (wave == 0) {
+        // decoupled look-back by one wave: 64 predecessors are examined per round
+        if (a.dbg && lane == 0) t1 = __builtin_amdgcn_s_memrealtime();
         uint32_t* flag = a.lb_flag;
         uint64_t* agg = a.lb_agg;      // [block][4]
         uint64_t* incl = a.lb_incl;    // [block][4]
-        if (bid == 0) {
-            lb_store(incl, btot);
+        if (lane == 0) {
+            lb_store(bid == 0 ? incl : agg + 4ull * bid, btot);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __hip_atomic_store(flag, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            lb_store(agg + 4ull * bid, btot);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __hip_atomic_store(flag + bid, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            int64_t j = (int64_t)bid - 1;
-            uint32_t spins = 0;
-            while (j >= 0) {
-                const uint32_t f = __hip_atomic_fetch_add(flag + j, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (f == 0) {
-                    if (++spins > (1u << 24)) {   // bounded: never hang the device
-                        __hip_atomic_fetch_or(a.lb_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(1);
-                    continue;
-                }
-                const SegCount v = lb_load((f == 2 ? incl : agg) + 4ull * j);
-                prefix = sc_add(v, prefix);
-                if (f == 2) break;
-                --j;
-            }
-            lb_store(incl + 4ull * bid, sc_add(prefix, btot));
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __hip_atomic_store(flag + bid, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(flag + bid, bid == 0 ? 2u : 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        sh_prefix = prefix;
+        SegCount prefix = zero;
+        int64_t j0 = (int64_t)bid - 1;
+        uint32_t spins = 0;
+        while (j0 >= 0) {
+            const int64_t j = j0 - (int64_t)lane;
+            const uint32_t f = j >= 0 ? __hip_atomic_fetch_add(flag + j, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                      : 2u;   // before block 0: an inclusive prefix of zero
+            const uint64_t m2 = __ballot(f == 2);
+            const uint64_t m0 = __ballot(f == 0);
+            const uint32_t first2 = m2 ? (uint32_t)__builtin_ctzll(m2) : 64u;
+            const uint64_t need = first2 >= 63 ? ~0ull : ((2ull << first2) - 1);   // lanes 0..first2
+            if (m0 & need) {   // a predecessor in range has not published yet: poll again
+                if (++spins > (1u << 22)) {   // bounded: never hang the device
+                    if (lane == 0) __hip_atomic_fetch_or(a.lb_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+                continue;
+            }
+            SegCount v = zero;
+            if (lane <= first2 && j >= 0) v = lb_load((lane == first2 ? incl : agg) + 4ull * j);
+#pragma unroll
+            for (int d = 32; d >= 1; d >>= 1) {
+                SegCount o;
+                o.frames = __shfl_xor(v.frames, d);
+                o.spans0 = __shfl_xor(v.spans0, d);
+                o.spans1 = __shfl_xor(v.spans1, d);
+                o.flags = __shfl_xor(v.flags, d);
+                o.bytes0 = __shfl_xor(v.bytes0, d);
+                o.bytes1 = __shfl_xor(v.bytes1, d);
+                v = sc_add(v, o);
+            }
+            prefix = sc_add(prefix, v);
+            if (first2 < 64) break;
+            j0 -= 64;
+        }
+        if (lane == 0) {
+            if (bid != 0) {
+                lb_store(incl + 4ull * bid, sc_add(prefix, btot));
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __hip_atomic_store(flag + bid, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            sh_prefix = prefix;
+        }
     }
     __syncthreads();
+    if (a.dbg && threadIdx.x == 0) t2 = __builtin_amdgcn_s_memrealtime();
     const SegCount base = sc_add(sh_prefix, sc_add(wpre, excl));
     if (s < a.n_segs) walk_segment<true, COMPACT>(a, s, base, own);
+    if (a.dbg) {   // diagnostic timestamps (100 MHz s_memrealtime), written only to the dbg buffer
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            a.dbg[4 * bid + 0] = t0;
+            a.dbg[4 * bid + 1] = t1;
+            a.dbg[4 * bid + 2] = t2;
+            a.dbg[4 * bid + 3] = __builtin_amdgcn_s_memrealtime();
+        }
+    }
     if (bid == n_blocks - 1 && threadIdx.x == 0) {
         const SegCount tot = sc_add(sh_prefix, btot);
         wsc_summary sm;

@@ -45,6 +45,7 @@ static_assert(sizeof(Span) == 24, "span layout");
 
 struct WalkArgs {
     const uint8_t* wire;
+    uint64_t n_bytes;
     const uint64_t* seg_off;
     uint32_t n_segs;
     uint32_t frames_cap;
@@ -65,6 +66,7 @@ struct WalkArgs {
     uint64_t* lb_agg;            // per block: SegCount as 4 x u64
     uint64_t* lb_incl;
     uint32_t* lb_err;            // bounded-spin timeout
+    uint64_t* dbg;               // optional per-block timestamps (WSC_DEBUG_STAMPS=1)
 };
 
 

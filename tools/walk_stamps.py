@@ -1,0 +1,36 @@
+"""Where does the header walk spend its time?  Per-block s_memrealtime stamps (diagnostic build
+path: WSC_DEBUG_STAMPS=1) for a workload; prints count / look-back / emit phase durations."""
+import os
+import sys
+os.environ["WSC_DEBUG_STAMPS"] = "1"
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np
+import torch
+from netman_amd import codec as K, synth
+
+wl = sys.argv[1] if len(sys.argv) > 1 else "64k"
+cfg = {"64k": lambda: synth.uniform_batch(16384, 65536, 4, seed=synth.SEED_BASE + 1),
+       "1k": lambda: synth.uniform_batch(1 << 20, 1024, 16, seed=synth.SEED_BASE + 1),
+       "mixed": lambda: synth.mixed_batch()}[wl]()
+dev = torch.device("cuda:0")
+n = len(cfg["seg_off"]) - 1
+c = K.Codec(0, max_batch_bytes=len(cfg["wire"]) + 4096, max_segs=n, max_frames=cfg["n_frames"] + 16)
+t = [torch.from_numpy(cfg["wire"]).to(dev), torch.from_numpy(cfg["seg_off"].view(np.int64)).to(dev),
+     torch.zeros(n * 16, dtype=torch.uint8, device=dev), torch.zeros(n * 32, dtype=torch.uint8, device=dev),
+     torch.zeros((cfg["n_frames"] + 16) * 32, dtype=torch.uint8, device=dev), torch.zeros(32, dtype=torch.uint8, device=dev)]
+b = c.make_batch(t[0], t[1], None, t[2], t[3], t[4], t[5])
+nb = (n + 255) // 256
+for it in range(3):
+    c.decode(b)
+    c.sync()
+    out = np.zeros(nb * 4, np.uint64)
+    assert c.lib.wsc_debug_stamps(c.h, out.ctypes.data, nb) == 0
+    st = out.reshape(nb, 4).astype(np.int64)
+    t0 = st[:, 0].min()
+    rel = (st - t0) / 100.0   # us
+    cnt = rel[:, 1] - rel[:, 0]
+    lb = rel[:, 2] - rel[:, 1]
+    em = rel[:, 3] - rel[:, 2]
+    print(f"{wl} iter {it}: blocks={nb} start spread {rel[:,0].max():.1f} us | count med {np.median(cnt):.1f} max {cnt.max():.1f} | "
+          f"lookback med {np.median(lb):.1f} max {lb.max():.1f} | emit med {np.median(em):.1f} max {em.max():.1f} | end {rel[:,3].max():.1f} us")
+print(c.profile(b, 5))
