@@ -187,7 +187,7 @@ int wsc_decode_host(wsc_ctx* ctx, uint8_t* wire, uint64_t n_bytes, const uint64_
 
 /* Timing helper for the benchmark: run `iters` back-to-back decodes of a device batch and
  * return the per-kernel average device time (ms) measured with hipEvents on the launch stream.
- * out_ms[0] = fused header walk, [1], [2] = 0 (reserved), [3] = unmask, [4] = utf8 pass,
+ * out_ms[0] = fused header walk (incl. utf8), [1], [2], [4] = 0 (reserved), [3] = unmask,
  * [5] = whole decode.  A context runs one decode at a time (its scratch is shared). */
 int wsc_profile(wsc_ctx* ctx, const wsc_batch* batch, int iters, double* out_ms);
 

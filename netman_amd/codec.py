@@ -236,7 +236,7 @@ class Codec:
         out = (C.c_double * 6)()
         _check(self.lib.wsc_profile(self.h, C.byref(batch), iters, out), "wsc_profile")
         v = list(out)
-        return {"walk": v[0], "unmask": v[3], "utf8": v[4], "total": v[5]}
+        return {"walk": v[0], "unmask": v[3], "total": v[5]}
 
     def decode_host(self, wire: np.ndarray, seg_off: np.ndarray, state_in: np.ndarray | None = None,
                     compact: bool = False, frames_cap: int | None = None) -> DecodeResult:

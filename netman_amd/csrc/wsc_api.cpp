@@ -14,8 +14,7 @@ namespace wsc {
 template <bool COMPACT> __global__ void k_walk_fused(WalkArgs);
 template <bool COMPACT, int P, int NT>
 __global__ void k_unmask(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*,
-                         const wsc_summary*);
-template <bool COMPACT> __global__ void k_utf8(Utf8Args);
+                         const wsc_summary*, uint32_t*, uint32_t);
 }  // namespace wsc
 
 using namespace wsc;
@@ -48,8 +47,8 @@ struct wsc_ctx {
     wsc_config cfg{};
     uint32_t pieces = 8;          // 16 B pieces per lane -> window = pieces KiB
     SegCount* counts = nullptr;
-    uint32_t* lb_ticket = nullptr;   // [0] ticket, [1] spin-timeout flag
-    uint32_t* lb_flag = nullptr;
+    uint32_t* lb_state = nullptr;    // [0] ticket, [1] spin-timeout flag, [2..] per-block flags
+    uint32_t* u8info = nullptr;      // per segment {utf8-failing frame ordinal, DFA state}
     uint64_t* lb_agg = nullptr;
     uint64_t* lb_incl = nullptr;
     uint64_t* dbg = nullptr;         // WSC_DEBUG_STAMPS=1: per-block walk timestamps
@@ -134,15 +133,14 @@ int wsc_create(int device, const wsc_config* cfg_in, wsc_ctx** out) {
     chk(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate");
     chk(hipMalloc(&c->counts, cfg.max_segs * sizeof(SegCount)), "hipMalloc counts");
     const uint64_t max_blocks = (cfg.max_segs + 255) / 256 + 1;
-    chk(hipMalloc(&c->lb_ticket, 16), "hipMalloc lb_ticket");
-    chk(hipMalloc(&c->lb_flag, max_blocks * sizeof(uint32_t)), "hipMalloc lb_flag");
+    chk(hipMalloc(&c->lb_state, (max_blocks + 2) * sizeof(uint32_t)), "hipMalloc lb_state");
+    chk(hipMalloc(&c->u8info, (uint64_t)cfg.max_segs * 2 * sizeof(uint32_t)), "hipMalloc u8info");
     chk(hipMalloc(&c->lb_agg, max_blocks * 4 * sizeof(uint64_t)), "hipMalloc lb_agg");
     chk(hipMalloc(&c->lb_incl, max_blocks * 4 * sizeof(uint64_t)), "hipMalloc lb_incl");
     if (const char* e = std::getenv("WSC_DEBUG_STAMPS"); e && e[0] == '1')
         chk(hipMalloc(&c->dbg, max_blocks * 4 * sizeof(uint64_t)), "hipMalloc dbg");
     if (rc == WSC_OK) {
-        chk(hipMemsetAsync(c->lb_ticket, 0, 16, c->stream), "hipMemset lb_ticket");
-        chk(hipMemsetAsync(c->lb_flag, 0, max_blocks * sizeof(uint32_t), c->stream), "hipMemset lb_flag");
+        chk(hipMemsetAsync(c->lb_state, 0, (max_blocks + 2) * sizeof(uint32_t), c->stream), "hipMemset lb_state");
         chk(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
     }
     chk(hipMalloc(&c->spans, (uint64_t)cfg.max_frames * sizeof(Span)), "hipMalloc spans");
@@ -160,7 +158,7 @@ int wsc_destroy(wsc_ctx* c) {
     if (!c) return WSC_OK;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    void* ptrs[] = {c->dbg, c->counts, c->lb_ticket, c->lb_flag, c->lb_agg, c->lb_incl, c->spans, c->tile, c->d_wire, c->d_arena,
+    void* ptrs[] = {c->dbg, c->counts, c->lb_state, c->u8info, c->lb_agg, c->lb_incl, c->spans, c->tile, c->d_wire, c->d_arena,
                     c->d_seg_off, c->d_state_in, c->d_state_out, c->d_seg_out, c->d_frames,
                     c->d_frame_dst, c->d_summary};
     for (void* p : ptrs)
@@ -214,11 +212,12 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     wa.state_in = b->state_in;
     wa.max_frame_len = c->cfg.max_frame_len;
     wa.counts = c->counts;
-    wa.lb_ticket = c->lb_ticket;
-    wa.lb_flag = c->lb_flag;
+    wa.lb_ticket = c->lb_state;
+    wa.lb_flag = c->lb_state + 2;
+    wa.u8info = c->u8info;
     wa.lb_agg = c->lb_agg;
     wa.lb_incl = c->lb_incl;
-    wa.lb_err = c->lb_ticket + 1;
+    wa.lb_err = c->lb_state + 1;
     wa.dbg = c->dbg;
     wa.frames = b->frames;
     wa.spans = c->spans;
@@ -251,7 +250,7 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     if (waves == 0) waves = 1;
     const dim3 ublk(256), ugrid((uint32_t)((waves + 3) / 4));
     using UK = void (*)(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*,
-                        const wsc_summary*);
+                        const wsc_summary*, uint32_t*, uint32_t);
     // [compact][pieces 4/8/16][nt 0..3]
     static const UK table[2][3][4] = {
         {{k_unmask<false, 4, 0>, k_unmask<false, 4, 1>, k_unmask<false, 4, 2>, k_unmask<false, 4, 3>},
@@ -263,26 +262,11 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     const int pi = c->pieces == 4 ? 0 : (c->pieces == 8 ? 1 : 2);
     const UK kern = table[compact ? 1 : 0][pi][c->cfg.unmask_nt & 3];
     hipLaunchKernelGGL(kern, ugrid, ublk, 0, st, udst, (const uint8_t*)b->wire, b->n_bytes, udst_bytes,
-                       (const Span*)c->spans, (const uint32_t*)c->tile, (const wsc_summary*)b->summary);
+                       (const Span*)c->spans, (const uint32_t*)c->tile, (const wsc_summary*)b->summary,
+                       c->lb_state, (n + 255) / 256);
     HIP_TRY(hipGetLastError());
     rec(4);
 
-    Utf8Args u8{};
-    u8.wire = b->wire;
-    u8.arena = b->arena;
-    u8.frame_dst = b->frame_dst;
-    u8.seg_off = b->seg_off;
-    u8.n_segs = n;
-    u8.counts = c->counts;
-    u8.state_in = b->state_in;
-    u8.frames = b->frames;
-    u8.state_out = b->state_out;
-    u8.seg_out = b->seg_out;
-    u8.lb_ticket = c->lb_ticket;
-    u8.lb_flag = c->lb_flag;
-    u8.lb_err = c->lb_ticket + 1;
-    if (compact) hipLaunchKernelGGL((k_utf8<true>), wgrid, wblk, 0, st, u8);
-    else hipLaunchKernelGGL((k_utf8<false>), wgrid, wblk, 0, st, u8);
     HIP_TRY(hipGetLastError());
     rec(5);
     return WSC_OK;

@@ -6,9 +6,8 @@
 //                         records, payload spans and the window->span index, in one launch.
 //   k_unmask<COMPACT,P,NT> the hot loop (websocket_frame.go:35-39): XOR-unmask every payload span,
 //                         byte-tile decomposed, 16 B per lane access, 1 KiB per wave instruction.
-//   k_utf8                utf8.Valid for TEXT messages / control payloads / close reasons
-//                         (websocket_frame.go:71-73, websocket.go:170-172) and the fix-up of a
-//                         connection whose text turns out invalid (CloseCode 1007).
+//   utf8.Valid (websocket_frame.go:71-73, websocket.go:170-172) runs inside the walk's counting
+//   pass on the still-masked wire, so a connection whose text is invalid stops at that frame.
 #include "wsc_kernels.hpp"
 
 namespace wsc {
@@ -34,6 +33,48 @@ __device__ __forceinline__ bool close_code_ok(uint32_t code) {
 // writes frame records, payload spans, the window->span index and the segment's results at the
 // output offsets `base` (exclusive prefix over segments) for its counts `own` (pass 1 result).
 // COMPACT arena layout per segment: [data payloads][control payloads] at base.bytes0+base.bytes1.
+// ---------------------------------------------------------------------------------------------
+// UTF-8 (Go utf8.Valid semantics): a 9-state DFA, state 0 = between characters, 8 = reject.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t u8_step(uint32_t s, uint32_t b) {
+    switch (s) {
+    case 0:
+        if (b < 0x80) return 0;
+        if (b >= 0xC2 && b <= 0xDF) return 1;
+        if (b == 0xE0) return 4;
+        if (b == 0xED) return 5;
+        if (b >= 0xE1 && b <= 0xEF) return 2;
+        if (b == 0xF0) return 6;
+        if (b >= 0xF1 && b <= 0xF3) return 3;
+        if (b == 0xF4) return 7;
+        return 8;
+    case 1: return (b >= 0x80 && b <= 0xBF) ? 0 : 8;
+    case 2: return (b >= 0x80 && b <= 0xBF) ? 1 : 8;
+    case 3: return (b >= 0x80 && b <= 0xBF) ? 2 : 8;
+    case 4: return (b >= 0xA0 && b <= 0xBF) ? 1 : 8;
+    case 5: return (b >= 0x80 && b <= 0x9F) ? 1 : 8;
+    case 6: return (b >= 0x90 && b <= 0xBF) ? 2 : 8;
+    case 7: return (b >= 0x80 && b <= 0x8F) ? 2 : 8;
+    default: return 8;
+    }
+}
+
+// Run the DFA over n payload bytes that are still MASKED on the wire: byte i of the payload is
+// w[p + i] ^ (mask >> 8*(i & 3)).  4-byte ASCII groups are skipped while between characters.
+__device__ uint32_t u8_run_masked(uint32_t s, const uint8_t* __restrict__ w, uint64_t p, uint64_t n,
+                                  uint32_t mask) {
+    uint64_t i = 0;
+    while (i < n && s != 8) {
+        if (s == 0 && ((p + i) & 3) == 0 && i + 4 <= n) {
+            const uint32_t v = *reinterpret_cast<const uint32_t*>(w + p + i) ^ rotr32(mask, 8u * (uint32_t)(i & 3));
+            if ((v & 0x80808080u) == 0) { i += 4; continue; }
+        }
+        s = u8_step(s, (uint32_t)w[p + i] ^ ((mask >> (8u * (uint32_t)(i & 3))) & 0xFFu));
+        ++i;
+    }
+    return s;
+}
+
 // Header fetch: the longest masked header is 14 bytes.  Two aligned 16-byte loads cover
 // [pos, pos+16) -- one request per lane per load instead of 14 byte gathers.  Bytes past the
 // segment end are never used (every use is guarded by `avail`).
@@ -95,6 +136,16 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
         } else {
             nx0 = (seg_start + W - 1) & ~(W - 1);
         }
+    }
+
+    // UTF-8 verdicts are decided by the counting pass (payload read on the still-masked wire) and
+    // replayed by the emitting pass: u8fail = ordinal of the first frame that fails, u8dfa = DFA
+    // state after the continueBuffer (carried to the next batch).
+    uint32_t u8fail = 0xFFFFFFFFu;
+    uint32_t u8dfa = cont ? st.cont_utf8 : 0u;
+    if constexpr (EMIT) {
+        u8fail = a.u8info[2 * s];
+        u8dfa = a.u8info[2 * s + 1];
     }
 
     uint64_t pos = seg_start;
@@ -240,9 +291,27 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
             }
         }
 
-        if (status == WSC_SEG_OPEN && seg_end - next >= 2) hdr_issue(w, a.n_bytes, next, hc0, hc1);
-        if (fr.flags & (WSC_FF_U8_PART | WSC_FF_U8_SELF | WSC_FF_U8_CHAIN | WSC_FF_U8_REASON))
+        // utf8.Valid: TEXT messages (websocket_frame.go:71-73; across fragments and batches),
+        // control payloads inside a TEXT message (Q6), close reasons (websocket.go:170-172)
+        if (fr.flags & (WSC_FF_U8_PART | WSC_FF_U8_SELF | WSC_FF_U8_CHAIN | WSC_FF_U8_REASON)) {
             sflags |= SEGF_UTF8;
+            if constexpr (!EMIT) {
+                const uint64_t ps = pos + fr.hdr_len;
+                bool ok = true;
+                if (fr.flags & WSC_FF_U8_PART) u8dfa = u8_run_masked(u8dfa, w, ps, plen, fr.mask);
+                else if (fr.flags & WSC_FF_U8_CHAIN) ok = u8_run_masked(u8dfa, w, ps, plen, fr.mask) == 0;
+                else if (fr.flags & WSC_FF_U8_SELF) ok = u8_run_masked(0, w, ps, plen, fr.mask) == 0;
+                else ok = u8_run_masked(0, w, ps + 2, plen - 2, rotr32(fr.mask, 16)) == 0;
+                if (!ok) u8fail = nf;
+            }
+            if (nf == u8fail) {   // -> CloseCode(1007) (epoll.go:126-127); nothing after it is read
+                fr.kind = WSC_FK_ERROR;
+                fr.err = WSC_ERR_MUST_UTF8;
+                status = WSC_SEG_ERROR; close_code = 1007; err_out = WSC_ERR_MUST_UTF8;
+            }
+        }
+        if constexpr (!EMIT) if (fr.flags & WSC_FF_CONT_MSG) u8dfa = 0;   // continueBuffer consumed
+        if (status == WSC_SEG_OPEN && seg_end - next >= 2) hdr_issue(w, a.n_bytes, next, hc0, hc1);
         if constexpr (COMPACT) if (region) fr.flags |= WSC_FF_CTRL_ARENA;
 
         if (emit_rec) {
@@ -296,6 +365,10 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
     SegCount c;
     c.frames = nf; c.spans0 = ns0; c.spans1 = ns1; c.flags = sflags;
     c.bytes0 = nb0; c.bytes1 = nb1;
+    if constexpr (!EMIT) {
+        a.u8info[2 * s] = u8fail;
+        a.u8info[2 * s + 1] = u8dfa;
+    }
     if constexpr (EMIT) {
         // windows that start in this segment's region(s) after its last span
         if constexpr (COMPACT) {
@@ -318,7 +391,7 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
         o.cont_len = cont;
         o.msg_id = msg;
         o.message_mode = (uint8_t)mode;
-        o.cont_utf8 = cont ? st.cont_utf8 : 0;   // k_utf8 recomputes it for TEXT chains
+        o.cont_utf8 = cont ? (uint8_t)u8dfa : 0;
         o.status = (uint8_t)status;
         o.pad = 0;
         a.state_out[s] = o;
@@ -333,8 +406,8 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
 // block stores its aggregate / inclusive prefix with agent-scope (sc1, write-through) stores,
 // drains them with s_waitcnt vmcnt(0), then publishes the flag with an agent-scope atomic; the
 // reader polls the flag and reads the payload with agent-scope atomic RMWs (fetch_add 0), which
-// are coherent across XCDs.  Spins are bounded; flags and the ticket are zeroed by k_utf8 at the
-// end of every decode (and at context creation).
+// are coherent across XCDs.  Spins are bounded; flags and the ticket are zeroed by k_unmask
+// (the next launch on the stream) of every decode, and at context creation.
 // ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ SegCount sc_add(const SegCount& x, const SegCount& y) { return SegCountAdd()(x, y); }
 
@@ -645,8 +718,13 @@ __global__ __launch_bounds__(256) void k_unmask(uint8_t* __restrict__ dst, const
                                                 uint64_t src_bytes, uint64_t dst_bytes_host,
                                                 const Span* __restrict__ spans,
                                                 const uint32_t* __restrict__ tile_first,
-                                                const wsc_summary* __restrict__ summary) {
+                                                const wsc_summary* __restrict__ summary,
+                                                uint32_t* __restrict__ lb_state, uint32_t n_walk_blocks) {
     constexpr uint32_t WB = 1024u * P;
+    // re-arm the walk's look-back state for the next decode (this launch is ordered after it):
+    // lb_state[0] = ticket, [1] = timeout flag, [2 ...] = per-block flags
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n_walk_blocks + 2; t += gridDim.x * blockDim.x)
+        lb_state[t] = 0;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t waves_per_block = blockDim.x >> 6;
     const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * waves_per_block + (threadIdx.x >> 6));
@@ -738,130 +816,32 @@ __global__ __launch_bounds__(256) void k_unmask(uint8_t* __restrict__ dst, const
     }
 }
 
-// ---------------------------------------------------------------------------------------------
-// UTF-8 (Go utf8.Valid semantics): a 9-state DFA, state 0 = between characters, 8 = reject.
-// ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t u8_step(uint32_t s, uint32_t b) {
-    switch (s) {
-    case 0:
-        if (b < 0x80) return 0;
-        if (b >= 0xC2 && b <= 0xDF) return 1;
-        if (b == 0xE0) return 4;
-        if (b == 0xED) return 5;
-        if (b >= 0xE1 && b <= 0xEF) return 2;
-        if (b == 0xF0) return 6;
-        if (b >= 0xF1 && b <= 0xF3) return 3;
-        if (b == 0xF4) return 7;
-        return 8;
-    case 1: return (b >= 0x80 && b <= 0xBF) ? 0 : 8;
-    case 2: return (b >= 0x80 && b <= 0xBF) ? 1 : 8;
-    case 3: return (b >= 0x80 && b <= 0xBF) ? 2 : 8;
-    case 4: return (b >= 0xA0 && b <= 0xBF) ? 1 : 8;
-    case 5: return (b >= 0x80 && b <= 0x9F) ? 1 : 8;
-    case 6: return (b >= 0x90 && b <= 0xBF) ? 2 : 8;
-    case 7: return (b >= 0x80 && b <= 0x8F) ? 2 : 8;
-    default: return 8;
-    }
-}
-
-__device__ uint32_t u8_run(uint32_t s, const uint8_t* p, uint64_t n) {
-    uint64_t i = 0;
-    while (i < n && s != 8) {
-        if (s == 0 && (((uintptr_t)(p + i)) & 3) == 0 && i + 4 <= n) {
-            const uint32_t wv = *reinterpret_cast<const uint32_t*>(p + i);
-            if ((wv & 0x80808080u) == 0) { i += 4; continue; }
-        }
-        s = u8_step(s, p[i]);
-        ++i;
-    }
-    return s;
-}
-
-template <bool COMPACT>
-__global__ __launch_bounds__(256) void k_utf8(Utf8Args a) {
-    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    // re-arm k_walk_fused's look-back state for the next decode (this launch is ordered after it)
-    if (s < (a.n_segs + 255) / 256) a.lb_flag[s] = 0;
-    if (s == 0) { *a.lb_ticket = 0; *a.lb_err = 0; }
-    if (s >= a.n_segs) return;
-    if (!(a.counts[s].flags & SEGF_UTF8)) return;
-    wsc_seg_result r = a.seg_out[s];
-    uint32_t dfa = 0;
-    if (a.state_in && a.state_in[s].cont_len) dfa = a.state_in[s].cont_utf8;
-    int64_t fail = -1;
-    for (uint32_t i = r.frame_begin; i < r.frame_begin + r.frame_count; ++i) {
-        const wsc_frame f = a.frames[i];
-        const uint8_t* p = COMPACT ? a.arena + a.frame_dst[i] : a.wire + f.hdr_off + f.hdr_len;
-        bool ok = true;
-        if (f.flags & WSC_FF_U8_PART) {
-            dfa = u8_run(dfa, p, f.payload_len);
-        } else if (f.flags & WSC_FF_U8_CHAIN) {
-            ok = u8_run(dfa, p, f.payload_len) == 0;
-        } else if (f.flags & WSC_FF_U8_SELF) {
-            ok = u8_run(0, p, f.payload_len) == 0;
-        } else if (f.flags & WSC_FF_U8_REASON) {
-            ok = u8_run(0, p + 2, f.payload_len - 2) == 0;
-        }
-        if (f.flags & WSC_FF_CONT_MSG) dfa = 0;   // continueBuffer consumed (frame.go:62-68)
-        if (!ok) { fail = i; break; }
-    }
-    wsc_conn_state o = a.state_out[s];
-    if (fail >= 0) {
-        wsc_frame f = a.frames[fail];
-        f.kind = WSC_FK_ERROR;
-        f.err = WSC_ERR_MUST_UTF8;
-        a.frames[fail] = f;
-        const uint32_t end = r.frame_begin + r.frame_count;
-        if constexpr (!COMPACT) {
-            // frames after the failing one were never reached by the reference: re-mask them
-            for (uint32_t j = (uint32_t)fail + 1; j < end; ++j) {
-                const wsc_frame g = a.frames[j];
-                if (!(g.flags & WSC_FF_UNMASKED)) continue;
-                uint8_t* q = a.wire + g.hdr_off + g.hdr_len;
-                for (uint32_t b = 0; b < g.payload_len; ++b) q[b] ^= (uint8_t)(g.mask >> (8 * (b & 3)));
-            }
-        }
-        r.frame_count = (uint32_t)fail - r.frame_begin + 1;
-        r.consumed = f.hdr_off + f.hdr_len + f.payload_len - a.seg_off[s];
-        r.status = WSC_SEG_ERROR;
-        r.close_code = 1007;
-        r.err = WSC_ERR_MUST_UTF8;
-        a.seg_out[s] = r;
-        o.status = WSC_SEG_ERROR;
-    } else {
-        o.cont_utf8 = o.cont_len ? (uint8_t)dfa : 0;
-    }
-    a.state_out[s] = o;
-}
-
 // explicit instantiations used by the host code
 template __global__ void k_walk_fused<false>(WalkArgs);
 template __global__ void k_walk_fused<true>(WalkArgs);
-template __global__ void k_unmask<false, 4, 0>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*);
-template __global__ void k_unmask<false, 4, 1>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*);
-template __global__ void k_unmask<false, 4, 2>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*);
-template __global__ void k_unmask<false, 4, 3>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*);
-template __global__ void k_unmask<false, 8, 0>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*);
-template __global__ void k_unmask<false, 8, 1>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*);
-template __global__ void k_unmask<false, 8, 2>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*);
-template __global__ void k_unmask<false, 8, 3>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*);
-template __global__ void k_unmask<false, 16, 0>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*);
-template __global__ void k_unmask<false, 16, 1>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*);
-template __global__ void k_unmask<false, 16, 2>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*);
-template __global__ void k_unmask<false, 16, 3>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*);
-template __global__ void k_unmask<true, 4, 0>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*);
-template __global__ void k_unmask<true, 4, 1>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*);
-template __global__ void k_unmask<true, 4, 2>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*);
-template __global__ void k_unmask<true, 4, 3>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*);
-template __global__ void k_unmask<true, 8, 0>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*);
-template __global__ void k_unmask<true, 8, 1>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*);
-template __global__ void k_unmask<true, 8, 2>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*);
-template __global__ void k_unmask<true, 8, 3>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*);
-template __global__ void k_unmask<true, 16, 0>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*);
-template __global__ void k_unmask<true, 16, 1>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*);
-template __global__ void k_unmask<true, 16, 2>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*);
-template __global__ void k_unmask<true, 16, 3>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*);
-template __global__ void k_utf8<false>(Utf8Args);
-template __global__ void k_utf8<true>(Utf8Args);
+template __global__ void k_unmask<false, 4, 0>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
+template __global__ void k_unmask<false, 4, 1>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
+template __global__ void k_unmask<false, 4, 2>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
+template __global__ void k_unmask<false, 4, 3>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
+template __global__ void k_unmask<false, 8, 0>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
+template __global__ void k_unmask<false, 8, 1>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
+template __global__ void k_unmask<false, 8, 2>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
+template __global__ void k_unmask<false, 8, 3>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
+template __global__ void k_unmask<false, 16, 0>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
+template __global__ void k_unmask<false, 16, 1>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
+template __global__ void k_unmask<false, 16, 2>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
+template __global__ void k_unmask<false, 16, 3>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
+template __global__ void k_unmask<true, 4, 0>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
+template __global__ void k_unmask<true, 4, 1>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
+template __global__ void k_unmask<true, 4, 2>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
+template __global__ void k_unmask<true, 4, 3>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
+template __global__ void k_unmask<true, 8, 0>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
+template __global__ void k_unmask<true, 8, 1>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
+template __global__ void k_unmask<true, 8, 2>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
+template __global__ void k_unmask<true, 8, 3>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
+template __global__ void k_unmask<true, 16, 0>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
+template __global__ void k_unmask<true, 16, 1>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
+template __global__ void k_unmask<true, 16, 2>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
+template __global__ void k_unmask<true, 16, 3>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
 
 }  // namespace wsc

@@ -67,23 +67,9 @@ struct WalkArgs {
     uint64_t* lb_incl;
     uint32_t* lb_err;            // bounded-spin timeout
     uint64_t* dbg;               // optional per-block timestamps (WSC_DEBUG_STAMPS=1)
+    uint32_t* u8info;            // per segment: {first utf8-failing frame ordinal, DFA state}
 };
 
 
-struct Utf8Args {
-    uint8_t* wire;
-    const uint8_t* arena;        // COMPACT
-    const uint64_t* frame_dst;   // COMPACT
-    const uint64_t* seg_off;
-    uint32_t n_segs;
-    const SegCount* counts;
-    const wsc_conn_state* state_in;
-    wsc_frame* frames;
-    wsc_conn_state* state_out;
-    wsc_seg_result* seg_out;
-    uint32_t* lb_ticket;
-    uint32_t* lb_flag;
-    uint32_t* lb_err;
-};
 
 }  // namespace wsc
