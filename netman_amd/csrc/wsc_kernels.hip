@@ -107,9 +107,178 @@ __device__ __forceinline__ void hdr_extract(const uint4& c0, const uint4& c1, ui
     for (int k = 0; k < 14; ++k) h[k] = (hd[k >> 2] >> (8 * (k & 3))) & 0xFFu;
 }
 
+// Output side of the walk: everything a frame writes (record, arena offset, span, window index)
+// and what a segment writes at its end.  Shared by the LDS replay and the re-walking emitter so
+// both produce identical outputs.
+struct EmitCtx {
+    uint32_t s;
+    uint64_t seg_start, seg_end;
+    uint64_t abase;          // COMPACT: this segment's arena offset
+    uint32_t sbase;          // first span index of this segment
+    uint32_t fbase;          // first frame index of this segment
+    uint64_t own_bytes0;     // COMPACT: data bytes of this segment (control payloads follow)
+    uint32_t own_spans0;
+    uint32_t nf, ns0, ns1;
+    uint64_t nb0, nb1;
+    uint64_t nx0, nx1;       // next window start not yet assigned, per region
+};
+
+template <bool COMPACT>
+__device__ __forceinline__ EmitCtx emit_begin(const WalkArgs& a, uint32_t s, uint64_t seg_start,
+                                              uint64_t seg_end, const SegCount& base, const SegCount& own) {
+    EmitCtx e;
+    e.s = s;
+    e.seg_start = seg_start;
+    e.seg_end = seg_end;
+    e.abase = base.bytes0 + base.bytes1;
+    e.sbase = base.spans0 + base.spans1;
+    e.fbase = base.frames;
+    e.own_bytes0 = own.bytes0;
+    e.own_spans0 = own.spans0;
+    e.nf = e.ns0 = e.ns1 = 0;
+    e.nb0 = e.nb1 = 0;
+    const uint64_t W = 1ull << a.win_shift;
+    if constexpr (COMPACT) {
+        e.nx0 = (e.abase + W - 1) & ~(W - 1);
+        e.nx1 = (e.abase + own.bytes0 + W - 1) & ~(W - 1);
+    } else {
+        e.nx0 = (seg_start + W - 1) & ~(W - 1);
+        e.nx1 = 0;
+    }
+    return e;
+}
+
+template <bool COMPACT>
+__device__ __forceinline__ void emit_frame(const WalkArgs& a, EmitCtx& e, const wsc_frame& fr, uint32_t plen,
+                                           bool have_span, uint32_t region) {
+    const uint64_t W = 1ull << a.win_shift;
+    const uint32_t fi = e.fbase + e.nf;
+    if (fi < a.frames_cap) {
+        // two 16-byte stores (the record is 32 B)
+        const uint4 r0 = make_uint4((uint32_t)fr.hdr_off, (uint32_t)(fr.hdr_off >> 32), fr.payload_len, fr.mask);
+        const uint4 r1 = make_uint4(fr.seg, fr.msg_id,
+                                    (uint32_t)fr.opcode | (uint32_t)fr.fin << 8 | (uint32_t)fr.kind << 16 |
+                                        (uint32_t)fr.mode << 24,
+                                    (uint32_t)fr.err | (uint32_t)fr.hdr_len << 8 | (uint32_t)fr.flags << 16);
+        reinterpret_cast<uint4*>(a.frames + fi)[0] = r0;
+        reinterpret_cast<uint4*>(a.frames + fi)[1] = r1;
+        if constexpr (COMPACT) {
+            uint64_t d = ~0ull;
+            if (fr.flags & WSC_FF_UNMASKED) d = region ? e.abase + e.own_bytes0 + e.nb1 : e.abase + e.nb0;
+            a.frame_dst[fi] = d;
+        }
+    }
+    if (have_span) {
+        Span sp;
+        sp.src = fr.hdr_off + fr.hdr_len;
+        sp.len = plen;
+        uint32_t idx;
+        if (COMPACT && region) {
+            sp.dst = e.abase + e.own_bytes0 + e.nb1;
+            idx = e.sbase + e.own_spans0 + e.ns1;
+        } else {
+            sp.dst = COMPACT ? e.abase + e.nb0 : sp.src;
+            idx = e.sbase + e.ns0;
+        }
+        sp.key = rotr32(fr.mask, 8u * ((uint32_t)(0u - (uint32_t)sp.dst) & 3u));
+        if (idx < a.spans_cap) a.spans[idx] = sp;
+        const uint64_t dend = sp.dst + plen;
+        uint64_t& nx = (COMPACT && region) ? e.nx1 : e.nx0;
+        if (nx < dend) {   // windows [nx, dend) start inside this span: consecutive entries
+            uint64_t t = nx >> a.win_shift;
+            const uint64_t t_end = ((dend - 1) >> a.win_shift) + 1;
+            nx = t_end << a.win_shift;
+            for (; t < t_end && (t & 3); ++t) a.tile_first[t] = idx;
+            const uint4 q = make_uint4(idx, idx, idx, idx);
+            for (; t + 4 <= t_end; t += 4) *reinterpret_cast<uint4*>(a.tile_first + t) = q;
+            for (; t < t_end; ++t) a.tile_first[t] = idx;
+        }
+        if (COMPACT && region) { e.ns1 += 1; e.nb1 += plen; }
+        else { e.ns0 += 1; e.nb0 += plen; }
+    }
+    e.nf += 1;
+}
+
+// the walk's final per-connection state (from the counting pass)
+struct WalkEnd {
+    uint64_t pos, cont;
+    uint32_t msg, mode, status, close_code, err, u8dfa;
+};
+
+template <bool COMPACT>
+__device__ __forceinline__ void emit_end(const WalkArgs& a, EmitCtx& e, const WalkEnd& w) {
+    const uint64_t W = 1ull << a.win_shift;
+    // windows that start in this segment's region(s) after its last span
+    if constexpr (COMPACT) {
+        const uint64_t e0 = e.abase + e.nb0, e1 = e0 + e.nb1;
+        for (; e.nx0 < e0; e.nx0 += W) a.tile_first[e.nx0 >> a.win_shift] = e.sbase + e.ns0;
+        for (; e.nx1 < e1; e.nx1 += W) a.tile_first[e.nx1 >> a.win_shift] = e.sbase + e.ns0 + e.ns1;
+    } else {
+        for (; e.nx0 < e.seg_end; e.nx0 += W) a.tile_first[e.nx0 >> a.win_shift] = e.sbase + e.ns0;
+    }
+    wsc_seg_result r;
+    r.consumed = w.pos - e.seg_start;
+    r.frame_begin = e.fbase;
+    r.frame_count = e.nf;
+    r.status = w.status;
+    r.close_code = w.close_code;
+    r.err = w.err;
+    r.pad = 0;
+    a.seg_out[e.s] = r;
+    wsc_conn_state o;
+    o.cont_len = w.cont;
+    o.msg_id = w.msg;
+    o.message_mode = (uint8_t)w.mode;
+    o.cont_utf8 = w.cont ? (uint8_t)w.u8dfa : 0;
+    o.status = (uint8_t)w.status;
+    o.pad = 0;
+    a.state_out[e.s] = o;
+}
+
+// Frames a lane keeps in LDS between its counting walk and its emission (16 B each); segments
+// with more frames are re-walked from the (cache-warm) wire instead.
+constexpr uint32_t KREC = 16;
+
+__device__ __forceinline__ uint4 rec_pack(const wsc_frame& fr, uint64_t seg_start, bool have_span,
+                                          uint32_t region, bool msg_inc) {
+    const uint32_t bits = (uint32_t)fr.opcode | (uint32_t)fr.fin << 4 | (uint32_t)fr.kind << 5 |
+                          (uint32_t)fr.mode << 8 | (uint32_t)fr.err << 10 | (uint32_t)fr.hdr_len << 13 |
+                          (uint32_t)fr.flags << 17 | region << 24 | (uint32_t)have_span << 25 |
+                          (uint32_t)msg_inc << 26;
+    return make_uint4((uint32_t)(fr.hdr_off - seg_start), fr.payload_len, fr.mask, bits);
+}
+
+template <bool COMPACT>
+__device__ __forceinline__ void emit_replay(const WalkArgs& a, uint32_t s, uint64_t seg_start, uint64_t seg_end,
+                                            const SegCount& base, const SegCount& own, const uint4* lrec,
+                                            uint32_t msg0, const WalkEnd& end) {
+    EmitCtx e = emit_begin<COMPACT>(a, s, seg_start, seg_end, base, own);
+    uint32_t msg = msg0;
+    for (uint32_t i = 0; i < own.frames; ++i) {
+        const uint4 r = lrec[i * 256];
+        wsc_frame fr;
+        fr.hdr_off = seg_start + r.x;
+        fr.payload_len = r.y;
+        fr.mask = r.z;
+        fr.seg = s;
+        fr.msg_id = msg;
+        fr.opcode = (uint8_t)(r.w & 0xF);
+        fr.fin = (uint8_t)((r.w >> 4) & 1);
+        fr.kind = (uint8_t)((r.w >> 5) & 7);
+        fr.mode = (uint8_t)((r.w >> 8) & 3);
+        fr.err = (uint8_t)((r.w >> 10) & 7);
+        fr.hdr_len = (uint8_t)((r.w >> 13) & 15);
+        fr.flags = (uint8_t)((r.w >> 17) & 0x7F);
+        fr.pad = 0;
+        if ((r.w >> 26) & 1) msg += 1;
+        emit_frame<COMPACT>(a, e, fr, r.y, (r.w >> 25) & 1, (r.w >> 24) & 1);
+    }
+    emit_end<COMPACT>(a, e, end);
+}
+
 template <bool EMIT, bool COMPACT>
 __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, const SegCount& base,
-                                                 const SegCount& own) {
+                                                 const SegCount& own, uint4* lrec, WalkEnd* wend) {
     const uint8_t* __restrict__ w = a.wire;
     const uint64_t seg_start = a.seg_off[s];
     const uint64_t seg_end = a.seg_off[s + 1];
@@ -121,22 +290,10 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
     uint32_t mode = st.message_mode;
     uint32_t status = st.status;
     uint32_t close_code = 0, err_out = 0;
-    const uint64_t abase = base.bytes0 + base.bytes1;   // COMPACT: this segment's arena offset
-    const uint32_t sbase = base.spans0 + base.spans1;   // first span index of this segment
     uint32_t nf = 0, ns0 = 0, ns1 = 0, sflags = 0;
     uint64_t nb0 = 0, nb1 = 0;
-
-    // window->span index bookkeeping (EMIT): next window start not yet assigned, per region
-    const uint64_t W = 1ull << a.win_shift;
-    uint64_t nx0 = 0, nx1 = 0;
-    if constexpr (EMIT) {
-        if constexpr (COMPACT) {
-            nx0 = (abase + W - 1) & ~(W - 1);
-            nx1 = (abase + own.bytes0 + W - 1) & ~(W - 1);
-        } else {
-            nx0 = (seg_start + W - 1) & ~(W - 1);
-        }
-    }
+    EmitCtx e{};
+    if constexpr (EMIT) e = emit_begin<COMPACT>(a, s, seg_start, seg_end, base, own);
 
     // UTF-8 verdicts are decided by the counting pass (payload read on the still-masked wire) and
     // replayed by the emitting pass: u8fail = ordinal of the first frame that fails, u8dfa = DFA
@@ -180,7 +337,6 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
         fr.flags = 0;
         fr.pad = 0;
 
-        bool emit_rec = true;
         uint64_t next = pos;
         bool have_span = false;
         uint32_t region = 0;
@@ -314,50 +470,18 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
         if (status == WSC_SEG_OPEN && seg_end - next >= 2) hdr_issue(w, a.n_bytes, next, hc0, hc1);
         if constexpr (COMPACT) if (region) fr.flags |= WSC_FF_CTRL_ARENA;
 
-        if (emit_rec) {
-            if constexpr (EMIT) {
-                const uint32_t fi = base.frames + nf;
-                if (fi < a.frames_cap) {
-                    a.frames[fi] = fr;
-                    if constexpr (COMPACT) {
-                        uint64_t d = ~0ull;
-                        if (fr.flags & WSC_FF_UNMASKED)
-                            d = region ? abase + own.bytes0 + nb1 : abase + nb0;
-                        a.frame_dst[fi] = d;
-                    }
-                }
-                if (have_span) {
-                    Span sp;
-                    sp.src = pos + fr.hdr_len;
-                    sp.len = (uint32_t)plen;
-                    uint32_t idx;
-                    if constexpr (COMPACT) {
-                        if (region) {
-                            sp.dst = abase + own.bytes0 + nb1;
-                            idx = sbase + own.spans0 + ns1;
-                        } else {
-                            sp.dst = abase + nb0;
-                            idx = sbase + ns0;
-                        }
-                    } else {
-                        sp.dst = sp.src;
-                        idx = sbase + ns0;
-                    }
-                    sp.key = rotr32(fr.mask, 8u * ((uint32_t)(0u - (uint32_t)sp.dst) & 3u));
-                    if (idx < a.spans_cap) a.spans[idx] = sp;
-                    const uint64_t dend = sp.dst + plen;
-                    uint64_t& nx = (COMPACT && region) ? nx1 : nx0;
-                    while (nx < dend) {
-                        a.tile_first[nx >> a.win_shift] = idx;
-                        nx += W;
-                    }
-                }
-            }
-            nf += 1;
-            if (have_span) {
-                if (COMPACT && region) { ns1 += 1; nb1 += plen; }
-                else { ns0 += 1; nb0 += plen; }
-            }
+        if constexpr (EMIT) {
+            emit_frame<COMPACT>(a, e, fr, (uint32_t)plen, have_span, region);
+        } else if (lrec && nf < KREC) {
+            const bool inc = fr.kind == WSC_FK_MESSAGE || fr.kind == WSC_FK_PING || fr.kind == WSC_FK_PONG ||
+                             (fr.kind == WSC_FK_ERROR && fr.err == WSC_ERR_MUST_UTF8 &&
+                              (fr.flags & (WSC_FF_U8_SELF | WSC_FF_U8_CHAIN)));
+            lrec[nf * 256] = rec_pack(fr, seg_start, have_span, region, inc);
+        }
+        nf += 1;
+        if (have_span) {
+            if (COMPACT && region) { ns1 += 1; nb1 += plen; }
+            else { ns0 += 1; nb0 += plen; }
         }
         pos = next;
     }
@@ -369,33 +493,11 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
         a.u8info[2 * s] = u8fail;
         a.u8info[2 * s + 1] = u8dfa;
     }
-    if constexpr (EMIT) {
-        // windows that start in this segment's region(s) after its last span
-        if constexpr (COMPACT) {
-            const uint64_t e0 = abase + nb0, e1 = e0 + nb1;
-            for (; nx0 < e0; nx0 += W) a.tile_first[nx0 >> a.win_shift] = sbase + ns0;
-            for (; nx1 < e1; nx1 += W) a.tile_first[nx1 >> a.win_shift] = sbase + ns0 + ns1;
-        } else {
-            for (; nx0 < seg_end; nx0 += W) a.tile_first[nx0 >> a.win_shift] = sbase + ns0;
-        }
-        wsc_seg_result r;
-        r.consumed = pos - seg_start;
-        r.frame_begin = base.frames;
-        r.frame_count = nf;
-        r.status = status;
-        r.close_code = close_code;
-        r.err = err_out;
-        r.pad = 0;
-        a.seg_out[s] = r;
-        wsc_conn_state o;
-        o.cont_len = cont;
-        o.msg_id = msg;
-        o.message_mode = (uint8_t)mode;
-        o.cont_utf8 = cont ? (uint8_t)u8dfa : 0;
-        o.status = (uint8_t)status;
-        o.pad = 0;
-        a.state_out[s] = o;
-    }
+    WalkEnd we;
+    we.pos = pos; we.cont = cont; we.msg = msg; we.mode = mode; we.status = status;
+    we.close_code = close_code; we.err = err_out; we.u8dfa = u8dfa;
+    if (wend) *wend = we;
+    if constexpr (EMIT) emit_end<COMPACT>(a, e, we);
     return c;
 }
 
@@ -446,6 +548,7 @@ __global__ __launch_bounds__(256) void k_walk_fused(WalkArgs a) {
     __shared__ uint32_t sh_bid;
     __shared__ SegCount sh_wave[4];
     __shared__ SegCount sh_prefix;
+    __shared__ uint4 sh_rec[KREC * 256];   // [frame ordinal][lane]: conflict-free 16 B per lane
     if (threadIdx.x == 0)
         sh_bid = __hip_atomic_fetch_add(a.lb_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
@@ -458,9 +561,12 @@ __global__ __launch_bounds__(256) void k_walk_fused(WalkArgs a) {
     uint64_t t0 = 0, t1 = 0, t2 = 0;
     if (a.dbg && threadIdx.x == 0) t0 = __builtin_amdgcn_s_memrealtime();
     SegCount own = zero;
+    WalkEnd wend = {};
+    uint32_t msg0 = 0;
     if (s < a.n_segs) {
-        own = walk_segment<false, COMPACT>(a, s, zero, zero);
+        own = walk_segment<false, COMPACT>(a, s, zero, zero, sh_rec + threadIdx.x, &wend);
         a.counts[s] = own;
+        msg0 = a.state_in ? a.state_in[s].msg_id : 0u;
     }
     // block-wide scan (64-lane shuffles, then across the 4 waves)
     SegCount inc = own;
@@ -538,7 +644,12 @@ __global__ __launch_bounds__(256) void k_walk_fused(WalkArgs a) {
     __syncthreads();
     if (a.dbg && threadIdx.x == 0) t2 = __builtin_amdgcn_s_memrealtime();
     const SegCount base = sc_add(sh_prefix, sc_add(wpre, excl));
-    if (s < a.n_segs) walk_segment<true, COMPACT>(a, s, base, own);
+    if (s < a.n_segs) {
+        if (own.frames <= KREC)   // replay from LDS: no second dependent walk, no loads at all
+            emit_replay<COMPACT>(a, s, a.seg_off[s], a.seg_off[s + 1], base, own, sh_rec + threadIdx.x, msg0, wend);
+        else                      // long segment: re-walk the (cache-warm) headers
+            walk_segment<true, COMPACT>(a, s, base, own, nullptr, nullptr);
+    }
     if (a.dbg) {   // diagnostic timestamps (100 MHz s_memrealtime), written only to the dbg buffer
         __syncthreads();
         if (threadIdx.x == 0) {
