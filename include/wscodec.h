@@ -154,7 +154,7 @@ typedef struct wsc_config {
     uint32_t unmask_window;    /* bytes per wave-window in the unmask kernel (0 = default)       */
     uint32_t unmask_waves_per_cu; /* unmask grid sizing (0 = default)                            */
     uint32_t unmask_nt;        /* bit0: non-temporal payload loads, bit1: non-temporal stores     */
-    uint32_t pad;
+    uint32_t unmask_minw;      /* occupancy hint for the unmask kernel: 0/1 none, 2/4/8 min waves per SIMD */
 } wsc_config;
 
 typedef struct wsc_ctx wsc_ctx;

@@ -54,7 +54,7 @@ assert SEG_RESULT_DTYPE.itemsize == 32 and SUMMARY_DTYPE.itemsize == 32
 class WscConfig(C.Structure):
     _fields_ = [("max_batch_bytes", C.c_uint64), ("max_segs", C.c_uint32), ("max_frames", C.c_uint32),
                 ("max_frame_len", C.c_uint64), ("unmask_window", C.c_uint32),
-                ("unmask_waves_per_cu", C.c_uint32), ("unmask_nt", C.c_uint32), ("pad", C.c_uint32)]
+                ("unmask_waves_per_cu", C.c_uint32), ("unmask_nt", C.c_uint32), ("unmask_minw", C.c_uint32)]
 
 
 class WscBatch(C.Structure):

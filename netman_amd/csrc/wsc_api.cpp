@@ -12,7 +12,7 @@
 
 namespace wsc {
 template <bool COMPACT> __global__ void k_walk_fused(WalkArgs);
-template <bool COMPACT, int P, int NT>
+template <bool COMPACT, int P, int NT, int MINW>
 __global__ void k_unmask(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*,
                          const wsc_summary*, uint32_t*, uint32_t);
 }  // namespace wsc
@@ -253,14 +253,20 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
                         const wsc_summary*, uint32_t*, uint32_t);
     // [compact][pieces 4/8/16][nt 0..3]
     static const UK table[2][3][4] = {
-        {{k_unmask<false, 4, 0>, k_unmask<false, 4, 1>, k_unmask<false, 4, 2>, k_unmask<false, 4, 3>},
-         {k_unmask<false, 8, 0>, k_unmask<false, 8, 1>, k_unmask<false, 8, 2>, k_unmask<false, 8, 3>},
-         {k_unmask<false, 16, 0>, k_unmask<false, 16, 1>, k_unmask<false, 16, 2>, k_unmask<false, 16, 3>}},
-        {{k_unmask<true, 4, 0>, k_unmask<true, 4, 1>, k_unmask<true, 4, 2>, k_unmask<true, 4, 3>},
-         {k_unmask<true, 8, 0>, k_unmask<true, 8, 1>, k_unmask<true, 8, 2>, k_unmask<true, 8, 3>},
-         {k_unmask<true, 16, 0>, k_unmask<true, 16, 1>, k_unmask<true, 16, 2>, k_unmask<true, 16, 3>}}};
+        {{k_unmask<false, 4, 0, 1>, k_unmask<false, 4, 1, 1>, k_unmask<false, 4, 2, 1>, k_unmask<false, 4, 3, 1>},
+         {k_unmask<false, 8, 0, 1>, k_unmask<false, 8, 1, 1>, k_unmask<false, 8, 2, 1>, k_unmask<false, 8, 3, 1>},
+         {k_unmask<false, 16, 0, 1>, k_unmask<false, 16, 1, 1>, k_unmask<false, 16, 2, 1>, k_unmask<false, 16, 3, 1>}},
+        {{k_unmask<true, 4, 0, 1>, k_unmask<true, 4, 1, 1>, k_unmask<true, 4, 2, 1>, k_unmask<true, 4, 3, 1>},
+         {k_unmask<true, 8, 0, 1>, k_unmask<true, 8, 1, 1>, k_unmask<true, 8, 2, 1>, k_unmask<true, 8, 3, 1>},
+         {k_unmask<true, 16, 0, 1>, k_unmask<true, 16, 1, 1>, k_unmask<true, 16, 2, 1>, k_unmask<true, 16, 3, 1>}}};
     const int pi = c->pieces == 4 ? 0 : (c->pieces == 8 ? 1 : 2);
-    const UK kern = table[compact ? 1 : 0][pi][c->cfg.unmask_nt & 3];
+    UK kern = table[compact ? 1 : 0][pi][c->cfg.unmask_nt & 3];
+    // occupancy variants (launch_bounds minimum waves per SIMD) for the tuned in-place kernels
+    static const UK occ[2][3] = {{k_unmask<false, 4, 3, 2>, k_unmask<false, 4, 3, 4>, k_unmask<false, 4, 3, 8>},
+                                 {k_unmask<false, 8, 3, 2>, k_unmask<false, 8, 3, 4>, k_unmask<false, 8, 3, 8>}};
+    const uint32_t mw = c->cfg.unmask_minw;
+    if (!compact && (c->cfg.unmask_nt & 3) == 3 && pi < 2 && (mw == 2 || mw == 4 || mw == 8))
+        kern = occ[pi][mw == 2 ? 0 : (mw == 4 ? 1 : 2)];
     hipLaunchKernelGGL(kern, ugrid, ublk, 0, st, udst, (const uint8_t*)b->wire, b->n_bytes, udst_bytes,
                        (const Span*)c->spans, (const uint32_t*)c->tile, (const wsc_summary*)b->summary,
                        c->lb_state, (n + 255) / 256);

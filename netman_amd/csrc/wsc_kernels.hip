@@ -824,8 +824,8 @@ __device__ __attribute__((noinline)) void unmask_window_general(
 
 // NT bit 0: non-temporal loads, bit 1: non-temporal stores.  In place, `src` is unused (dst is
 // both source and destination) so the two restrict pointers never alias in an access.
-template <bool COMPACT, int P, int NT>
-__global__ __launch_bounds__(256) void k_unmask(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src,
+template <bool COMPACT, int P, int NT, int MINW = 1>
+__global__ __launch_bounds__(256, MINW) void k_unmask(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src,
                                                 uint64_t src_bytes, uint64_t dst_bytes_host,
                                                 const Span* __restrict__ spans,
                                                 const uint32_t* __restrict__ tile_first,
@@ -879,55 +879,59 @@ __global__ __launch_bounds__(256) void k_unmask(uint8_t* __restrict__ dst, const
             }
             continue;
         }
-        // several spans overlap the window (small frames) or it holds a frame edge
-        u32x4 key[P];
-        uint32_t cov = 0;
+        // Several spans overlap the window (small frames) or it holds a frame edge.  Each 1 KiB
+        // sub-window k (one wave instruction) is finished before the next, so only one piece's key
+        // is live at a time; the span cursor only moves forward (spans are sorted by dst).
 #pragma unroll
         for (int k = 0; k < P; ++k) {
-            key[k] = u32x4{0, 0, 0, 0};
-            if constexpr (COMPACT) v[k] = u32x4{0, 0, 0, 0};
-        }
-        while (sp.dst < wbase + WB) {
-            const uint64_t d0 = sp.dst, d1 = sp.dst + sp.len;
-#pragma unroll
-            for (int k = 0; k < P; ++k) {
-                const uint64_t pa = wbase + k * 1024u + lofs;
-                const uint64_t lo = d0 > pa ? d0 : pa;
+            const uint64_t sb = wbase + k * 1024u;
+            const uint64_t pa = sb + lofs;
+            while (r < n_spans && sp.dst + sp.len <= sb) {   // spans that end before this sub-window
+                ++r;
+                if (r < n_spans) sp = spans[r];
+            }
+            u32x4 key = {0, 0, 0, 0};
+            u32x4 sv = {0, 0, 0, 0};
+            bool cov = false;
+            Span q = sp;
+            for (uint32_t qi = r; qi < n_spans && q.dst < sb + 1024u;) {
+                const uint64_t lo = q.dst > pa ? q.dst : pa;
+                const uint64_t d1 = q.dst + q.len;
                 const uint64_t hi = d1 < pa + 16 ? d1 : pa + 16;
                 if (lo < hi) {
                     const uint32_t bl = (uint32_t)(lo - pa), bh = (uint32_t)(hi - pa);
-                    uint32_t m[4];
+                    u32x4 m;
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
                         const uint32_t l = bl > 4u * j ? bl - 4u * j : 0u;
                         const uint32_t hh = bh > 4u * j ? bh - 4u * j : 0u;
                         m[j] = l < hh ? bytes_to_mask(l, hh > 4 ? 4 : hh) : 0u;
                     }
-                    key[k].x |= sp.key & m[0];
-                    key[k].y |= sp.key & m[1];
-                    key[k].z |= sp.key & m[2];
-                    key[k].w |= sp.key & m[3];
-                    cov |= 1u << k;
+                    key |= q.key & m;
+                    cov = true;
                     if constexpr (COMPACT) {
-                        const int64_t so = (int64_t)sp.src + ((int64_t)pa - (int64_t)sp.dst);
-                        const uint4 sv = load16_unaligned(src, so, src_bytes);
-                        v[k].x |= sv.x & m[0];
-                        v[k].y |= sv.y & m[1];
-                        v[k].z |= sv.z & m[2];
-                        v[k].w |= sv.w & m[3];
+                        const int64_t so = (int64_t)q.src + ((int64_t)pa - (int64_t)q.dst);
+                        const uint4 t = load16_unaligned(src, so, src_bytes);
+                        sv |= u32x4{t.x, t.y, t.z, t.w} & m;
                     }
                 }
+                if (++qi < n_spans) q = spans[qi]; else break;
             }
-            if (++r >= n_spans) break;
-            sp = spans[r];
+            if (cov) {
+                if constexpr (COMPACT) st16v<NT>(dst + pa, sv ^ key);
+                else st16v<NT>(dst + pa, v[k] ^ key);
+            }
         }
-#pragma unroll
-        for (int k = 0; k < P; ++k)
-            if (cov & (1u << k)) st16v<NT>(dst + wbase + k * 1024u + lofs, v[k] ^ key[k]);
     }
 }
 
 // explicit instantiations used by the host code
+template __global__ void k_unmask<false, 4, 3, 2>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
+template __global__ void k_unmask<false, 4, 3, 4>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
+template __global__ void k_unmask<false, 4, 3, 8>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
+template __global__ void k_unmask<false, 8, 3, 2>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
+template __global__ void k_unmask<false, 8, 3, 4>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
+template __global__ void k_unmask<false, 8, 3, 8>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
 template __global__ void k_walk_fused<false>(WalkArgs);
 template __global__ void k_walk_fused<true>(WalkArgs);
 template __global__ void k_unmask<false, 4, 0>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);

@@ -21,6 +21,7 @@ ap.add_argument("--rounds", type=int, default=3)
 ap.add_argument("--windows", default="4096,8192,16384")
 ap.add_argument("--wpc", default="8,16,32,4096")
 ap.add_argument("--nt", default="0,1,2,3")
+ap.add_argument("--minw", default="0")
 a = ap.parse_args()
 
 if a.workload == "64k":
@@ -42,12 +43,12 @@ summ = torch.zeros(32, dtype=torch.uint8, device=dev)
 hdr = np.where(cfg["plen"] <= 125, 6, np.where(cfg["plen"] <= 65535, 8, 14))
 alg = int((2 * cfg["plen"].astype(np.int64) + hdr + 32).sum())
 combos = list(itertools.product([int(x) for x in a.windows.split(",")], [int(x) for x in a.wpc.split(",")],
-                                [int(x) for x in a.nt.split(",")]))
+                                [int(x) for x in a.nt.split(",")], [int(x) for x in a.minw.split(",")]))
 codecs = {}
-for w, wpc, nt in combos:
-    codecs[(w, wpc, nt)] = K.Codec(0, max_batch_bytes=len(cfg["wire"]) + 4096, max_segs=n_segs,
-                                   max_frames=cfg["n_frames"] + 16, unmask_window=w,
-                                   unmask_waves_per_cu=wpc, unmask_nt=nt)
+for w, wpc, nt, mw in combos:
+    codecs[(w, wpc, nt, mw)] = K.Codec(0, max_batch_bytes=len(cfg["wire"]) + 4096, max_segs=n_segs,
+                                       max_frames=cfg["n_frames"] + 16, unmask_window=w,
+                                       unmask_waves_per_cu=wpc, unmask_nt=nt, unmask_minw=mw)
 res = {c: [] for c in combos}
 for r in range(a.rounds):
     for c in combos:
@@ -63,8 +64,8 @@ for c in combos:
 rows.sort()
 print(f"workload={a.workload} payload={cfg['payload_bytes']} alg_bytes={alg}")
 for um, c, tot in rows:
-    print(f"window={c[0]:6d} wpc={c[1]:5d} nt={c[2]}  unmask {um*1e3:8.1f} us  {alg/um/1e6:8.1f} GB/s  "
+    print(f"window={c[0]:6d} wpc={c[1]:5d} nt={c[2]} minw={c[3]}  unmask {um*1e3:8.1f} us  {alg/um/1e6:8.1f} GB/s  "
           f"total {tot*1e3:8.1f} us  payload {cfg['payload_bytes']/tot/1e6/1.073741824:8.1f} GiB/s")
 best = rows[0]
 print(json.dumps({"workload": a.workload, "best": {"window": best[1][0], "wpc": best[1][1], "nt": best[1][2],
-                                                   "unmask_us": best[0] * 1e3}}))
+                                                   "minw": best[1][3], "unmask_us": best[0] * 1e3}}))
