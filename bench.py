@@ -42,6 +42,8 @@ def parse():
     ap.add_argument("--no-host-inclusive", action="store_true")
     ap.add_argument("--window", type=int, default=0, help="unmask window bytes (0 = library default)")
     ap.add_argument("--waves-per-cu", type=int, default=0)
+    ap.add_argument("--no-other-configs", action="store_true",
+                    help="skip the device-time lines for BASELINE.json configs[1], [2], [4]")
     return ap.parse_args()
 
 
@@ -182,6 +184,11 @@ def main():
     }
     if rank == 0 and not a.no_host_inclusive:
         out["host_inclusive"] = host_inclusive(codec, cfg, K)
+    codec.close()
+    if rank == 0 and not a.no_other_configs:
+        del wire, frames, st_out, seg_out
+        torch.cuda.empty_cache()
+        out["other_configs"] = other_configs(torch, K, synth)
     if rank == 0 and not a.no_cpu and a.cpu_seconds > 0:
         threads = min(16, len(os.sched_getaffinity(0)))
         v1, p1, e1 = cpu_baseline(cfg, a.cpu_seconds / 2, 1)
@@ -194,7 +201,43 @@ def main():
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()
-    codec.close()
+
+
+def other_configs(torch, K, synth):
+    """Device time of the full decode for the other single-GPU BASELINE.json configs (hipEvents,
+    median of 10), reported beside the headline; parity for each is in tests/test_gpu_parity.py."""
+    dev = torch.device("cuda", torch.cuda.current_device())
+    res = {}
+    cases = [("configs[1] 1M x 1 KiB BIN, 16 frames/segment", lambda: synth.uniform_batch(1 << 20, 1024, 16, seed=synth.SEED_BASE + 1), False),
+             ("configs[2] 256k mixed 125 B / 64 KiB / 1 MiB (p~1/size)", lambda: synth.mixed_batch(), False),
+             ("configs[4] 64k connections x fragmented message, reassembled (COMPACT)", lambda: synth.fragmented_batch(), True)]
+    for name, make, compact in cases:
+        cfg = make()
+        n = len(cfg["seg_off"]) - 1
+        c = K.Codec(dev.index, max_batch_bytes=len(cfg["wire"]) + 4096, max_segs=n, max_frames=cfg["n_frames"] + 16)
+        t = dict(wire=torch.from_numpy(cfg["wire"]).to(dev), seg_off=torch.from_numpy(cfg["seg_off"].view(np.int64)).to(dev),
+                 st=torch.zeros(n * 16, dtype=torch.uint8, device=dev), so=torch.zeros(n * 32, dtype=torch.uint8, device=dev),
+                 fr=torch.zeros((cfg["n_frames"] + 16) * 32, dtype=torch.uint8, device=dev),
+                 sm=torch.zeros(32, dtype=torch.uint8, device=dev))
+        if compact:
+            t["arena"] = torch.zeros(len(cfg["wire"]) + 64, dtype=torch.uint8, device=dev)
+            t["fd"] = torch.zeros(cfg["n_frames"] + 16, dtype=torch.int64, device=dev)
+        b = c.make_batch(t["wire"], t["seg_off"], None, t["st"], t["so"], t["fr"], t["sm"], compact=compact,
+                         arena=t.get("arena"), frame_dst=t.get("fd"))
+        c.decode(b)
+        torch.cuda.synchronize()
+        p = [c.profile(b, 1) for _ in range(10)]
+        tot = float(np.median([q["total"] for q in p]))
+        um = float(np.median([q["unmask"] for q in p]))
+        hdr = np.where(cfg["plen"] <= 125, 6, np.where(cfg["plen"] <= 65535, 8, 14))
+        alg = int((2 * cfg["plen"].astype(np.int64) + hdr + 32).sum())
+        res[name] = {"gib_s": round(cfg["payload_bytes"] / (tot * 1e-3) / 2**30, 1), "ms": round(tot, 4),
+                     "unmask_ms": round(um, 4), "unmask_gb_s": round(alg / (um * 1e-3) / 1e9, 1),
+                     "frames": int(cfg["n_frames"]), "payload_bytes": int(cfg["payload_bytes"])}
+        c.close()
+        del t
+        torch.cuda.empty_cache()
+    return res
 
 
 def host_inclusive(codec, cfg, K):

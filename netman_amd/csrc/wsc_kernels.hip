@@ -276,6 +276,17 @@ __device__ __forceinline__ void emit_replay(const WalkArgs& a, uint32_t s, uint6
     emit_end<COMPACT>(a, e, end);
 }
 
+// Walk one segment's frames (one lane).  Pass 1 (EMIT=false) counts, decides utf8 verdicts and
+// keeps up to KREC frame records in LDS; pass 2 (EMIT=true, only for segments with more frames)
+// re-walks and writes every output at the offsets `base` (exclusive prefix over segments).
+//
+// The header chain is serial, so the walk fetches SPEC_D headers per memory round trip: the
+// next header and the ones at +stride, +2*stride, ... (stride = the last frame's size).  A
+// speculative header is used only when its address is the real next position, so results never
+// depend on the guess; frames that repeat their size (the common case on one connection) cost
+// one round trip per SPEC_D frames.  All loads of a round are waited together.
+constexpr int SPEC_D = 4;
+
 template <bool EMIT, bool COMPACT>
 __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, const SegCount& base,
                                                  const SegCount& own, uint4* lrec, WalkEnd* wend) {
@@ -306,14 +317,12 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
     }
 
     uint64_t pos = seg_start;
-    // The header of the next frame is loaded as soon as its position is known, before this
-    // frame's record stores are issued: vmcnt counts loads and stores in order, so a load issued
-    // after the stores would also wait for them.
-    uint4 hc0 = make_uint4(0, 0, 0, 0), hc1 = make_uint4(0, 0, 0, 0);
-    if (status == WSC_SEG_OPEN && seg_end - pos >= 2) hdr_issue(w, a.n_bytes, pos, hc0, hc1);
-    while (status == WSC_SEG_OPEN) {
+
+    // One frame at `pos` from its 32-byte header window; returns false when the walk stops
+    // (terminal status, or the frame is incomplete and is carried to the next batch).
+    auto step = [&](const uint4& hc0, const uint4& hc1) -> bool {
         const uint64_t avail = seg_end - pos;
-        if (avail < 2) break;
+        if (avail < 2) return false;
         uint32_t h[14];
         hdr_extract(hc0, hc1, pos, h);
         const uint32_t fin = h[0] >> 7;
@@ -350,7 +359,7 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
             const uint32_t mode_h = (op == 1 || op == 2) ? op : mode;   // :234-236
             fr.mode = (uint8_t)mode_h;
             const uint32_t ext = len7 == 126 ? 2 : (len7 == 127 ? 8 : 0);
-            if (avail < 2 + ext) break;                                  // wait for the length
+            if (avail < 2 + ext) return false;                           // wait for the length
             if (ext == 2) plen = (h[2] << 8) | h[3];
             else if (ext == 8) {
                 plen = 0;
@@ -364,7 +373,7 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
                 next = pos + 2 + ext;
             } else {
                 const uint32_t hl = 2 + ext + 4;
-                if (avail < hl) break;                                   // wait for the mask
+                if (avail < hl) return false;                            // wait for the mask
                 uint32_t mask = 0;
                 if (ext == 0) mask = h[2] | h[3] << 8 | h[4] << 16 | h[5] << 24;
                 else if (ext == 2) mask = h[4] | h[5] << 8 | h[6] << 16 | h[7] << 24;
@@ -375,37 +384,37 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
                 const uint64_t pstart = pos + hl;
 
                 // opcode switch, websocket.go:136-208
-                uint32_t e = 0, kind = WSC_FK_ERROR;
+                uint32_t err = 0, kind = WSC_FK_ERROR;
                 bool payload = false;
                 if (op == 0) {
-                    if (mode_h < 1) e = WSC_ERR_OPCODE_FAIL;
+                    if (mode_h < 1) err = WSC_ERR_OPCODE_FAIL;
                     else { payload = true; kind = fin ? WSC_FK_MESSAGE : WSC_FK_FRAG; }
                 } else if (op == 1 || op == 2) {
-                    if (cont >= 1) e = WSC_ERR_PING_PAYLOAD_OVERSIZE;
+                    if (cont >= 1) err = WSC_ERR_PING_PAYLOAD_OVERSIZE;
                     else { payload = true; kind = fin ? WSC_FK_MESSAGE : WSC_FK_FRAG; }
                 } else if (op == 8) {
-                    if (!(plen == 0 || plen >= 2) || plen > 125) e = WSC_ERR_PROTOCOL_ERROR;
+                    if (!(plen == 0 || plen >= 2) || plen > 125) err = WSC_ERR_PROTOCOL_ERROR;
                     else if (plen == 0) kind = WSC_FK_CLOSE;
                     else { payload = true; kind = fin ? WSC_FK_CLOSE : WSC_FK_FRAG; }
                 } else if (op == 9) {
-                    if (fin != 1) e = WSC_ERR_CTRL_FRAGMENTED;
-                    else if (plen > 125) e = WSC_ERR_PING_PAYLOAD_OVERSIZE;     // ctrl.go:130-132
+                    if (fin != 1) err = WSC_ERR_CTRL_FRAGMENTED;
+                    else if (plen > 125) err = WSC_ERR_PING_PAYLOAD_OVERSIZE;   // ctrl.go:130-132
                     else { payload = true; kind = WSC_FK_PING; }
                 } else if (op == 10) {
-                    if (fin != 1) e = WSC_ERR_CTRL_FRAGMENTED;
+                    if (fin != 1) err = WSC_ERR_CTRL_FRAGMENTED;
                     else if (plen == 0) kind = WSC_FK_PONG_EMPTY;
                     else { payload = true; kind = WSC_FK_PONG; }
                 } else {
-                    e = WSC_ERR_OPCODE_FAIL;
+                    err = WSC_ERR_OPCODE_FAIL;
                 }
-                if (payload && !e) {
-                    if (plen > a.max_frame_len) e = WSC_ERR_TOO_LARGE;          // Q4
-                    else if (avail < hl + plen) break;                           // wait for payload
+                if (payload && !err) {
+                    if (plen > a.max_frame_len) err = WSC_ERR_TOO_LARGE;        // Q4
+                    else if (avail < hl + plen) return false;                    // wait for payload
                 }
-                next = pstart + (payload && !e ? plen : 0);
-                if (e) {
-                    fr.err = (uint8_t)e;
-                    status = WSC_SEG_ERROR; close_code = 1002; err_out = e;
+                next = pstart + (payload && !err ? plen : 0);
+                if (err) {
+                    fr.err = (uint8_t)err;
+                    status = WSC_SEG_ERROR; close_code = 1002; err_out = err;
                     next = pstart;
                 } else {
                     fr.kind = (uint8_t)kind;
@@ -467,15 +476,12 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
             }
         }
         if constexpr (!EMIT) if (fr.flags & WSC_FF_CONT_MSG) u8dfa = 0;   // continueBuffer consumed
-        if (status == WSC_SEG_OPEN && seg_end - next >= 2) hdr_issue(w, a.n_bytes, next, hc0, hc1);
         if constexpr (COMPACT) if (region) fr.flags |= WSC_FF_CTRL_ARENA;
 
         if constexpr (EMIT) {
             emit_frame<COMPACT>(a, e, fr, (uint32_t)plen, have_span, region);
         } else if (lrec && nf < KREC) {
-            const bool inc = fr.kind == WSC_FK_MESSAGE || fr.kind == WSC_FK_PING || fr.kind == WSC_FK_PONG ||
-                             (fr.kind == WSC_FK_ERROR && fr.err == WSC_ERR_MUST_UTF8 &&
-                              (fr.flags & (WSC_FF_U8_SELF | WSC_FF_U8_CHAIN)));
+            const bool inc = fr.kind == WSC_FK_MESSAGE || fr.kind == WSC_FK_PING || fr.kind == WSC_FK_PONG;
             lrec[nf * 256] = rec_pack(fr, seg_start, have_span, region, inc);
         }
         nf += 1;
@@ -484,6 +490,30 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
             else { ns0 += 1; nb0 += plen; }
         }
         pos = next;
+        return status == WSC_SEG_OPEN;
+    };
+
+    uint64_t stride = 0;
+    bool go = status == WSC_SEG_OPEN;
+    while (go) {
+        // one memory round trip: the next header + SPEC_D-1 speculative ones
+        uint4 hc0[SPEC_D], hc1[SPEC_D];
+        uint64_t hp[SPEC_D];
+#pragma unroll
+        for (int k = 0; k < SPEC_D; ++k) {
+            hp[k] = pos + (uint64_t)k * stride;
+            hc0[k] = make_uint4(0, 0, 0, 0);
+            hc1[k] = hc0[k];
+            if (k == 0 || (stride != 0 && hp[k] + 2 <= seg_end)) hdr_issue(w, a.n_bytes, hp[k], hc0[k], hc1[k]);
+            else hp[k] = ~0ull;
+        }
+#pragma unroll
+        for (int k = 0; k < SPEC_D; ++k) {
+            if (!go || hp[k] != pos) break;   // speculation ran out or missed: next round trip
+            const uint64_t p0 = pos;
+            go = step(hc0[k], hc1[k]);
+            stride = pos - p0;
+        }
     }
 
     SegCount c;
