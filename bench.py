@@ -82,10 +82,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU; WSC_BENCH_BACKEND=gloo + a shared device is only for rehearsing the
+    # N>1 control path on a 1-GPU box (the driver's N>1 runs use RCCL, one GPU per rank)
+    backend = os.environ.get("WSC_BENCH_BACKEND", "nccl")
+    local = local % max(1, torch.cuda.device_count())
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
+    cdev = dev if backend == "nccl" else torch.device("cpu")   # where the timing collectives live
 
     from netman_amd import codec as K
     from netman_amd import synth
@@ -133,10 +141,10 @@ def main():
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        t = torch.tensor([el], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-        okt = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+        okt = torch.tensor([1 if ok else 0], dtype=torch.int32, device=cdev)
         dist.all_reduce(okt, op=dist.ReduceOp.MIN)
         ok = bool(okt.item())
 
