@@ -61,7 +61,7 @@ __device__ __forceinline__ uint32_t u8_step(uint32_t s, uint32_t b) {
 
 // Run the DFA over n payload bytes that are still MASKED on the wire: byte i of the payload is
 // w[p + i] ^ (mask >> 8*(i & 3)).  4-byte ASCII groups are skipped while between characters.
-__device__ uint32_t u8_run_masked(uint32_t s, const uint8_t* __restrict__ w, uint64_t p, uint64_t n,
+__device__ __attribute__((noinline)) uint32_t u8_run_masked(uint32_t s, const uint8_t* __restrict__ w, uint64_t p, uint64_t n,
                                   uint32_t mask) {
     uint64_t i = 0;
     while (i < n && s != 8) {
@@ -507,12 +507,21 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
             if (k == 0 || (stride != 0 && hp[k] + 2 <= seg_end)) hdr_issue(w, a.n_bytes, hp[k], hc0[k], hc1[k]);
             else hp[k] = ~0ull;
         }
-#pragma unroll
+        // consume the round's headers in order from the front of the queue; one copy of `step`
+        // in the code (an unrolled consumer made the walk ~20k instructions: instruction-cache bound)
+#pragma unroll 1
         for (int k = 0; k < SPEC_D; ++k) {
-            if (!go || hp[k] != pos) break;   // speculation ran out or missed: next round trip
+            if (!go || hp[0] != pos) break;   // speculation ran out or missed: next round trip
             const uint64_t p0 = pos;
-            go = step(hc0[k], hc1[k]);
+            go = step(hc0[0], hc1[0]);
             stride = pos - p0;
+#pragma unroll
+            for (int q = 0; q + 1 < SPEC_D; ++q) {
+                hc0[q] = hc0[q + 1];
+                hc1[q] = hc1[q + 1];
+                hp[q] = hp[q + 1];
+            }
+            hp[SPEC_D - 1] = ~0ull;
         }
     }
 

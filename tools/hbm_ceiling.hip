@@ -1,0 +1,135 @@
+// Achievable-HBM microbenchmark for the unmask's access pattern on one MI355X (gfx950).
+// Measures, on a 1 GiB buffer, the rate of plain streaming kernels that do no span lookup at all:
+//   xor_inplace<P>  : the k_unmask fast path alone (P x 16 B per lane, one P KiB window per wave,
+//                     non-temporal loads/stores), read + write of every byte;
+//   copy            : float4 copy src -> dst (the guide's 6.29 TB/s reference pattern);
+//   read_only       : 16 B per lane loads reduced to one dword per wave;
+//   write_only      : 16 B per lane non-temporal stores.
+// It gives the ceiling k_unmask is measured against besides the 8.0 TB/s spec.
+// Build: hipcc --offload-arch=gfx950 -O3 -o tools/hbm_ceiling tools/hbm_ceiling.hip
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+#define CK(x)                                                                              \
+    do {                                                                                   \
+        hipError_t e_ = (x);                                                               \
+        if (e_ != hipSuccess) {                                                            \
+            fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_));      \
+            exit(1);                                                                       \
+        }                                                                                  \
+    } while (0)
+
+template <int P>
+__global__ __launch_bounds__(256) void xor_inplace(uint8_t* __restrict__ buf, uint64_t n_win, uint32_t key) {
+    const uint64_t w = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (w >= n_win) return;
+    const uint64_t base = w * (1024u * P) + (threadIdx.x & 63) * 16u;
+    u32x4 v[P];
+#pragma unroll
+    for (int k = 0; k < P; ++k) v[k] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(buf + base + k * 1024u));
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+        v[k] ^= key;
+        __builtin_nontemporal_store(v[k], reinterpret_cast<u32x4*>(buf + base + k * 1024u));
+    }
+}
+
+__global__ __launch_bounds__(256) void copy16(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, uint64_t n16) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n16) reinterpret_cast<float4*>(dst)[i] = reinterpret_cast<const float4*>(src)[i];
+}
+
+template <int P>
+__global__ __launch_bounds__(256) void read_only(const uint8_t* __restrict__ buf, uint64_t n_win, uint32_t* out) {
+    const uint64_t w = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (w >= n_win) return;
+    const uint64_t base = w * (1024u * P) + (threadIdx.x & 63) * 16u;
+    u32x4 acc = {0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < P; ++k) acc ^= __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(buf + base + k * 1024u));
+    const uint32_t r = acc.x ^ acc.y ^ acc.z ^ acc.w;
+    if (r == 0x9E3779B9u) out[0] = r;   // practically never: keeps the loads alive
+}
+
+template <int P>
+__global__ __launch_bounds__(256) void write_only(uint8_t* __restrict__ buf, uint64_t n_win, uint32_t key) {
+    const uint64_t w = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (w >= n_win) return;
+    const uint64_t base = w * (1024u * P) + (threadIdx.x & 63) * 16u;
+    const u32x4 v = {key, key + 1, key + 2, key + 3};
+#pragma unroll
+    for (int k = 0; k < P; ++k) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(buf + base + k * 1024u));
+}
+
+template <typename F>
+static void timeit(const char* name, double bytes, F&& launch, int iters = 30) {
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    for (int i = 0; i < 3; ++i) launch();
+    CK(hipDeviceSynchronize());
+    std::vector<float> ms;
+    for (int i = 0; i < iters; ++i) {
+        CK(hipEventRecord(a, 0));
+        launch();
+        CK(hipEventRecord(b, 0));
+        CK(hipEventSynchronize(b));
+        float t = 0;
+        CK(hipEventElapsedTime(&t, a, b));
+        ms.push_back(t);
+    }
+    std::sort(ms.begin(), ms.end());
+    const double med = ms[ms.size() / 2], best = ms[0];
+    printf("%-18s median %8.1f us  %7.1f GB/s   best %8.1f us  %7.1f GB/s\n", name, med * 1e3,
+           bytes / (med * 1e-3) / 1e9, best * 1e3, bytes / (best * 1e-3) / 1e9);
+    CK(hipEventDestroy(a));
+    CK(hipEventDestroy(b));
+}
+
+int main(int argc, char** argv) {
+    const uint64_t n = (argc > 1 ? strtoull(argv[1], nullptr, 0) : 1ull << 30);
+    uint8_t *buf = nullptr, *dst = nullptr;
+    uint32_t* sink = nullptr;
+    CK(hipMalloc(&buf, n));
+    CK(hipMalloc(&dst, n));
+    CK(hipMalloc(&sink, 4));
+    CK(hipMemset(buf, 0x5A, n));
+    CK(hipMemset(dst, 0, n));
+    printf("buffer %llu bytes\n", (unsigned long long)n);
+    const double rw = 2.0 * (double)n;
+    timeit("xor_inplace<4>", rw, [&] {
+        const uint64_t nw = n / 4096;
+        hipLaunchKernelGGL(xor_inplace<4>, dim3((uint32_t)((nw + 3) / 4)), dim3(256), 0, 0, buf, nw, 0x12345678u);
+    });
+    timeit("xor_inplace<8>", rw, [&] {
+        const uint64_t nw = n / 8192;
+        hipLaunchKernelGGL(xor_inplace<8>, dim3((uint32_t)((nw + 3) / 4)), dim3(256), 0, 0, buf, nw, 0x12345678u);
+    });
+    timeit("xor_inplace<2>", rw, [&] {
+        const uint64_t nw = n / 2048;
+        hipLaunchKernelGGL(xor_inplace<2>, dim3((uint32_t)((nw + 3) / 4)), dim3(256), 0, 0, buf, nw, 0x12345678u);
+    });
+    timeit("copy16", rw, [&] {
+        const uint64_t n16 = n / 16;
+        hipLaunchKernelGGL(copy16, dim3((uint32_t)((n16 + 255) / 256)), dim3(256), 0, 0, buf, dst, n16);
+    });
+    timeit("read_only<4>", (double)n, [&] {
+        const uint64_t nw = n / 4096;
+        hipLaunchKernelGGL(read_only<4>, dim3((uint32_t)((nw + 3) / 4)), dim3(256), 0, 0, buf, nw, sink);
+    });
+    timeit("write_only<4>", (double)n, [&] {
+        const uint64_t nw = n / 4096;
+        hipLaunchKernelGGL(write_only<4>, dim3((uint32_t)((nw + 3) / 4)), dim3(256), 0, 0, dst, nw, 7u);
+    });
+    timeit("hipMemcpyDtoD", rw, [&] { CK(hipMemcpyAsync(dst, buf, n, hipMemcpyDeviceToDevice, 0)); });
+    CK(hipFree(buf));
+    CK(hipFree(dst));
+    CK(hipFree(sink));
+    return 0;
+}
