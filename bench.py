@@ -226,6 +226,7 @@ def main():
         del keep, batches
         torch.cuda.empty_cache()
         out["other_configs"] = other_configs(torch, K, synth)
+        out["encode"] = encode_configs(torch, K, synth)
     if rank == 0 and not a.no_cpu and a.cpu_seconds > 0:
         threads = min(16, len(os.sched_getaffinity(0)))
         v1, p1, e1 = cpu_baseline(cfg, a.cpu_seconds / 2, 1)
@@ -273,6 +274,59 @@ def other_configs(torch, K, synth):
                      "frames": int(cfg["n_frames"]), "payload_bytes": int(cfg["payload_bytes"])}
         c.close()
         del t
+        torch.cuda.empty_cache()
+    return res
+
+
+def encode_configs(torch, K, synth):
+    """Batched server->client framing (wsc_encode, websocket_ctrl.go:23-70) of the decoded
+    payloads of a batch -- the echo path's outbound half: device time (torch events on the launch
+    stream, median of 10) of k_encode_scan + k_encode_copy, algorithmic bytes = payload read +
+    frames written + 24 B descriptor + 8 B offset per message."""
+    dev = torch.device("cuda", torch.cuda.current_device())
+    res = {}
+    cases = [("16384 x 64 KiB BIN (echo of the headline batch)", lambda: synth.uniform_batch(16384, 65536, 4, seed=synth.SEED_BASE + 1)),
+             ("1M x 1 KiB BIN (echo of configs[1])", lambda: synth.uniform_batch(1 << 20, 1024, 16, seed=synth.SEED_BASE + 1))]
+    for name, make in cases:
+        cfg = make()
+        n = int(cfg["n_frames"])
+        msgs = np.zeros(n, K.OUT_MSG_DTYPE)
+        msgs["src_off"] = cfg["payload_off"]
+        msgs["len"] = cfg["plen"]
+        msgs["first_byte"] = 0x82
+        hl = np.where(cfg["plen"] <= 125, 2, np.where(cfg["plen"] <= 65535, 4, 10)).astype(np.int64)
+        total = int((cfg["plen"].astype(np.int64) + hl).sum())
+        c = K.Codec(dev.index, max_batch_bytes=len(cfg["wire"]) + 4096, max_segs=1024, max_frames=n + 16)
+        src = torch.from_numpy(cfg["wire"]).to(dev)
+        d_msgs = torch.from_numpy(msgs.view(np.uint8).copy()).to(dev)
+        d_out = torch.empty(total + 4096, dtype=torch.uint8, device=dev)
+        d_off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+        st = torch.cuda.Stream(device=dev)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        times = []
+        for it in range(13):
+            with torch.cuda.stream(st):
+                ev[0].record(st)
+                c.encode(d_msgs, n, src, len(cfg["wire"]), d_out, total + 4096, d_off, st.cuda_stream)
+                ev[1].record(st)
+            ev[1].synchronize()
+            if it >= 3:
+                times.append(ev[0].elapsed_time(ev[1]))
+        ok = int(d_off[-1].item()) == total
+        # spot check: the first frame's header + payload and the last frame's payload end
+        o = d_out[: 16].cpu().numpy()
+        L = int(cfg["plen"][0])
+        exp_hdr = bytes([0x82, 127]) + L.to_bytes(8, "big") if L > 65535 else (bytes([0x82, 126]) + L.to_bytes(2, "big") if L > 125 else bytes([0x82, L]))
+        ok = ok and o[: len(exp_hdr)].tobytes() == exp_hdr
+        p0 = int(cfg["payload_off"][0])
+        ok = ok and bool(np.array_equal(d_out[len(exp_hdr): len(exp_hdr) + 64].cpu().numpy(), cfg["wire"][p0:p0 + 64]))
+        ms = float(np.median(times))
+        alg = int(cfg["payload_bytes"]) + total + 32 * n
+        res[name] = {"ms": round(ms, 4), "gb_s": round(alg / (ms * 1e-3) / 1e9, 1),
+                     "payload_gib_s": round(cfg["payload_bytes"] / (ms * 1e-3) / 2**30, 1),
+                     "frames": n, "out_bytes": total, "alg_bytes": alg, "check_ok": ok}
+        c.close()
+        del src, d_msgs, d_out, d_off
         torch.cuda.empty_cache()
     return res
 

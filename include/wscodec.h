@@ -185,6 +185,32 @@ int wsc_decode_host(wsc_ctx* ctx, uint8_t* wire, uint64_t n_bytes, const uint64_
                     wsc_conn_state* state_out, wsc_seg_result* seg_out, wsc_frame* frames,
                     uint32_t frames_cap, uint8_t* arena, uint64_t* frame_dst, wsc_summary* summary);
 
+/* ---- encode: batched server -> client framing ------------------------------------------------
+ * Replaces websocketProtocol.encode(firstByte, bs) (server/websocket_ctrl.go:23-70) as used by
+ * Text / Binary (server/websocket.go:378-398), pong (websocket_ctrl.go:140-143) and CloseCode
+ * (websocket_ctrl.go:108-109): each message becomes firstByte, a minimal 7/16/64-bit big-endian
+ * length, then the payload, unmasked.  A batch frames many messages (many connections) back to
+ * back into one output buffer in one device call.                                              */
+typedef struct wsc_out_msg {
+    uint64_t src_off;      /* payload offset in `src`                                            */
+    uint64_t len;          /* payload length                                                     */
+    uint8_t first_byte;    /* 0x81 Text, 0x82 Binary, 0x8A pong, 0x88 close (FIN | opcode)       */
+    uint8_t pad[7];
+} wsc_out_msg;             /* 24 B */
+
+/* Enqueue the framing of n_msgs messages (device-resident `msgs`, `src`; both `src` and `out`
+ * 16-byte aligned).  Frame i is written at out + out_off[i]; out_off[n_msgs] = total bytes.
+ * Bytes at or past out_cap are never written: the caller checks out_off[n_msgs] <= out_cap.
+ * Capacity: n_msgs <= max_frames, out_cap <= max_batch_bytes + 16 * max_frames.  Async on
+ * hip_stream (NULL = default stream); the context runs one decode or encode at a time.          */
+int wsc_encode(wsc_ctx* ctx, const wsc_out_msg* msgs, uint32_t n_msgs, const uint8_t* src,
+               uint64_t src_bytes, uint8_t* out, uint64_t out_cap, uint64_t* out_off, void* hip_stream);
+
+/* Host-buffer encode (synchronous): H2D of msgs + src, wsc_encode, D2H of out_off and the frames.
+ * Returns WSC_E_CAPACITY if the frames need more than out_cap bytes.                            */
+int wsc_encode_host(wsc_ctx* ctx, const wsc_out_msg* msgs, uint32_t n_msgs, const uint8_t* src,
+                    uint64_t src_bytes, uint8_t* out, uint64_t out_cap, uint64_t* out_off);
+
 /* Timing helper for the benchmark: run `iters` back-to-back decodes of a device batch and
  * return the per-kernel average device time (ms) measured with hipEvents on the launch stream.
  * out_ms[0] = fused header walk (incl. utf8), [1], [2], [4] = 0 (reserved), [3] = unmask,

@@ -1,6 +1,6 @@
 """Build recipes for the in-tree native libraries (gfx950 only).
 
-libwscodec.so  <- netman_amd/csrc/{wsc_kernels.hip, wsc_api.cpp, wsc_session.cpp}   (hipcc)
+libwscodec.so  <- netman_amd/csrc/{wsc_kernels.hip, wsc_encode.hip, wsc_api.cpp, wsc_session.cpp}   (hipcc)
 The oracle (test infrastructure) has its own recipe in oracle/Makefile; __graft_entry__.build()
 drives both.
 """
@@ -11,7 +11,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libwscodec.so")
-SOURCES = ["wsc_kernels.hip", "wsc_api.cpp", "wsc_session.cpp"]
+SOURCES = ["wsc_kernels.hip", "wsc_encode.hip", "wsc_api.cpp", "wsc_session.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
@@ -22,18 +22,22 @@ def _newest(paths):
 
 def build_codec(force=False, verbose=False):
     srcs = [os.path.join(CSRC, s) for s in SOURCES]
-    deps = srcs + [os.path.join(CSRC, "wsc_kernels.hpp"), os.path.join(ROOT, "include", "wscodec.h")]
+    deps = srcs + [os.path.join(CSRC, "wsc_kernels.hpp"), os.path.join(CSRC, "wsc_dev.hpp"),
+                   os.path.join(ROOT, "include", "wscodec.h")]
     if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= _newest(deps):
         return LIB
-    objs = []
-    for s in srcs:
+    objs, procs = [], []
+    for s in srcs:   # compile the translation units in parallel
         o = os.path.join("/tmp", "wsc_" + os.path.basename(s) + ".o")
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
                "-x", "hip", "-c", s, "-o", o]
         if verbose:
             print(" ".join(cmd))
-        subprocess.run(cmd, check=True)
+        procs.append((subprocess.Popen(cmd), cmd))
         objs.append(o)
+    for p, cmd in procs:
+        if p.wait() != 0:
+            raise subprocess.CalledProcessError(p.returncode, cmd)
     tmp = LIB + ".tmp"
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
     subprocess.run(cmd, check=True)

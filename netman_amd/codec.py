@@ -49,6 +49,9 @@ SUMMARY_DTYPE = np.dtype([("data_bytes", "<u8"), ("ctrl_bytes", "<u8"), ("n_fram
                           ("n_spans", "<u4"), ("overflow", "<u4"), ("pad", "<u4")])
 assert CONN_STATE_DTYPE.itemsize == 16 and FRAME_DTYPE.itemsize == 32
 assert SEG_RESULT_DTYPE.itemsize == 32 and SUMMARY_DTYPE.itemsize == 32
+# wsc_out_msg: one outbound frame for wsc_encode (websocket_ctrl.go:23-70 encode(firstByte, bs))
+OUT_MSG_DTYPE = np.dtype([("src_off", "<u8"), ("len", "<u8"), ("first_byte", "u1"), ("pad", "u1", (7,))])
+assert OUT_MSG_DTYPE.itemsize == 24
 
 
 class WscConfig(C.Structure):
@@ -91,6 +94,8 @@ SIGNATURES = {
     "wsc_decode": (_I, [_P, C.POINTER(WscBatch), _P]),
     "wsc_sync": (_I, [_P, _P]),
     "wsc_decode_host": (_I, [_P, _P, _U64, _P, _U32, _U32, _P, _P, _P, _P, _U32, _P, _P, _P]),
+    "wsc_encode": (_I, [_P, _P, _U32, _P, _U64, _P, _U64, _P, _P]),
+    "wsc_encode_host": (_I, [_P, _P, _U32, _P, _U64, _P, _U64, _P]),
     "wsc_profile": (_I, [_P, C.POINTER(WscBatch), _I, C.POINTER(C.c_double)]),
     "wsc_debug_stamps": (_I, [_P, _P, _U32]),
     "wsc_session_create": (_I, [_I, C.POINTER(WscConfig), _U32, C.POINTER(_P)]),
@@ -237,6 +242,26 @@ class Codec:
         _check(self.lib.wsc_profile(self.h, C.byref(batch), iters, out), "wsc_profile")
         v = list(out)
         return {"walk": v[0], "unmask": v[3], "total": v[5]}
+
+    # ---- encode (server -> client framing, websocket_ctrl.go:23-70) ----
+    def encode(self, msgs, n_msgs: int, src, src_bytes: int, out, out_cap: int, out_off, stream=None):
+        """Device-resident batched encode: msgs (OUT_MSG_DTYPE records), src, out, out_off are
+        torch CUDA tensors; out_off[n_msgs] receives the total frame bytes."""
+        _check(self.lib.wsc_encode(self.h, _ptr(msgs), int(n_msgs), _ptr(src), int(src_bytes), _ptr(out),
+                                   int(out_cap), _ptr(out_off), self._stream(stream)), "wsc_encode")
+
+    def encode_host(self, msgs: np.ndarray, src: np.ndarray, out_cap: int | None = None):
+        """Host-buffer encode: returns (frames bytes as np.uint8 array, out_off)."""
+        msgs = np.ascontiguousarray(msgs, dtype=OUT_MSG_DTYPE)
+        src = np.ascontiguousarray(src, dtype=np.uint8)
+        n = len(msgs)
+        if out_cap is None:
+            out_cap = int(msgs["len"].astype(np.uint64).sum()) + 10 * n
+        out = np.zeros(max(out_cap, 16), np.uint8)
+        off = np.zeros(n + 1, np.uint64)
+        _check(self.lib.wsc_encode_host(self.h, _ptr(msgs), n, _ptr(src), len(src), _ptr(out), int(out_cap),
+                                        _ptr(off)), "wsc_encode_host")
+        return out[: int(off[n])], off
 
     def decode_host(self, wire: np.ndarray, seg_off: np.ndarray, state_in: np.ndarray | None = None,
                     compact: bool = False, frames_cap: int | None = None) -> DecodeResult:

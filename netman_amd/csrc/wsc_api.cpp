@@ -15,6 +15,8 @@ template <bool COMPACT> __global__ void k_walk_fused(WalkArgs);
 template <bool COMPACT, int P, int NT, int MINW>
 __global__ void k_unmask(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*,
                          const wsc_summary*, uint32_t*, uint32_t);
+__global__ void k_encode_scan(EncArgs);
+template <int NT> __global__ void k_encode_copy(EncCopyArgs);
 }  // namespace wsc
 
 using namespace wsc;
@@ -65,6 +67,19 @@ struct wsc_ctx {
     wsc_frame* d_frames = nullptr;
     uint64_t* d_frame_dst = nullptr;
     wsc_summary* d_summary = nullptr;
+    // encode scratch: look-back state [ticket, timeout, flags...], aggregates, window index
+    uint32_t* enc_lb_state = nullptr;
+    uint64_t* enc_lb_agg = nullptr;
+    uint64_t* enc_lb_incl = nullptr;
+    uint32_t enc_blocks = 0;
+    uint32_t* enc_tile = nullptr;
+    uint64_t enc_cap = 0;             // largest out_cap: max_batch_bytes + 16 * max_frames
+    uint64_t enc_tile_entries = 0;
+    // host-staged encode buffers (lazily allocated)
+    wsc_out_msg* d_enc_msgs = nullptr;
+    uint8_t* d_enc_src = nullptr;
+    uint8_t* d_enc_out = nullptr;
+    uint64_t* d_enc_off = nullptr;
 };
 
 extern "C" {
@@ -146,6 +161,17 @@ int wsc_create(int device, const wsc_config* cfg_in, wsc_ctx** out) {
     chk(hipMalloc(&c->spans, (uint64_t)cfg.max_frames * sizeof(Span)), "hipMalloc spans");
     c->tile_entries = cfg.max_batch_bytes / 1024 + 2;
     chk(hipMalloc(&c->tile, c->tile_entries * sizeof(uint32_t)), "hipMalloc tile");
+    c->enc_blocks = (cfg.max_frames + 255) / 256 + 1;
+    c->enc_cap = cfg.max_batch_bytes + 16ull * cfg.max_frames;
+    c->enc_tile_entries = c->enc_cap / ENC_WIN + 2;
+    chk(hipMalloc(&c->enc_lb_state, (c->enc_blocks + 2) * sizeof(uint32_t)), "hipMalloc enc_lb_state");
+    chk(hipMalloc(&c->enc_lb_agg, c->enc_blocks * sizeof(uint64_t)), "hipMalloc enc_lb_agg");
+    chk(hipMalloc(&c->enc_lb_incl, c->enc_blocks * sizeof(uint64_t)), "hipMalloc enc_lb_incl");
+    chk(hipMalloc(&c->enc_tile, c->enc_tile_entries * sizeof(uint32_t)), "hipMalloc enc_tile");
+    if (rc == WSC_OK) {
+        chk(hipMemsetAsync(c->enc_lb_state, 0, (c->enc_blocks + 2) * sizeof(uint32_t), c->stream), "hipMemset enc_lb_state");
+        chk(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+    }
     if (rc != WSC_OK) {
         wsc_destroy(c);
         return rc;
@@ -160,7 +186,8 @@ int wsc_destroy(wsc_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void* ptrs[] = {c->dbg, c->counts, c->lb_state, c->u8info, c->lb_agg, c->lb_incl, c->spans, c->tile, c->d_wire, c->d_arena,
                     c->d_seg_off, c->d_state_in, c->d_state_out, c->d_seg_out, c->d_frames,
-                    c->d_frame_dst, c->d_summary};
+                    c->d_frame_dst, c->d_summary, c->enc_lb_state, c->enc_lb_agg, c->enc_lb_incl, c->enc_tile,
+                    c->d_enc_msgs, c->d_enc_src, c->d_enc_out, c->d_enc_off};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -342,6 +369,88 @@ int wsc_decode_host(wsc_ctx* c, uint8_t* wire, uint64_t n_bytes, const uint64_t*
     }
     HIP_TRY(hipStreamSynchronize(st));
     if (summary->overflow) return fail(WSC_E_CAPACITY, "frame capacity exceeded");
+    return WSC_OK;
+}
+
+// ---- encode ---------------------------------------------------------------------------------
+static int launch_encode(wsc_ctx* c, const wsc_out_msg* msgs, uint32_t n, const uint8_t* src, uint64_t src_bytes,
+                         uint8_t* out, uint64_t out_cap, uint64_t* out_off, hipStream_t st) {
+    if (!msgs || !out || !out_off || (!src && src_bytes)) return fail(WSC_E_INVAL, "NULL encode pointer");
+    if (n > c->cfg.max_frames) return fail(WSC_E_CAPACITY, "n_msgs > max_frames");
+    if (out_cap > c->enc_cap) return fail(WSC_E_CAPACITY, "out_cap > max_batch_bytes + 16 * max_frames");
+    if ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(out)) & 15)
+        return fail(WSC_E_INVAL, "src and out must be 16-byte aligned");
+    if (n == 0) {
+        HIP_TRY(hipMemsetAsync(out_off, 0, sizeof(uint64_t), st));
+        return WSC_OK;
+    }
+    EncArgs ea{};
+    ea.msgs = msgs;
+    ea.n_msgs = n;
+    ea.out_off = out_off;
+    ea.tile = c->enc_tile;
+    ea.tile_entries = c->enc_tile_entries;
+    ea.lb_ticket = c->enc_lb_state;
+    ea.lb_err = c->enc_lb_state + 1;
+    ea.lb_flag = c->enc_lb_state + 2;
+    ea.lb_agg = c->enc_lb_agg;
+    ea.lb_incl = c->enc_lb_incl;
+    const uint32_t sblocks = (n + 255) / 256;
+    hipLaunchKernelGGL(k_encode_scan, dim3(sblocks), dim3(256), 0, st, ea);
+    HIP_TRY(hipGetLastError());
+    EncCopyArgs ca{};
+    ca.msgs = msgs;
+    ca.n_msgs = n;
+    ca.out_off = out_off;
+    ca.src = src;
+    ca.src_bytes = src_bytes;
+    ca.out = out;
+    ca.out_cap = out_cap;
+    ca.tile = c->enc_tile;
+    ca.tile_entries = c->enc_tile_entries;
+    ca.lb_state = c->enc_lb_state;
+    ca.n_lb = sblocks + 2;
+    uint64_t wins = (out_cap + ENC_WIN - 1) / ENC_WIN;   // the grid covers out_cap; waves past the total exit
+    if (wins > c->enc_tile_entries) wins = c->enc_tile_entries;
+    if (wins == 0) wins = 1;
+    const dim3 cgrid((uint32_t)((wins + 3) / 4));
+    if ((c->cfg.unmask_nt & 3) == 3) hipLaunchKernelGGL(k_encode_copy<3>, cgrid, dim3(256), 0, st, ca);
+    else hipLaunchKernelGGL(k_encode_copy<0>, cgrid, dim3(256), 0, st, ca);
+    HIP_TRY(hipGetLastError());
+    return WSC_OK;
+}
+
+int wsc_encode(wsc_ctx* c, const wsc_out_msg* msgs, uint32_t n_msgs, const uint8_t* src, uint64_t src_bytes,
+               uint8_t* out, uint64_t out_cap, uint64_t* out_off, void* hip_stream) {
+    if (!c) return fail(WSC_E_INVAL, "NULL ctx");
+    HIP_TRY(hipSetDevice(c->device));
+    return launch_encode(c, msgs, n_msgs, src, src_bytes, out, out_cap, out_off, static_cast<hipStream_t>(hip_stream));
+}
+
+int wsc_encode_host(wsc_ctx* c, const wsc_out_msg* msgs, uint32_t n_msgs, const uint8_t* src, uint64_t src_bytes,
+                    uint8_t* out, uint64_t out_cap, uint64_t* out_off) {
+    if (!c || !msgs || !out || !out_off || (!src && src_bytes)) return fail(WSC_E_INVAL, "NULL argument");
+    if (n_msgs > c->cfg.max_frames) return fail(WSC_E_CAPACITY, "n_msgs > max_frames");
+    if (src_bytes > c->cfg.max_batch_bytes) return fail(WSC_E_CAPACITY, "src_bytes > max_batch_bytes");
+    HIP_TRY(hipSetDevice(c->device));
+    if (!c->d_enc_msgs) {
+        HIP_TRY(hipMalloc(&c->d_enc_msgs, (uint64_t)c->cfg.max_frames * sizeof(wsc_out_msg)));
+        HIP_TRY(hipMalloc(&c->d_enc_src, c->cfg.max_batch_bytes + 64));
+        HIP_TRY(hipMalloc(&c->d_enc_out, c->enc_cap + 64));
+        HIP_TRY(hipMalloc(&c->d_enc_off, ((uint64_t)c->cfg.max_frames + 1) * sizeof(uint64_t)));
+    }
+    const uint64_t cap = out_cap < c->enc_cap ? out_cap : c->enc_cap;
+    hipStream_t st = c->stream;
+    if (n_msgs) HIP_TRY(hipMemcpyAsync(c->d_enc_msgs, msgs, (uint64_t)n_msgs * sizeof(wsc_out_msg), hipMemcpyHostToDevice, st));
+    if (src_bytes) HIP_TRY(hipMemcpyAsync(c->d_enc_src, src, src_bytes, hipMemcpyHostToDevice, st));
+    int rc = launch_encode(c, c->d_enc_msgs, n_msgs, c->d_enc_src, src_bytes, c->d_enc_out, cap, c->d_enc_off, st);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(out_off, c->d_enc_off, ((uint64_t)n_msgs + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    const uint64_t total = out_off[n_msgs];
+    if (total > out_cap) return fail(WSC_E_CAPACITY, "encoded frames exceed out_cap");
+    if (total) HIP_TRY(hipMemcpyAsync(out, c->d_enc_out, total, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
     return WSC_OK;
 }
 

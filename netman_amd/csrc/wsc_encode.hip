@@ -1,0 +1,251 @@
+// wsc_encode.hip -- gfx950 kernels of the batched server -> client framer.
+//
+// Replaces websocketProtocol.encode(firstByte, bs) (server/websocket_ctrl.go:23-70): firstByte,
+// a minimal length (<=125: 1 byte; <=65535: 126 + u16 BE; else 127 + u64 BE), then the payload,
+// unmasked.  Called per message in the reference by Text/Binary (websocket.go:378-398), pong
+// (websocket_ctrl.go:140-143) and CloseCode (websocket_ctrl.go:108-109).  Here one launch pair
+// frames a whole batch of messages back to back:
+//   k_encode_scan  one lane per message: frame size, block scan + decoupled look-back -> out_off,
+//                  and the output-window -> first-message index for the copy kernel.
+//   k_encode_copy  one 4 KiB output window per wave, 16 B per lane, 1 KiB per wave instruction:
+//                  a window inside one payload is a shifted stream copy (two aligned loads +
+//                  alignbyte per 16 B); windows holding frame edges assemble header bytes in
+//                  registers and OR in the payload bytes of every frame that overlaps them.
+// Byte work, HBM-bound: no MFMA.  Algorithmic bytes per message: len read + (hl + len) written
+// + 24 B descriptor + 8 B offset.
+#include "wsc_kernels.hpp"
+#include "wsc_dev.hpp"
+
+namespace wsc {
+
+__device__ __forceinline__ uint32_t enc_hlen(uint64_t len) { return len <= 125 ? 2u : (len <= 65535 ? 4u : 10u); }
+
+// The header of one frame as 16 little-endian bytes (only the first enc_hlen(len) are used).
+__device__ __forceinline__ void enc_header(uint32_t first_byte, uint64_t len, uint32_t (&h)[4]) {
+    // written as selects (no branches) so the compiler keeps h in registers
+    const bool l7 = len <= 125;                 // websocket_ctrl.go:33-37  one length byte
+    const bool l16 = !l7 && len <= 65535;       // :39-49  126, uint16 big-endian
+    const bool l64 = !l7 && !l16;               // :51-61  127, uint64 big-endian
+    const uint64_t be = __builtin_bswap64(len);
+    const uint32_t code = l7 ? (uint32_t)len : (l16 ? 126u : 127u);
+    const uint32_t ext = l16 ? ((uint32_t)((len >> 8) & 0xFF) | (uint32_t)(len & 0xFF) << 8)
+                             : (l64 ? (uint32_t)(be & 0xFFFF) : 0u);
+    h[0] = first_byte | code << 8 | ext << 16;
+    h[1] = l64 ? (uint32_t)(be >> 16) : 0u;
+    h[2] = l64 ? (uint32_t)(be >> 48) : 0u;
+    h[3] = 0;
+}
+
+// 16 bytes b = 0..15 with b -> h[b - d] (zero outside h's 16 bytes), for d in (-16, 16).
+__device__ __forceinline__ uint4 enc_place(const uint32_t (&h)[4], int32_t d) {
+    const uint32_t z[12] = {0, 0, 0, 0, h[0], h[1], h[2], h[3], 0, 0, 0, 0};
+    const uint32_t s = (uint32_t)(16 - d);   // byte index in z of output byte 0: 1..31
+    const uint32_t q = s >> 2, rb = s & 3;
+    uint32_t w[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {           // w[j] = z[q + j] without dynamic register indexing
+        uint32_t v = z[j];
+#pragma unroll
+        for (uint32_t t = 1; t < 8; ++t)
+            if (q == t) v = z[t + j];
+        w[j] = v;
+    }
+    return make_uint4(__builtin_amdgcn_alignbyte(w[1], w[0], rb), __builtin_amdgcn_alignbyte(w[2], w[1], rb),
+                      __builtin_amdgcn_alignbyte(w[3], w[2], rb), __builtin_amdgcn_alignbyte(w[4], w[3], rb));
+}
+
+__device__ __forceinline__ uint4 and4(const uint4& v, const uint32_t (&m)[4]) {
+    return make_uint4(v.x & m[0], v.y & m[1], v.z & m[2], v.w & m[3]);
+}
+
+// byte masks of [lo, hi) within a 16-byte piece, per dword
+__device__ __forceinline__ void piece_mask(uint32_t bl, uint32_t bh, uint32_t (&m)[4]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t l = bl > 4u * j ? bl - 4u * j : 0u;
+        const uint32_t hh = bh > 4u * j ? bh - 4u * j : 0u;
+        m[j] = l < hh ? bytes_to_mask(l, hh > 4 ? 4 : hh) : 0u;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Scan: frame sizes -> out_off (exclusive), window index.  Same look-back protocol as the
+// decoder's walk (wsc_kernels.hip): ticket block ids, agent-scope payload stores drained with
+// vmcnt(0) before the agent-scope flag store, readers poll with agent-scope atomics, bounded spin.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_encode_scan(EncArgs a) {
+    __shared__ uint32_t sh_bid;
+    __shared__ uint64_t sh_wave[4];
+    __shared__ uint64_t sh_prefix;
+    if (threadIdx.x == 0)
+        sh_bid = __hip_atomic_fetch_add(a.lb_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const uint32_t bid = sh_bid;
+    const uint32_t i = bid * 256 + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint64_t sz = 0;
+    if (i < a.n_msgs) {
+        const uint64_t len = a.msgs[i].len;
+        sz = enc_hlen(len) + len;
+    }
+    uint64_t inc = sz;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t o = __shfl_up(inc, d);
+        if (lane >= (uint32_t)d) inc += o;
+    }
+    if (lane == 63) sh_wave[wave] = inc;
+    __syncthreads();
+    uint64_t wpre = 0, btot = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        if ((uint32_t)q < wave) wpre += sh_wave[q];
+        btot += sh_wave[q];
+    }
+    if (wave == 0) {
+        if (lane == 0) {
+            __hip_atomic_store(bid == 0 ? a.lb_incl : a.lb_agg + bid, btot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(a.lb_flag + bid, bid == 0 ? 2u : 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        uint64_t prefix = 0;
+        int64_t j0 = (int64_t)bid - 1;
+        uint32_t spins = 0;
+        while (j0 >= 0) {
+            const int64_t j = j0 - (int64_t)lane;
+            const uint32_t f = j >= 0 ? __hip_atomic_fetch_add(a.lb_flag + j, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 2u;
+            const uint64_t m2 = __ballot(f == 2);
+            const uint64_t m0 = __ballot(f == 0);
+            const uint32_t first2 = m2 ? (uint32_t)__builtin_ctzll(m2) : 64u;
+            const uint64_t need = first2 >= 63 ? ~0ull : ((2ull << first2) - 1);
+            if (m0 & need) {
+                if (++spins > (1u << 22)) {
+                    if (lane == 0) __hip_atomic_fetch_or(a.lb_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+                continue;
+            }
+            uint64_t v = 0;
+            if (lane <= first2 && j >= 0)
+                v = __hip_atomic_fetch_add((lane == first2 ? a.lb_incl : a.lb_agg) + j, 0ull, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+            for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
+            prefix += v;
+            if (first2 < 64) break;
+            j0 -= 64;
+        }
+        if (lane == 0) {
+            if (bid != 0) {
+                __hip_atomic_store(a.lb_incl + bid, prefix + btot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __hip_atomic_store(a.lb_flag + bid, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            sh_prefix = prefix;
+        }
+    }
+    __syncthreads();
+    const uint64_t off = sh_prefix + wpre + (inc - sz);
+    if (i < a.n_msgs) {
+        a.out_off[i] = off;
+        // windows that start inside this frame: [ceil(off / W), floor((off + sz - 1) / W)]
+        uint64_t w = (off + ENC_WIN - 1) >> ENC_WIN_SHIFT;
+        uint64_t w_end = ((off + sz - 1) >> ENC_WIN_SHIFT) + 1;
+        if (w_end > a.tile_entries) w_end = a.tile_entries;
+        for (; w < w_end; ++w) a.tile[w] = i;
+        if (i == a.n_msgs - 1) {
+            uint64_t total = off + sz;
+            if (__hip_atomic_load(a.lb_err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) total = ~0ull;   // invalid
+            a.out_off[a.n_msgs] = total;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Copy: one ENC_WIN-byte output window per wave.
+// ---------------------------------------------------------------------------------------------
+template <int NT>
+__global__ __launch_bounds__(256) void k_encode_copy(EncCopyArgs a) {
+    constexpr uint32_t P = ENC_WIN / 1024;
+    // re-arm the scan's look-back state for the next encode (this launch is ordered after it)
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < a.n_lb; t += gridDim.x * blockDim.x) a.lb_state[t] = 0;
+    const uint32_t n = a.n_msgs;
+    if (n == 0) return;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+    uint64_t limit = a.out_off[n];
+    if (limit > a.out_cap) limit = a.out_cap;
+    const uint64_t wbase = gw << ENC_WIN_SHIFT;
+    if (wbase >= limit || gw >= a.tile_entries) return;
+    const uint32_t lofs = lane * 16u;
+    uint32_t m = a.tile[gw];
+    const wsc_out_msg mm = a.msgs[m];
+    const uint64_t o = a.out_off[m];
+    const uint64_t p0 = o + enc_hlen(mm.len), p1 = p0 + mm.len;
+    if (p0 <= wbase && p1 >= wbase + ENC_WIN && wbase + ENC_WIN <= limit) {
+        // fast path: the window lies inside one payload -> shifted stream copy
+        const int64_t so = (int64_t)mm.src_off - (int64_t)p0;
+        uint4 v[P];
+#pragma unroll
+        for (uint32_t k = 0; k < P; ++k) v[k] = load16_unaligned(a.src, so + (int64_t)(wbase + k * 1024u + lofs), a.src_bytes);
+#pragma unroll
+        for (uint32_t k = 0; k < P; ++k) st16v<NT>(a.out + wbase + k * 1024u + lofs, u32x4{v[k].x, v[k].y, v[k].z, v[k].w});
+        return;
+    }
+    // general path: frame edges in the window -> assemble every piece from all overlapping frames
+    uint4 acc[P];
+#pragma unroll
+    for (uint32_t k = 0; k < P; ++k) acc[k] = make_uint4(0, 0, 0, 0);
+    for (uint32_t j = m; j < n; ++j) {
+        const uint64_t oj = j == m ? o : a.out_off[j];
+        if (oj >= wbase + ENC_WIN) break;
+        const wsc_out_msg mj = j == m ? mm : a.msgs[j];
+        const uint32_t hl = enc_hlen(mj.len);
+        uint32_t h[4];
+        enc_header(mj.first_byte, mj.len, h);
+        const uint64_t pj = oj + hl, ej = pj + mj.len;
+#pragma unroll
+        for (uint32_t k = 0; k < P; ++k) {
+            const uint64_t pa = wbase + k * 1024u + lofs;
+            uint32_t msk[4];
+            // header bytes [oj, pj)
+            uint64_t lo = oj > pa ? oj : pa;
+            uint64_t hi = pj < pa + 16 ? pj : pa + 16;
+            if (lo < hi) {
+                piece_mask((uint32_t)(lo - pa), (uint32_t)(hi - pa), msk);
+                const uint4 hv = enc_place(h, (int32_t)((int64_t)oj - (int64_t)pa));
+                const uint4 t = and4(hv, msk);
+                acc[k].x |= t.x; acc[k].y |= t.y; acc[k].z |= t.z; acc[k].w |= t.w;
+            }
+            // payload bytes [pj, ej)
+            lo = pj > pa ? pj : pa;
+            hi = ej < pa + 16 ? ej : pa + 16;
+            if (lo < hi) {
+                piece_mask((uint32_t)(lo - pa), (uint32_t)(hi - pa), msk);
+                const uint4 sv = load16_unaligned(a.src, (int64_t)mj.src_off + ((int64_t)pa - (int64_t)pj), a.src_bytes);
+                const uint4 t = and4(sv, msk);
+                acc[k].x |= t.x; acc[k].y |= t.y; acc[k].z |= t.z; acc[k].w |= t.w;
+            }
+        }
+        if (ej >= wbase + ENC_WIN) break;   // this frame runs past the window
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < P; ++k) {
+        const uint64_t pa = wbase + k * 1024u + lofs;
+        if (pa >= limit) continue;
+        if (pa + 16 <= limit) {
+            st16v<NT>(a.out + pa, u32x4{acc[k].x, acc[k].y, acc[k].z, acc[k].w});
+        } else {   // the tail piece: never write at or past the total / out_cap
+            const uint32_t d[4] = {acc[k].x, acc[k].y, acc[k].z, acc[k].w};
+#pragma unroll
+            for (uint32_t b = 0; b < 16; ++b)   // unrolled: constant register indices, no scratch
+                if (pa + b < limit) a.out[pa + b] = (uint8_t)(d[b >> 2] >> (8 * (b & 3)));
+        }
+    }
+}
+
+template __global__ void k_encode_copy<0>(EncCopyArgs);
+template __global__ void k_encode_copy<3>(EncCopyArgs);
+
+}  // namespace wsc

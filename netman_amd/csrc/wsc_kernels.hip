@@ -9,13 +9,10 @@
 //   utf8.Valid (websocket_frame.go:71-73, websocket.go:170-172) runs inside the walk's counting
 //   pass on the still-masked wire, so a connection whose text is invalid stops at that frame.
 #include "wsc_kernels.hpp"
+#include "wsc_dev.hpp"
 
 namespace wsc {
 
-__device__ __forceinline__ uint32_t rotr32(uint32_t x, uint32_t r) {
-    r &= 31;
-    return r ? (x >> r) | (x << (32 - r)) : x;
-}
 
 // ---------------------------------------------------------------------------------------------
 // Header walk
@@ -151,7 +148,6 @@ __device__ __forceinline__ EmitCtx emit_begin(const WalkArgs& a, uint32_t s, uin
 template <bool COMPACT>
 __device__ __forceinline__ void emit_frame(const WalkArgs& a, EmitCtx& e, const wsc_frame& fr, uint32_t plen,
                                            bool have_span, uint32_t region) {
-    const uint64_t W = 1ull << a.win_shift;
     const uint32_t fi = e.fbase + e.nf;
     if (fi < a.frames_cap) {
         // two 16-byte stores (the record is 32 B)
@@ -720,76 +716,6 @@ __global__ __launch_bounds__(256) void k_walk_fused(WalkArgs a) {
 // 1 KiB contiguous.  For each overlapping span a lane ORs the span's rotated mask word into the
 // bytes of its pieces that the span covers, then XORs and stores once.
 // ---------------------------------------------------------------------------------------------
-
-__device__ __forceinline__ uint32_t bytes_to_mask(uint32_t lo, uint32_t hi) {
-    // byte lanes [lo, hi) of a dword, lo <= hi <= 4
-    const uint32_t a = lo >= 4 ? 0u : (0xFFFFFFFFu << (8 * lo));
-    const uint32_t b = hi >= 4 ? 0xFFFFFFFFu : ~(0xFFFFFFFFu << (8 * hi));
-    return a & b;
-}
-
-// 16 bytes starting at src + off (off may be unaligned); bytes outside [0, n) read as 0
-__device__ __forceinline__ uint4 load16_unaligned(const uint8_t* __restrict__ src, int64_t off,
-                                                  uint64_t n) {
-    const int64_t c0 = off & ~(int64_t)15;
-    const uint32_t sh = (uint32_t)(off - c0);
-    uint4 v0 = make_uint4(0, 0, 0, 0), v1 = make_uint4(0, 0, 0, 0);
-    if (c0 >= 0 && (uint64_t)c0 + 16 <= n) v0 = *reinterpret_cast<const uint4*>(src + c0);
-    else {
-        uint32_t t[4] = {0, 0, 0, 0};
-        for (int j = 0; j < 16; ++j) {
-            const int64_t q = c0 + j;
-            if (q >= 0 && (uint64_t)q < n) t[j >> 2] |= (uint32_t)src[q] << (8 * (j & 3));
-        }
-        v0 = make_uint4(t[0], t[1], t[2], t[3]);
-    }
-    if (sh == 0) return v0;
-    const int64_t c1 = c0 + 16;
-    if (c1 >= 0 && (uint64_t)c1 + 16 <= n) v1 = *reinterpret_cast<const uint4*>(src + c1);
-    else {
-        uint32_t t[4] = {0, 0, 0, 0};
-        for (int j = 0; j < 16; ++j) {
-            const int64_t q = c1 + j;
-            if (q >= 0 && (uint64_t)q < n) t[j >> 2] |= (uint32_t)src[q] << (8 * (j & 3));
-        }
-        v1 = make_uint4(t[0], t[1], t[2], t[3]);
-    }
-    const uint32_t d[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-    const uint32_t q = sh >> 2, rb = sh & 3;
-    uint32_t o[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        // select dwords q+j and q+j+1 without dynamic register indexing
-        uint32_t lo = d[j], hi = d[j + 1];
-        if (q == 1) { lo = d[j + 1]; hi = d[j + 2]; }
-        else if (q == 2) { lo = d[j + 2]; hi = d[j + 3]; }
-        else if (q == 3) { lo = d[j + 3]; hi = d[j + 4]; }
-        o[j] = __builtin_amdgcn_alignbyte(hi, lo, rb);
-    }
-    return make_uint4(o[0], o[1], o[2], o[3]);
-}
-
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-template <int NT>
-__device__ __forceinline__ u32x4 ld16v(const uint8_t* p) {
-    if constexpr (NT & 1) return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
-    else return *reinterpret_cast<const u32x4*>(p);
-}
-template <int NT>
-__device__ __forceinline__ void st16v(uint8_t* p, u32x4 v) {
-    if constexpr (NT & 2) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
-    else *reinterpret_cast<u32x4*>(p) = v;
-}
-template <int NT>
-__device__ __forceinline__ uint4 ld16(const uint8_t* p) {
-    const u32x4 t = ld16v<NT>(p);
-    return make_uint4(t.x, t.y, t.z, t.w);
-}
-template <int NT>
-__device__ __forceinline__ void st16(uint8_t* p, uint4 v) {
-    u32x4 t = {v.x, v.y, v.z, v.w};
-    st16v<NT>(p, t);
-}
 
 // General window: several spans overlap it (small frames), or it is the last, partial window.
 // Builds a per-byte key from every span that overlaps each 16-byte piece.

@@ -71,5 +71,35 @@ struct WalkArgs {
 };
 
 
+// ---- encode (wsc_encode.hip) ----------------------------------------------------------------
+constexpr uint32_t ENC_WIN_SHIFT = 12;                 // 4 KiB output windows
+constexpr uint32_t ENC_WIN = 1u << ENC_WIN_SHIFT;
+
+struct EncArgs {
+    const wsc_out_msg* msgs;
+    uint32_t n_msgs;
+    uint64_t* out_off;           // n_msgs + 1
+    uint32_t* tile;              // per output window: the frame its first byte belongs to
+    uint64_t tile_entries;
+    uint32_t* lb_ticket;
+    uint32_t* lb_flag;
+    uint64_t* lb_agg;
+    uint64_t* lb_incl;
+    uint32_t* lb_err;
+};
+
+struct EncCopyArgs {
+    const wsc_out_msg* msgs;
+    uint32_t n_msgs;
+    const uint64_t* out_off;
+    const uint8_t* src;
+    uint64_t src_bytes;
+    uint8_t* out;
+    uint64_t out_cap;
+    const uint32_t* tile;
+    uint64_t tile_entries;
+    uint32_t* lb_state;          // the scan's look-back state, re-armed by this launch
+    uint32_t n_lb;
+};
 
 }  // namespace wsc

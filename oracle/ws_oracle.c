@@ -527,3 +527,32 @@ int wso_run(const uint8_t* stream, uint64_t len, const uint64_t* chunk_ends, uin
     buf_free(&r.c.continueBuffer);
     return r.overflow ? -1 : 0;
 }
+
+/* ---- encode (server/websocket_ctrl.go:23-70) ------------------------------------------------ */
+uint64_t wso_encode(uint8_t first_byte, const uint8_t* bs, uint64_t len, uint8_t* out) {
+    uint64_t k = 0;
+    out[k++] = first_byte;                              /* :28 binary.Write(firstByte) */
+    if (len <= 125) {                                   /* :33-37 */
+        out[k++] = (uint8_t)len;
+    } else if (len >= 126 && len <= 65535) {           /* :39-49 uint8(126) + uint16 BE */
+        out[k++] = 126;
+        out[k++] = (uint8_t)(len >> 8);
+        out[k++] = (uint8_t)len;
+    } else {                                            /* :51-61 uint8(127) + uint64 BE */
+        out[k++] = 127;
+        for (int s = 56; s >= 0; s -= 8) out[k++] = (uint8_t)(len >> s);
+    }
+    if (len) memcpy(out + k, bs, len);                  /* :64-66 the payload, unmasked */
+    return k + len;
+}
+
+uint64_t wso_encode_batch(const uint8_t* src, const uint64_t* src_off, const uint64_t* len,
+                          const uint8_t* first_byte, uint32_t n, uint8_t* out, uint64_t* out_off) {
+    uint64_t pos = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        out_off[i] = pos;
+        pos += wso_encode(first_byte[i], src + src_off[i], len[i], out + pos);
+    }
+    out_off[n] = pos;
+    return pos;
+}

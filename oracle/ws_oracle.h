@@ -116,6 +116,20 @@ int wso_utf8_valid(const uint8_t* p, uint64_t n);
 /* server/websocket_frame.go:35-39 restated on its own: decodeBuffer[i] = buf[i] ^ masks[i%4] */
 void wso_unmask(const uint8_t* in, uint8_t* out, uint64_t n, const uint8_t masks[4]);
 
+/*
+ * ENCODE side (server -> client framing), server/websocket_ctrl.go:23-70 encode(firstByte, bs):
+ * firstByte, then len <= 125 -> one length byte; 126..65535 -> 126 + u16 big-endian;
+ * otherwise 127 + u64 big-endian; then the payload, never masked.  Callers: Text 0x81 / Binary
+ * 0x82 (websocket.go:378-398), pong 0x8A (websocket_ctrl.go:140-143), CloseCode 0x88
+ * (websocket_ctrl.go:108-109).  Writes into out (room for len + 10) and returns the frame size.
+ */
+uint64_t wso_encode(uint8_t first_byte, const uint8_t* bs, uint64_t len, uint8_t* out);
+
+/* A batch of encodes back to back: message i = src[src_off[i] .. +len[i]) with first_byte[i];
+ * out_off[i] = where frame i starts, out_off[n] = total.  Returns the total. */
+uint64_t wso_encode_batch(const uint8_t* src, const uint64_t* src_off, const uint64_t* len,
+                          const uint8_t* first_byte, uint32_t n, uint8_t* out, uint64_t* out_off);
+
 #ifdef __cplusplus
 }
 #endif

@@ -54,6 +54,11 @@ def lib():
                                  C.c_void_p, C.c_uint64, C.POINTER(WsoResult)]
         _lib.wso_utf8_valid.restype = C.c_int
         _lib.wso_utf8_valid.argtypes = [C.c_void_p, C.c_uint64]
+        _lib.wso_encode.restype = C.c_uint64
+        _lib.wso_encode.argtypes = [C.c_uint8, C.c_void_p, C.c_uint64, C.c_void_p]
+        _lib.wso_encode_batch.restype = C.c_uint64
+        _lib.wso_encode_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
+                                          C.c_void_p, C.c_void_p]
     return _lib
 
 
@@ -126,3 +131,25 @@ def goport():
         _goport.goport_unmask_frames.argtypes = [C.c_void_p] * 4 + [C.c_uint64]
         _goport.goport_unmask_frames_mt.argtypes = [C.c_void_p] * 4 + [C.c_uint64, C.c_int]
     return _goport
+
+
+def encode(first_byte: int, payload: bytes) -> bytes:
+    """websocket_ctrl.go:23-70 encode(firstByte, bs), restated in oracle/ws_oracle.c"""
+    out = (C.c_uint8 * (len(payload) + 10))()
+    src = (C.c_uint8 * max(1, len(payload))).from_buffer_copy(payload or b"\0")
+    n = lib().wso_encode(first_byte, src, len(payload), out)
+    return bytes(out[:n])
+
+
+def encode_batch(src: np.ndarray, src_off: np.ndarray, lens: np.ndarray, first_byte: np.ndarray):
+    """encode of every message back to back; returns (frames, out_off[n+1])"""
+    src = np.ascontiguousarray(src, dtype=np.uint8)
+    so = np.ascontiguousarray(src_off, dtype=np.uint64)
+    ln = np.ascontiguousarray(lens, dtype=np.uint64)
+    fb = np.ascontiguousarray(first_byte, dtype=np.uint8)
+    n = len(ln)
+    out = np.zeros(int(ln.sum()) + 10 * n + 16, np.uint8)
+    off = np.zeros(n + 1, np.uint64)
+    tot = lib().wso_encode_batch(src.ctypes.data, so.ctypes.data, ln.ctypes.data, fb.ctypes.data, n,
+                                 out.ctypes.data, off.ctypes.data)
+    return out[:tot], off
