@@ -151,10 +151,10 @@ typedef struct wsc_config {
     uint32_t max_segs;         /* largest n_segs                                                 */
     uint32_t max_frames;       /* largest number of frames in one batch                          */
     uint64_t max_frame_len;    /* payloads above this -> WSC_ERR_TOO_LARGE (<= 0xFFFFFFFF)       */
-    uint32_t unmask_window;    /* bytes per wave-window in the unmask kernel (0 = default)       */
+    uint32_t unmask_window;    /* bytes per wave-window in the unmask kernel: 4096 / 8192 (0 = 4096) */
     uint32_t unmask_waves_per_cu; /* unmask grid sizing (0 = default)                            */
     uint32_t unmask_nt;        /* bit0: non-temporal payload loads, bit1: non-temporal stores     */
-    uint32_t unmask_minw;      /* occupancy hint for the unmask kernel: 0/1 none, 2/4/8 min waves per SIMD */
+    uint32_t unmask_minw;      /* reserved (0); was an occupancy hint, measured no gain        */
 } wsc_config;
 
 typedef struct wsc_ctx wsc_ctx;

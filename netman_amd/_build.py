@@ -1,6 +1,7 @@
 """Build recipes for the in-tree native libraries (gfx950 only).
 
-libwscodec.so  <- netman_amd/csrc/{wsc_kernels.hip, wsc_encode.hip, wsc_api.cpp, wsc_session.cpp}   (hipcc)
+libwscodec.so  <- netman_amd/csrc/{wsc_kernels.hip, wsc_unmask_{inplace,compact}.hip, wsc_encode.hip,
+                  wsc_api.cpp, wsc_session.cpp}   (hipcc, translation units compiled in parallel)
 The oracle (test infrastructure) has its own recipe in oracle/Makefile; __graft_entry__.build()
 drives both.
 """
@@ -11,7 +12,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libwscodec.so")
-SOURCES = ["wsc_kernels.hip", "wsc_encode.hip", "wsc_api.cpp", "wsc_session.cpp"]
+SOURCES = ["wsc_kernels.hip", "wsc_unmask_inplace.hip", "wsc_unmask_compact.hip", "wsc_encode.hip",
+           "wsc_api.cpp", "wsc_session.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
@@ -23,6 +25,7 @@ def _newest(paths):
 def build_codec(force=False, verbose=False):
     srcs = [os.path.join(CSRC, s) for s in SOURCES]
     deps = srcs + [os.path.join(CSRC, "wsc_kernels.hpp"), os.path.join(CSRC, "wsc_dev.hpp"),
+                   os.path.join(CSRC, "wsc_unmask.inl"),
                    os.path.join(ROOT, "include", "wscodec.h")]
     if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= _newest(deps):
         return LIB

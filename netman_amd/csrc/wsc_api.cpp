@@ -132,7 +132,7 @@ int wsc_create(int device, const wsc_config* cfg_in, wsc_ctx** out) {
         return fail(WSC_E_INVAL, "zero capacity in config");
     if (cfg.max_frame_len > 0xFFFFFFFFull) return fail(WSC_E_INVAL, "max_frame_len > 2^32-1");
     uint32_t win = cfg.unmask_window ? cfg.unmask_window : 4096;
-    if (win != 4096 && win != 8192 && win != 16384) return fail(WSC_E_INVAL, "unmask_window must be 4096/8192/16384");
+    if (win != 4096 && win != 8192) return fail(WSC_E_INVAL, "unmask_window must be 4096 or 8192");
     cfg.unmask_window = win;
 
     HIP_TRY(hipSetDevice(device));
@@ -278,22 +278,14 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     const dim3 ublk(256), ugrid((uint32_t)((waves + 3) / 4));
     using UK = void (*)(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*,
                         const wsc_summary*, uint32_t*, uint32_t);
-    // [compact][pieces 4/8/16][nt 0..3]
-    static const UK table[2][3][4] = {
+    // [compact][pieces 4/8][nt 0..3]
+    static const UK table[2][2][4] = {
         {{k_unmask<false, 4, 0, 1>, k_unmask<false, 4, 1, 1>, k_unmask<false, 4, 2, 1>, k_unmask<false, 4, 3, 1>},
-         {k_unmask<false, 8, 0, 1>, k_unmask<false, 8, 1, 1>, k_unmask<false, 8, 2, 1>, k_unmask<false, 8, 3, 1>},
-         {k_unmask<false, 16, 0, 1>, k_unmask<false, 16, 1, 1>, k_unmask<false, 16, 2, 1>, k_unmask<false, 16, 3, 1>}},
+         {k_unmask<false, 8, 0, 1>, k_unmask<false, 8, 1, 1>, k_unmask<false, 8, 2, 1>, k_unmask<false, 8, 3, 1>}},
         {{k_unmask<true, 4, 0, 1>, k_unmask<true, 4, 1, 1>, k_unmask<true, 4, 2, 1>, k_unmask<true, 4, 3, 1>},
-         {k_unmask<true, 8, 0, 1>, k_unmask<true, 8, 1, 1>, k_unmask<true, 8, 2, 1>, k_unmask<true, 8, 3, 1>},
-         {k_unmask<true, 16, 0, 1>, k_unmask<true, 16, 1, 1>, k_unmask<true, 16, 2, 1>, k_unmask<true, 16, 3, 1>}}};
-    const int pi = c->pieces == 4 ? 0 : (c->pieces == 8 ? 1 : 2);
+         {k_unmask<true, 8, 0, 1>, k_unmask<true, 8, 1, 1>, k_unmask<true, 8, 2, 1>, k_unmask<true, 8, 3, 1>}}};
+    const int pi = c->pieces == 4 ? 0 : 1;
     UK kern = table[compact ? 1 : 0][pi][c->cfg.unmask_nt & 3];
-    // occupancy variants (launch_bounds minimum waves per SIMD) for the tuned in-place kernels
-    static const UK occ[2][3] = {{k_unmask<false, 4, 3, 2>, k_unmask<false, 4, 3, 4>, k_unmask<false, 4, 3, 8>},
-                                 {k_unmask<false, 8, 3, 2>, k_unmask<false, 8, 3, 4>, k_unmask<false, 8, 3, 8>}};
-    const uint32_t mw = c->cfg.unmask_minw;
-    if (!compact && (c->cfg.unmask_nt & 3) == 3 && pi < 2 && (mw == 2 || mw == 4 || mw == 8))
-        kern = occ[pi][mw == 2 ? 0 : (mw == 4 ? 1 : 2)];
     hipLaunchKernelGGL(kern, ugrid, ublk, 0, st, udst, (const uint8_t*)b->wire, b->n_bytes, udst_bytes,
                        (const Span*)c->spans, (const uint32_t*)c->tile, (const wsc_summary*)b->summary,
                        c->lb_state, (n + 255) / 256);

@@ -708,220 +708,8 @@ __global__ __launch_bounds__(256) void k_walk_fused(WalkArgs a) {
     }
 }
 
-// ---------------------------------------------------------------------------------------------
-// Unmask: the hot loop.  The destination byte range is cut into windows of P KiB; wave w owns
-// window w (grid-stride).  tile_first[w] names the first span whose destination ends after the
-// window start, so the wave walks only the spans that overlap its window (scalar loads).  Each
-// lane holds P pieces of 16 B at dst + w*W + k*1024 + lane*16: every wave instruction touches
-// 1 KiB contiguous.  For each overlapping span a lane ORs the span's rotated mask word into the
-// bytes of its pieces that the span covers, then XORs and stores once.
-// ---------------------------------------------------------------------------------------------
-
-// General window: several spans overlap it (small frames), or it is the last, partial window.
-// Builds a per-byte key from every span that overlaps each 16-byte piece.
-template <bool COMPACT, int P, int NT>
-__device__ __attribute__((noinline)) void unmask_window_general(
-    uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, uint64_t src_bytes, uint64_t total,
-    const Span* __restrict__ spans, uint32_t n_spans, uint32_t r, uint64_t wbase, uint32_t lofs) {
-    constexpr uint32_t WB = 1024u * P;
-    uint4 v[P], key[P];
-    uint32_t cov[P];
-#pragma unroll
-    for (int k = 0; k < P; ++k) {
-        key[k] = make_uint4(0, 0, 0, 0);
-        cov[k] = 0;
-        v[k] = make_uint4(0, 0, 0, 0);
-        if constexpr (!COMPACT) {
-            const uint64_t addr = wbase + k * 1024u + lofs;
-            if (addr + 16 <= total) v[k] = ld16<NT>(dst + addr);
-        }
-    }
-    for (; r < n_spans; ++r) {
-        const Span sp = spans[r];
-        if (sp.dst >= wbase + WB) break;
-        const uint64_t d0 = sp.dst, d1 = sp.dst + sp.len;
-#pragma unroll
-        for (int k = 0; k < P; ++k) {
-            const uint64_t pa = wbase + k * 1024u + lofs;
-            const uint64_t lo = d0 > pa ? d0 : pa;
-            const uint64_t hi = d1 < pa + 16 ? d1 : pa + 16;
-            if (lo < hi) {
-                const uint32_t bl = (uint32_t)(lo - pa), bh = (uint32_t)(hi - pa);
-                uint32_t m[4];
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const uint32_t l = bl > 4u * j ? bl - 4u * j : 0u;
-                    const uint32_t hh = bh > 4u * j ? bh - 4u * j : 0u;
-                    m[j] = l < hh ? bytes_to_mask(l, hh > 4 ? 4 : hh) : 0u;
-                }
-                key[k].x |= sp.key & m[0];
-                key[k].y |= sp.key & m[1];
-                key[k].z |= sp.key & m[2];
-                key[k].w |= sp.key & m[3];
-                cov[k] |= 1u;
-                if constexpr (COMPACT) {
-                    const int64_t so = (int64_t)sp.src + ((int64_t)pa - (int64_t)sp.dst);
-                    const uint4 sv = load16_unaligned(src, so, src_bytes);
-                    v[k].x |= sv.x & m[0];
-                    v[k].y |= sv.y & m[1];
-                    v[k].z |= sv.z & m[2];
-                    v[k].w |= sv.w & m[3];
-                }
-            }
-        }
-    }
-#pragma unroll
-    for (int k = 0; k < P; ++k) {
-        if (!cov[k]) continue;
-        const uint64_t addr = wbase + k * 1024u + lofs;
-        uint4 o = v[k];
-        o.x ^= key[k].x; o.y ^= key[k].y; o.z ^= key[k].z; o.w ^= key[k].w;
-        if (COMPACT || addr + 16 <= total) {
-            st16<NT>(dst + addr, o);
-        } else {
-            // in-place tail piece past the last full 16 B of the buffer: byte stores
-            const uint32_t kd[4] = {key[k].x, key[k].y, key[k].z, key[k].w};
-            for (uint32_t j = 0; addr + j < total; ++j)
-                dst[addr + j] ^= (uint8_t)(kd[j >> 2] >> (8 * (j & 3)));
-        }
-    }
-}
-
-// NT bit 0: non-temporal loads, bit 1: non-temporal stores.  In place, `src` is unused (dst is
-// both source and destination) so the two restrict pointers never alias in an access.
-template <bool COMPACT, int P, int NT, int MINW = 1>
-__global__ __launch_bounds__(256, MINW) void k_unmask(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src,
-                                                uint64_t src_bytes, uint64_t dst_bytes_host,
-                                                const Span* __restrict__ spans,
-                                                const uint32_t* __restrict__ tile_first,
-                                                const wsc_summary* __restrict__ summary,
-                                                uint32_t* __restrict__ lb_state, uint32_t n_walk_blocks) {
-    constexpr uint32_t WB = 1024u * P;
-    // re-arm the walk's look-back state for the next decode (this launch is ordered after it):
-    // lb_state[0] = ticket, [1] = timeout flag, [2 ...] = per-block flags
-    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n_walk_blocks + 2; t += gridDim.x * blockDim.x)
-        lb_state[t] = 0;
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t waves_per_block = blockDim.x >> 6;
-    const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * waves_per_block + (threadIdx.x >> 6));
-    const uint32_t nw = gridDim.x * waves_per_block;
-    const uint64_t total = COMPACT ? summary->data_bytes + summary->ctrl_bytes : dst_bytes_host;
-    const uint32_t n_spans = summary->n_spans;
-    const uint64_t n_win = (total + WB - 1) / WB;
-    const uint32_t lofs = lane * 16u;
-    if (n_spans == 0) return;
-
-    for (uint64_t win = gw; win < n_win; win += nw) {
-        const uint64_t wbase = win * WB;
-        if (wbase + WB > total) {   // the last, partial window
-            const uint32_t r = tile_first[win];
-            unmask_window_general<COMPACT, P, NT>(dst, src, src_bytes, total, spans, n_spans, r, wbase, lofs);
-            continue;
-        }
-        u32x4 v[P];
-        if constexpr (!COMPACT) {
-            // in place the loads do not depend on the span lookup: issue them first
-#pragma unroll
-            for (int k = 0; k < P; ++k) v[k] = ld16v<NT>(dst + wbase + k * 1024u + lofs);
-        }
-        uint32_t r = tile_first[win];
-        Span sp = spans[r < n_spans ? r : n_spans - 1];
-        if (r >= n_spans) sp.dst = ~0ull;   // no span starts before the window's end
-        if (sp.dst <= wbase && sp.dst + sp.len >= wbase + WB) {
-            // fast path: one span covers the whole window -> one rotated key for every dword
-            if constexpr (COMPACT) {
-                const int64_t so = (int64_t)sp.src - (int64_t)sp.dst;
-#pragma unroll
-                for (int k = 0; k < P; ++k) {
-                    const uint4 t = load16_unaligned(src, so + (int64_t)(wbase + k * 1024u + lofs), src_bytes);
-                    v[k] = u32x4{t.x, t.y, t.z, t.w};
-                }
-            }
-#pragma unroll
-            for (int k = 0; k < P; ++k) {
-                v[k] ^= sp.key;
-                st16v<NT>(dst + wbase + k * 1024u + lofs, v[k]);
-            }
-            continue;
-        }
-        // Several spans overlap the window (small frames) or it holds a frame edge.  Each 1 KiB
-        // sub-window k (one wave instruction) is finished before the next, so only one piece's key
-        // is live at a time; the span cursor only moves forward (spans are sorted by dst).
-#pragma unroll
-        for (int k = 0; k < P; ++k) {
-            const uint64_t sb = wbase + k * 1024u;
-            const uint64_t pa = sb + lofs;
-            while (r < n_spans && sp.dst + sp.len <= sb) {   // spans that end before this sub-window
-                ++r;
-                if (r < n_spans) sp = spans[r];
-            }
-            u32x4 key = {0, 0, 0, 0};
-            u32x4 sv = {0, 0, 0, 0};
-            bool cov = false;
-            Span q = sp;
-            for (uint32_t qi = r; qi < n_spans && q.dst < sb + 1024u;) {
-                const uint64_t lo = q.dst > pa ? q.dst : pa;
-                const uint64_t d1 = q.dst + q.len;
-                const uint64_t hi = d1 < pa + 16 ? d1 : pa + 16;
-                if (lo < hi) {
-                    const uint32_t bl = (uint32_t)(lo - pa), bh = (uint32_t)(hi - pa);
-                    u32x4 m;
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const uint32_t l = bl > 4u * j ? bl - 4u * j : 0u;
-                        const uint32_t hh = bh > 4u * j ? bh - 4u * j : 0u;
-                        m[j] = l < hh ? bytes_to_mask(l, hh > 4 ? 4 : hh) : 0u;
-                    }
-                    key |= q.key & m;
-                    cov = true;
-                    if constexpr (COMPACT) {
-                        const int64_t so = (int64_t)q.src + ((int64_t)pa - (int64_t)q.dst);
-                        const uint4 t = load16_unaligned(src, so, src_bytes);
-                        sv |= u32x4{t.x, t.y, t.z, t.w} & m;
-                    }
-                }
-                if (++qi < n_spans) q = spans[qi]; else break;
-            }
-            if (cov) {
-                if constexpr (COMPACT) st16v<NT>(dst + pa, sv ^ key);
-                else st16v<NT>(dst + pa, v[k] ^ key);
-            }
-        }
-    }
-}
-
 // explicit instantiations used by the host code
-template __global__ void k_unmask<false, 4, 3, 2>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
-template __global__ void k_unmask<false, 4, 3, 4>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
-template __global__ void k_unmask<false, 4, 3, 8>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
-template __global__ void k_unmask<false, 8, 3, 2>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
-template __global__ void k_unmask<false, 8, 3, 4>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
-template __global__ void k_unmask<false, 8, 3, 8>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
 template __global__ void k_walk_fused<false>(WalkArgs);
 template __global__ void k_walk_fused<true>(WalkArgs);
-template __global__ void k_unmask<false, 4, 0>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
-template __global__ void k_unmask<false, 4, 1>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
-template __global__ void k_unmask<false, 4, 2>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
-template __global__ void k_unmask<false, 4, 3>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
-template __global__ void k_unmask<false, 8, 0>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
-template __global__ void k_unmask<false, 8, 1>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
-template __global__ void k_unmask<false, 8, 2>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
-template __global__ void k_unmask<false, 8, 3>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
-template __global__ void k_unmask<false, 16, 0>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
-template __global__ void k_unmask<false, 16, 1>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
-template __global__ void k_unmask<false, 16, 2>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
-template __global__ void k_unmask<false, 16, 3>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
-template __global__ void k_unmask<true, 4, 0>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
-template __global__ void k_unmask<true, 4, 1>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
-template __global__ void k_unmask<true, 4, 2>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
-template __global__ void k_unmask<true, 4, 3>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
-template __global__ void k_unmask<true, 8, 0>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
-template __global__ void k_unmask<true, 8, 1>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
-template __global__ void k_unmask<true, 8, 2>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
-template __global__ void k_unmask<true, 8, 3>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
-template __global__ void k_unmask<true, 16, 0>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
-template __global__ void k_unmask<true, 16, 1>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
-template __global__ void k_unmask<true, 16, 2>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
-template __global__ void k_unmask<true, 16, 3>(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*, const wsc_summary*, uint32_t*, uint32_t);
 
 }  // namespace wsc

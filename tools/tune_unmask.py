@@ -18,7 +18,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--workload", default="64k", choices=["64k", "1k", "mixed", "4k"])
 ap.add_argument("--iters", type=int, default=10)
 ap.add_argument("--rounds", type=int, default=3)
-ap.add_argument("--windows", default="4096,8192,16384")
+ap.add_argument("--windows", default="4096,8192")
 ap.add_argument("--wpc", default="8,16,32,4096")
 ap.add_argument("--nt", default="0,1,2,3")
 ap.add_argument("--minw", default="0")
