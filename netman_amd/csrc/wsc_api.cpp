@@ -272,7 +272,10 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     const uint64_t udst_bytes = compact ? 0 : b->n_bytes;
     const uint64_t wb = (uint64_t)c->pieces * 1024;
     const uint64_t n_win = (b->n_bytes + wb - 1) / wb;
-    uint64_t waves = c->cfg.unmask_waves_per_cu ? (uint64_t)c->n_cu * c->cfg.unmask_waves_per_cu : n_win;
+    // in place: one window per wave; COMPACT: a resident grid that strides over the windows so the
+    // span lookup of the next window is prefetched under the current one (wsc_unmask.inl)
+    uint64_t waves = c->cfg.unmask_waves_per_cu ? (uint64_t)c->n_cu * c->cfg.unmask_waves_per_cu
+                                                : (compact ? (uint64_t)c->n_cu * 12 : n_win);
     if (waves > n_win) waves = n_win;
     if (waves == 0) waves = 1;
     const dim3 ublk(256), ugrid((uint32_t)((waves + 3) / 4));

@@ -125,18 +125,35 @@ __device__ __forceinline__ u32x4 range_mask16(int32_t lo, int32_t hi) {
 // 16-byte piece unless spans are shorter than 16 B, which a uniform tail loop handles.  No
 // dependent scalar loads per span; in COMPACT mode all of a lane's gathers are issued together.
 // Returns false (nothing written) when more than 64 spans overlap the window.
+// lane 0's value, as a wave-uniform (scalar) value
+__device__ __forceinline__ uint64_t lane0_u64(uint64_t x) {
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)x, 0), hi = __builtin_amdgcn_readlane((uint32_t)(x >> 32), 0);
+    return (uint64_t)hi << 32 | lo;
+}
+__device__ __forceinline__ uint32_t lane0_u32(uint32_t x) { return __builtin_amdgcn_readlane(x, 0); }
+
+// The span lane r0 + lane of a window, as loaded (valid = the span exists).
+__device__ __forceinline__ bool load_span_lane(const Span* __restrict__ spans, uint32_t n_spans, uint32_t r0,
+                                               uint32_t lane, Span& sp) {
+    const uint32_t si = r0 + lane;
+    if (si < n_spans) {
+        sp = spans[si];
+        return true;
+    }
+    sp = Span{0, ~0ull, 0, 0};
+    return false;
+}
+
 template <bool COMPACT, int P, int NT>
 __device__ __forceinline__ bool unmask_window_lanes(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src,
-                                                    uint64_t src_bytes, const Span* __restrict__ spans,
+                                                    uint64_t src_bytes, const Span& sp, bool valid,
                                                     uint32_t n_spans, uint32_t r0, uint64_t wbase, uint32_t lane,
                                                     u32x4 (&v)[P]) {
     constexpr int32_t WB = 1024 * P;
-    const uint32_t si = r0 + lane;
     int32_t rd = WB + 64, re = WB + 64;   // window-relative [start, end), clipped to [-1, WB + 64]
     uint32_t key = 0;
     int64_t sd = 0;                       // COMPACT: src - dst
-    if (si < n_spans) {
-        const Span sp = spans[si];
+    if (valid) {
         const int64_t d0 = (int64_t)sp.dst - (int64_t)wbase, d1 = d0 + (int64_t)sp.len;
         rd = (int32_t)(d0 < -1 ? -1 : (d0 > WB + 64 ? WB + 64 : d0));
         re = (int32_t)(d1 < -1 ? -1 : (d1 > WB + 64 ? WB + 64 : d1));
@@ -271,6 +288,50 @@ __global__ __launch_bounds__(256, MINW) void k_unmask(uint8_t* __restrict__ dst,
     const uint32_t lofs = lane * 16u;
     if (n_spans == 0) return;
 
+    if constexpr (COMPACT) {
+        // Arena windows: the source bytes depend on the span lookup (tile -> spans -> gathers), so
+        // the lookup of window i + nw is prefetched while window i is gathered and stored: spans
+        // one window ahead (vector), the tile index two ahead (scalar).  Grid-stride over windows.
+        uint64_t win = gw;
+        if (win >= n_win) return;
+        uint32_t r = tile_first[win];
+        Span sp;
+        bool sv = load_span_lane(spans, n_spans, r, lane, sp);
+        uint32_t r_next = win + nw < n_win ? tile_first[win + nw] : 0u;
+        while (true) {
+            const uint64_t wbase = win * WB;
+            const uint64_t nx = win + nw;
+            const Span cur = sp;
+            const bool cv = sv;
+            const uint32_t rc = r;
+            if (nx < n_win) {   // prefetch
+                r = r_next;
+                sv = load_span_lane(spans, n_spans, r, lane, sp);
+                r_next = nx + nw < n_win ? tile_first[nx + nw] : 0u;
+            }
+            const uint64_t s_dst = lane0_u64(cur.dst), s_end = s_dst + lane0_u32(cur.len);
+            if (wbase + WB > total) {
+                unmask_window_general<COMPACT, P, NT>(dst, src, src_bytes, total, spans, n_spans, rc, wbase, lofs);
+            } else if (lane0_u32(cv) && s_dst <= wbase && s_end >= wbase + WB) {
+                // one span covers the whole window -> gather with one shift, one rotated key
+                const int64_t so = (int64_t)lane0_u64(cur.src) - (int64_t)s_dst;
+                const uint32_t key = lane0_u32(cur.key);
+                uint4 t[P];
+#pragma unroll
+                for (int k = 0; k < P; ++k) t[k] = gather16(src, so + (int64_t)(wbase + k * 1024u + lofs), src_bytes);
+#pragma unroll
+                for (int k = 0; k < P; ++k) st16v<NT>(dst + wbase + k * 1024u + lofs, u32x4{t[k].x, t[k].y, t[k].z, t[k].w} ^ key);
+            } else {
+                u32x4 vv[P];
+                if (!unmask_window_lanes<COMPACT, P, NT>(dst, src, src_bytes, cur, cv, n_spans, rc, wbase, lane, vv))
+                    unmask_window_general<COMPACT, P, NT>(dst, src, src_bytes, total, spans, n_spans, rc, wbase, lofs);
+            }
+            if (nx >= n_win) break;
+            win = nx;
+        }
+        return;
+    }
+
     for (uint64_t win = gw; win < n_win; win += nw) {
         const uint64_t wbase = win * WB;
         if (wbase + WB > total) {   // the last, partial window
@@ -279,37 +340,26 @@ __global__ __launch_bounds__(256, MINW) void k_unmask(uint8_t* __restrict__ dst,
             continue;
         }
         u32x4 v[P];
-        if constexpr (!COMPACT) {
-            // in place the loads do not depend on the span lookup: issue them first
+        // in place the loads do not depend on the span lookup: issue them first
 #pragma unroll
-            for (int k = 0; k < P; ++k) v[k] = ld16v<NT>(dst + wbase + k * 1024u + lofs);
-        }
-        uint32_t r = tile_first[win];
-        Span sp = spans[r < n_spans ? r : n_spans - 1];
-        if (r >= n_spans) sp.dst = ~0ull;   // no span starts before the window's end
-        if (sp.dst <= wbase && sp.dst + sp.len >= wbase + WB) {
+        for (int k = 0; k < P; ++k) v[k] = ld16v<NT>(dst + wbase + k * 1024u + lofs);
+        // the fast-path test uses scalar loads (lgkmcnt), so it never waits behind the data loads
+        const uint32_t r = tile_first[win];
+        Span s0 = spans[r < n_spans ? r : n_spans - 1];
+        if (r >= n_spans) s0.dst = ~0ull;   // no span starts before the window's end
+        if (s0.dst <= wbase && s0.dst + s0.len >= wbase + WB) {
             // fast path: one span covers the whole window -> one rotated key for every dword
-            if constexpr (COMPACT) {
-                const int64_t so = (int64_t)sp.src - (int64_t)sp.dst;
 #pragma unroll
-                for (int k = 0; k < P; ++k) {
-                    const uint4 t = load16_unaligned(src, so + (int64_t)(wbase + k * 1024u + lofs), src_bytes);
-                    v[k] = u32x4{t.x, t.y, t.z, t.w};
-                }
-            }
-#pragma unroll
-            for (int k = 0; k < P; ++k) {
-                v[k] ^= sp.key;
-                st16v<NT>(dst + wbase + k * 1024u + lofs, v[k]);
-            }
+            for (int k = 0; k < P; ++k) st16v<NT>(dst + wbase + k * 1024u + lofs, v[k] ^ s0.key);
             continue;
         }
         // Several spans overlap the window (small frames) or it holds a frame edge: lane-parallel
         // span lookup; more than 64 spans in one window falls back to the serial span walk.
-        if (!unmask_window_lanes<COMPACT, P, NT>(dst, src, src_bytes, spans, n_spans, r, wbase, lane, v))
+        Span sp;
+        const bool valid = load_span_lane(spans, n_spans, r, lane, sp);
+        if (!unmask_window_lanes<COMPACT, P, NT>(dst, src, src_bytes, sp, valid, n_spans, r, wbase, lane, v))
             unmask_window_general<COMPACT, P, NT>(dst, src, src_bytes, total, spans, n_spans, r, wbase, lofs);
     }
 }
-
 
 }  // namespace wsc

@@ -15,7 +15,7 @@ from netman_amd import codec as K  # noqa: E402
 from netman_amd import synth  # noqa: E402
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--workload", default="64k", choices=["64k", "1k", "mixed", "4k"])
+ap.add_argument("--workload", default="64k", choices=["64k", "1k", "mixed", "4k", "frag"])
 ap.add_argument("--iters", type=int, default=10)
 ap.add_argument("--rounds", type=int, default=3)
 ap.add_argument("--windows", default="4096,8192")
@@ -30,8 +30,11 @@ elif a.workload == "4k":
     cfg = synth.uniform_batch(262144, 4096, 16, seed=synth.SEED_BASE + 3)
 elif a.workload == "1k":
     cfg = synth.uniform_batch(1 << 20, 1024, 16, seed=synth.SEED_BASE + 1)
+elif a.workload == "frag":
+    cfg = synth.fragmented_batch()
 else:
     cfg = synth.mixed_batch()
+compact = a.workload == "frag"
 dev = torch.device("cuda:0")
 n_segs = len(cfg["seg_off"]) - 1
 wire = torch.from_numpy(cfg["wire"]).to(dev)
@@ -40,6 +43,8 @@ st_out = torch.zeros(n_segs * 16, dtype=torch.uint8, device=dev)
 seg_out = torch.zeros(n_segs * 32, dtype=torch.uint8, device=dev)
 frames = torch.zeros((cfg["n_frames"] + 16) * 32, dtype=torch.uint8, device=dev)
 summ = torch.zeros(32, dtype=torch.uint8, device=dev)
+arena = torch.zeros(len(cfg["wire"]) + 64, dtype=torch.uint8, device=dev) if compact else None
+fdst = torch.zeros(cfg["n_frames"] + 16, dtype=torch.int64, device=dev) if compact else None
 hdr = np.where(cfg["plen"] <= 125, 6, np.where(cfg["plen"] <= 65535, 8, 14))
 alg = int((2 * cfg["plen"].astype(np.int64) + hdr + 32).sum())
 combos = list(itertools.product([int(x) for x in a.windows.split(",")], [int(x) for x in a.wpc.split(",")],
@@ -53,7 +58,7 @@ res = {c: [] for c in combos}
 for r in range(a.rounds):
     for c in combos:
         cd = codecs[c]
-        b = cd.make_batch(wire, seg_off, None, st_out, seg_out, frames, summ)
+        b = cd.make_batch(wire, seg_off, None, st_out, seg_out, frames, summ, compact=compact, arena=arena, frame_dst=fdst)
         p = cd.profile(b, a.iters)
         res[c].append(p)
 rows = []
