@@ -45,6 +45,7 @@ def parse():
     ap.add_argument("--pipeline", type=int, default=2,
                     help="batches in flight: each has its own context, wire buffer and HIP stream, so the "
                          "header walk of batch k+1 overlaps the unmask of batch k")
+    ap.add_argument("--no-echo", action="store_true", help="skip the configs[0] loopback echo lines")
     ap.add_argument("--no-other-configs", action="store_true",
                     help="skip the device-time lines for BASELINE.json configs[1], [2], [4]")
     return ap.parse_args()
@@ -227,6 +228,8 @@ def main():
         torch.cuda.empty_cache()
         out["other_configs"] = other_configs(torch, K, synth)
         out["encode"] = encode_configs(torch, K, synth)
+    if rank == 0 and not a.no_echo:
+        out["echo"] = echo_configs(with_cpu=not a.no_cpu)
     if rank == 0 and not a.no_cpu and a.cpu_seconds > 0:
         threads = min(16, len(os.sched_getaffinity(0)))
         v1, p1, e1 = cpu_baseline(cfg, a.cpu_seconds / 2, 1)
@@ -328,6 +331,37 @@ def encode_configs(torch, K, synth):
         c.close()
         del src, d_msgs, d_out, d_off
         torch.cuda.empty_cache()
+    return res
+
+
+def echo_configs(with_cpu=True):
+    """configs[0]: examples/websocket echo on loopback, rebuilt around a pluggable decoder
+    (tools/echo_harness.hpp; the Go reference server cannot run here).  gpu = tools/ws_echo
+    (libwscodec wsc_session, one device decode per poller round); cpu = oracle/_build/ws_echo_cpu,
+    the reference's frame-at-a-time decode ported to C++ (cpu_baseline leg, kind "port").  Each
+    run is a separate process; msgs/s and GiB/s of echoed payload, every byte checked."""
+    import subprocess
+    runs = [("1 conn x 4000 x 64 KiB (configs[0])", ["--conns", "1", "--frames", "4000", "--size", "65536"]),
+            ("64 conns x 200 x 64 KiB", ["--conns", "64", "--frames", "200", "--size", "65536", "--client-threads", "4"]),
+            ("64 conns x 2000 x 1 KiB", ["--conns", "64", "--frames", "2000", "--size", "1024", "--client-threads", "4"])]
+    bins = [("gpu", os.path.join(ROOT, "tools", "ws_echo"))]
+    if with_cpu:
+        bins.append(("cpu_port", os.path.join(ROOT, "oracle", "_build", "ws_echo_cpu")))
+    res = {}
+    for name, args in runs:
+        row = {}
+        for kind, exe in bins:
+            if not os.path.exists(exe):
+                row[kind] = None
+                continue
+            try:
+                p = subprocess.run([exe] + args, capture_output=True, text=True, timeout=120)
+                line = [x for x in p.stdout.splitlines() if x.startswith("{")]
+                d = json.loads(line[-1]) if line else {"ok": False, "error": p.stderr[-300:]}
+                row[kind] = {k: d.get(k) for k in ("ok", "gib_s", "msgs_per_s", "seconds", "rounds", "error")}
+            except Exception as e:   # the echo lines are reported beside the metric, never fatal
+                row[kind] = {"ok": False, "error": repr(e)[:200]}
+        res[name] = row
     return res
 
 

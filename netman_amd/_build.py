@@ -48,6 +48,22 @@ def build_codec(force=False, verbose=False):
     return LIB
 
 
+TOOLS = os.path.join(ROOT, "tools")
+ECHO = os.path.join(TOOLS, "ws_echo")
+
+
+def build_tools(force=False):
+    """tools/ws_echo (configs[0] loopback echo through libwscodec's wsc_session); needs the library"""
+    src = os.path.join(TOOLS, "ws_echo.cpp")
+    deps = [src, os.path.join(TOOLS, "echo_harness.hpp"), os.path.join(ROOT, "include", "wscodec.h"), LIB]
+    if not force and os.path.exists(ECHO) and os.path.getmtime(ECHO) >= _newest(deps):
+        return ECHO
+    cmd = ["g++", "-O2", "-std=c++17", "-Wall", "-pthread", "-o", ECHO, src, "-L" + HERE, "-lwscodec",
+           "-Wl,-rpath,$ORIGIN/../netman_amd", "-Wl,-rpath,/opt/rocm/lib"]
+    subprocess.run(cmd, check=True)
+    return ECHO
+
+
 def build_oracle(force=False):
     subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")] + (["-B"] if force else []),
                    check=True)

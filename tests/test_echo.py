@@ -1,0 +1,44 @@
+"""configs[0] loopback echo harness (tools/echo_harness.hpp): every echoed frame is checked byte for
+byte by the client threads.  CPU: the reference-port twin (oracle/_build/ws_echo_cpu); GPU: the
+product binary tools/ws_echo over libwscodec's wsc_session."""
+import json
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(exe, *args):
+    p = subprocess.run([exe, *args], capture_output=True, text=True, timeout=120)
+    line = [x for x in p.stdout.splitlines() if x.startswith("{")]
+    assert line, p.stderr
+    return p.returncode, json.loads(line[-1])
+
+
+@pytest.fixture(scope="module")
+def cpu_echo():
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    return os.path.join(ROOT, "oracle", "_build", "ws_echo_cpu")
+
+
+@pytest.mark.parametrize("args", [("--conns", "1", "--frames", "50", "--size", "65536"),
+                                  ("--conns", "8", "--frames", "40", "--size", "70000", "--client-threads", "2"),
+                                  ("--conns", "16", "--frames", "300", "--size", "100", "--client-threads", "4")])
+def test_cpu_echo_roundtrip(cpu_echo, args):
+    rc, d = _run(cpu_echo, *args)
+    assert rc == 0 and d["ok"], d
+    assert d["messages"] == int(args[1]) * int(args[3])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("args", [("--conns", "1", "--frames", "200", "--size", "65536"),
+                                  ("--conns", "32", "--frames", "50", "--size", "70000", "--client-threads", "4"),
+                                  ("--conns", "16", "--frames", "500", "--size", "125", "--client-threads", "4")])
+def test_gpu_echo_roundtrip(codec_lib, args):
+    from netman_amd import _build
+    exe = _build.build_tools()
+    rc, d = _run(exe, *args)
+    assert rc == 0 and d["ok"], d
+    assert d["messages"] == int(args[1]) * int(args[3])

@@ -1,0 +1,336 @@
+// echo_harness.hpp -- loopback WebSocket echo harness for configs[0] of BASELINE.json (the
+// reference's examples/websocket echo server needs Go, which this image and the GPU box lack, so
+// the harness rebuilds the same traffic around a pluggable decoder).
+//
+// One server thread plays one netman poller (eventloop/epoll.go:36-143): level-triggered epoll,
+// ONE bulk read per ready connection per round fed to a Decoder, one decode pass per round, then
+// every delivered message echoed as an unmasked server frame -- the examples/websocket handler's
+// connect.Binary(message.Bytes()) (examples/websocket/server.go:30-44, encode at
+// server/websocket_ctrl.go:23-70; the handler's fmt.Println is left out).  Client threads send
+// `frames` masked 0x82 frames of `frame_bytes` per connection and check every echoed byte.
+//
+// The Decoder is what the two binaries differ in:
+//   tools/ws_echo.cpp       product path: libwscodec's wsc_session, one batched device decode per round
+//   oracle/ws_echo_cpu.cpp  CPU baseline: a port of the reference's frame-at-a-time Go decode
+// The handshake (once per connection, CPU, websocket.go:315-375) is not part of the timed loop.
+#pragma once
+#include <arpa/inet.h>
+#include <fcntl.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <sys/epoll.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <chrono>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace echo {
+
+struct Decoder {
+    virtual ~Decoder() = default;
+    virtual int open() = 0;                                               // newWebsocketProtocol
+    virtual void feed(int conn, const uint8_t* p, size_t n) = 0;          // one bulk read
+    virtual void decode() = 0;                                            // once per poller round
+    virtual bool next(int conn, const uint8_t** data, size_t* len) = 0;   // DecodePacket() -> message
+};
+
+struct Result {
+    double seconds = 0;
+    uint64_t messages = 0;
+    uint64_t payload_bytes = 0;
+    uint64_t rounds = 0;   // server epoll rounds that decoded something (= decode passes)
+    bool ok = false;
+    std::string error;
+};
+
+inline void set_nonblock(int fd) { fcntl(fd, F_SETFL, fcntl(fd, F_GETFL) | O_NONBLOCK); }
+
+inline void big_buffers(int fd) {
+    const int sz = 8 << 20;
+    setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &sz, sizeof(sz));
+    setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &sz, sizeof(sz));
+}
+
+// frame header: first byte, minimal 7/16/64-bit big-endian length (websocket_ctrl.go:23-70)
+inline size_t put_header(uint8_t* h, uint8_t first, uint64_t n) {
+    h[0] = first;
+    if (n <= 125) { h[1] = (uint8_t)n; return 2; }
+    if (n <= 65535) { h[1] = 126; h[2] = (uint8_t)(n >> 8); h[3] = (uint8_t)n; return 4; }
+    h[1] = 127;
+    for (int k = 0; k < 8; ++k) h[2 + k] = (uint8_t)(n >> (56 - 8 * k));
+    return 10;
+}
+
+struct ServerConn {
+    int fd = -1;
+    int id = -1;
+    std::vector<uint8_t> out;   // echo bytes not yet written
+    size_t out_pos = 0;
+    bool want_out = false;
+};
+
+inline Result run(Decoder& dec, int conns, int frames, size_t frame_bytes, int client_threads, int timeout_s = 60) {
+    Result res;
+    const int lfd = socket(AF_INET, SOCK_STREAM, 0);
+    int one = 1;
+    setsockopt(lfd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+    sockaddr_in a{};
+    a.sin_family = AF_INET;
+    a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+    a.sin_port = 0;
+    if (bind(lfd, (sockaddr*)&a, sizeof(a)) || listen(lfd, 1024)) {
+        res.error = "bind/listen";
+        return res;
+    }
+    socklen_t al = sizeof(a);
+    getsockname(lfd, (sockaddr*)&a, &al);
+
+    // the payload every client sends (and must get back); one masked wire image per connection
+    std::vector<uint8_t> payload(frame_bytes);
+    std::mt19937_64 rng(0x57530000);
+    for (auto& b : payload) b = (uint8_t)rng();
+    auto make_wire = [&](uint64_t seed) {
+        std::mt19937_64 r(seed);
+        std::vector<uint8_t> w;
+        w.reserve((frame_bytes + 14) * (size_t)frames);
+        for (int f = 0; f < frames; ++f) {
+            uint8_t h[14];
+            const size_t hl = put_header(h, 0x82, frame_bytes);
+            h[1] |= 0x80;   // MASK
+            const uint32_t m = (uint32_t)r();
+            std::memcpy(h + hl, &m, 4);
+            w.insert(w.end(), h, h + hl + 4);
+            const uint8_t* mb = h + hl;
+            const size_t at = w.size();
+            w.resize(at + frame_bytes);
+            for (size_t i = 0; i < frame_bytes; ++i) w[at + i] = payload[i] ^ mb[i & 3];
+        }
+        return w;
+    };
+    const size_t frame_out = frame_bytes + (frame_bytes <= 125 ? 2 : (frame_bytes <= 65535 ? 4 : 10));
+
+    std::atomic<int> client_fail{0};
+    std::atomic<uint64_t> client_msgs{0};
+    std::atomic<bool> go{false};
+    std::atomic<int> ready{0};   // clients whose wire images are built (not timed)
+    std::vector<std::thread> clients;
+    for (int t = 0; t < client_threads; ++t) {
+        clients.emplace_back([&, t] {
+            std::vector<int> fds;
+            std::vector<std::vector<uint8_t>> wires;
+            for (int c = t; c < conns; c += client_threads) {
+                const int fd = socket(AF_INET, SOCK_STREAM, 0);
+                if (connect(fd, (sockaddr*)&a, sizeof(a))) {
+                    client_fail++;
+                    return;
+                }
+                setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+                big_buffers(fd);
+                set_nonblock(fd);
+                fds.push_back(fd);
+                wires.push_back(make_wire(1000 + (uint64_t)c));
+            }
+            ready++;
+            while (!go.load()) std::this_thread::yield();
+            const int ep = epoll_create1(0);
+            for (size_t i = 0; i < fds.size(); ++i) {
+                epoll_event e{};
+                e.events = EPOLLIN | EPOLLOUT;
+                e.data.u64 = i;
+                epoll_ctl(ep, EPOLL_CTL_ADD, fds[i], &e);
+            }
+            std::vector<size_t> sent(fds.size(), 0);
+            std::vector<std::vector<uint8_t>> inbuf(fds.size());
+            std::vector<int> got(fds.size(), 0);
+            size_t done = 0;
+            std::vector<uint8_t> rb(1 << 20);
+            epoll_event evs[256];
+            uint8_t want_h[10];
+            const size_t want_hl = put_header(want_h, 0x82, frame_bytes);
+            const auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(timeout_s);
+            while (done < fds.size() && client_fail.load() == 0) {
+                if (std::chrono::steady_clock::now() > deadline) {
+                    client_fail++;
+                    break;
+                }
+                const int n = epoll_wait(ep, evs, 256, 100);
+                for (int k = 0; k < n; ++k) {
+                    const size_t i = evs[k].data.u64;
+                    if ((evs[k].events & EPOLLOUT) && sent[i] < wires[i].size()) {
+                        while (sent[i] < wires[i].size()) {   // until the socket buffer is full
+                            const ssize_t w = send(fds[i], wires[i].data() + sent[i], wires[i].size() - sent[i], MSG_NOSIGNAL);
+                            if (w <= 0) break;
+                            sent[i] += (size_t)w;
+                        }
+                        if (sent[i] == wires[i].size()) {
+                            epoll_event e{};
+                            e.events = EPOLLIN;
+                            e.data.u64 = i;
+                            epoll_ctl(ep, EPOLL_CTL_MOD, fds[i], &e);
+                        }
+                    }
+                    if (evs[k].events & EPOLLIN) {
+                        while (true) {
+                            const ssize_t r = recv(fds[i], rb.data(), rb.size(), 0);
+                            if (r <= 0) break;
+                            inbuf[i].insert(inbuf[i].end(), rb.data(), rb.data() + r);
+                        }
+                        size_t p = 0;   // every complete echoed frame must equal header + payload
+                        while (inbuf[i].size() - p >= frame_out) {
+                            const uint8_t* f = inbuf[i].data() + p;
+                            if (std::memcmp(f, want_h, want_hl) || std::memcmp(f + want_hl, payload.data(), frame_bytes)) {
+                                client_fail++;
+                                break;
+                            }
+                            p += frame_out;
+                            client_msgs++;
+                            if (++got[i] == frames) done++;
+                        }
+                        inbuf[i].erase(inbuf[i].begin(), inbuf[i].begin() + (long)p);
+                    }
+                }
+            }
+            close(ep);
+            for (int fd : fds) close(fd);
+        });
+    }
+
+    // server: accept every connection, then the poller loop
+    std::vector<ServerConn> sc;
+    const int ep = epoll_create1(0);
+    while ((int)sc.size() < conns && client_fail.load() == 0) {
+        const int fd = accept(lfd, nullptr, nullptr);
+        if (fd < 0) {
+            res.error = "accept";
+            break;
+        }
+        set_nonblock(fd);
+        setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+        big_buffers(fd);
+        ServerConn c;
+        c.fd = fd;
+        c.id = dec.open();
+        epoll_event e{};
+        e.events = EPOLLIN;
+        e.data.u64 = sc.size();
+        epoll_ctl(ep, EPOLL_CTL_ADD, fd, &e);
+        sc.push_back(c);
+    }
+    std::vector<uint8_t> rb(4 << 20);
+    std::vector<size_t> fed;
+    epoll_event evs[1024];
+    uint64_t served = 0;
+    const uint64_t want = (uint64_t)conns * (uint64_t)frames;
+    while (ready.load() < client_threads && client_fail.load() == 0) std::this_thread::yield();
+    const auto t0 = std::chrono::steady_clock::now();
+    go = true;
+    const auto deadline = t0 + std::chrono::seconds(timeout_s);
+    while (res.error.empty() && served < want && client_fail.load() == 0) {
+        if (std::chrono::steady_clock::now() > deadline) {
+            res.error = "server timeout";
+            break;
+        }
+        const int n = epoll_wait(ep, evs, 1024, 100);
+        fed.clear();
+        for (int k = 0; k < n; ++k) {
+            ServerConn& c = sc[evs[k].data.u64];
+            if (evs[k].events & EPOLLIN) {
+                const ssize_t r = recv(c.fd, rb.data(), rb.size(), 0);   // ONE bulk read per event
+                if (r > 0) {
+                    dec.feed(c.id, rb.data(), (size_t)r);
+                    fed.push_back(evs[k].data.u64);
+                }
+            }
+        }
+        if (!fed.empty()) {
+            dec.decode();
+            res.rounds++;
+        }
+        for (size_t q : fed) {   // drain the round: every delivered message is echoed
+            ServerConn& c = sc[q];
+            const uint8_t* d;
+            size_t len;
+            while (dec.next(c.id, &d, &len)) {
+                uint8_t h[10];
+                const size_t hl = put_header(h, 0x82, len);
+                c.out.insert(c.out.end(), h, h + hl);
+                c.out.insert(c.out.end(), d, d + len);
+                served++;
+                res.payload_bytes += len;
+            }
+        }
+        for (size_t i = 0; i < sc.size(); ++i) {
+            ServerConn& c = sc[i];
+            while (c.out_pos < c.out.size()) {   // until the socket buffer is full
+                const ssize_t w = send(c.fd, c.out.data() + c.out_pos, c.out.size() - c.out_pos, MSG_NOSIGNAL);
+                if (w <= 0) break;
+                c.out_pos += (size_t)w;
+            }
+            if (c.out_pos == c.out.size()) {
+                c.out.clear();
+                c.out_pos = 0;
+            }
+            const bool need = c.out_pos < c.out.size();
+            if (need != c.want_out) {
+                epoll_event e{};
+                e.events = EPOLLIN | (need ? EPOLLOUT : 0u);
+                e.data.u64 = i;
+                epoll_ctl(ep, EPOLL_CTL_MOD, c.fd, &e);
+                c.want_out = need;
+            }
+        }
+    }
+    // flush what is left, then wait for the clients to have checked every echo
+    for (auto& c : sc) {
+        while (c.out_pos < c.out.size() && client_fail.load() == 0 && res.error.empty()) {
+            const ssize_t w = send(c.fd, c.out.data() + c.out_pos, c.out.size() - c.out_pos, MSG_NOSIGNAL);
+            if (w > 0) c.out_pos += (size_t)w;
+            else std::this_thread::yield();
+        }
+    }
+    if (!res.error.empty()) client_fail++;   // release the client threads
+    for (auto& t : clients) t.join();
+    const auto t1 = std::chrono::steady_clock::now();
+    res.seconds = std::chrono::duration<double>(t1 - t0).count();
+    res.messages = served;
+    res.ok = res.error.empty() && client_fail.load() == 0 && client_msgs.load() == want;
+    if (!res.ok && res.error.empty()) res.error = "client check failed";
+    for (auto& c : sc) close(c.fd);
+    close(ep);
+    close(lfd);
+    return res;
+}
+
+inline void print_json(const char* codec, const Result& r, int conns, int frames, size_t frame_bytes) {
+    printf("{\"codec\": \"%s\", \"ok\": %s, \"connections\": %d, \"frames_per_conn\": %d, \"frame_bytes\": %zu, "
+           "\"seconds\": %.4f, \"messages\": %llu, \"msgs_per_s\": %.1f, \"gib_s\": %.3f, \"rounds\": %llu, "
+           "\"error\": \"%s\"}\n",
+           codec, r.ok ? "true" : "false", conns, frames, frame_bytes, r.seconds, (unsigned long long)r.messages,
+           r.seconds > 0 ? (double)r.messages / r.seconds : 0.0,
+           r.seconds > 0 ? (double)r.payload_bytes / r.seconds / 1073741824.0 : 0.0, (unsigned long long)r.rounds,
+           r.error.c_str());
+}
+
+inline void parse_args(int argc, char** argv, int& conns, int& frames, size_t& frame_bytes, int& threads) {
+    for (int i = 1; i + 1 < argc; i += 2) {
+        const std::string k = argv[i];
+        if (k == "--conns") conns = atoi(argv[i + 1]);
+        else if (k == "--frames") frames = atoi(argv[i + 1]);
+        else if (k == "--size") frame_bytes = (size_t)atoll(argv[i + 1]);
+        else if (k == "--client-threads") threads = atoi(argv[i + 1]);
+    }
+    if (conns < 1) conns = 1;
+    if (threads > conns) threads = conns;
+    if (threads < 1) threads = 1;
+}
+
+}  // namespace echo
