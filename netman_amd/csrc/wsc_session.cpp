@@ -16,6 +16,9 @@
 // continueBuffer for fragmented messages, and the device-visible wsc_conn_state.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <string>
@@ -27,7 +30,9 @@ namespace {
 
 struct Event {
     wsc_event ev;
-    std::vector<uint8_t> data;
+    std::vector<uint8_t> data;     // owned copy (fragmented messages, earlier batches of a decode)
+    const uint8_t* view = nullptr; // zero-copy: points into the pinned staging of the last batch
+    uint64_t view_len = 0;
 };
 
 struct Conn {
@@ -61,7 +66,15 @@ struct wsc_session {
     wsc_seg_result* h_seg_out = nullptr;
     wsc_frame* h_frames = nullptr;
     uint64_t* h_frame_dst = nullptr;
+    // WSC_SESSION_TIMING=1: seconds spent per phase of wsc_session_decode, printed at destroy
+    bool timing = false;
+    double t_pack = 0, t_device = 0, t_harvest = 0;
+    uint64_t n_decodes = 0, n_bytes = 0;
 };
+
+static double now_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 
 extern "C" {
 
@@ -91,12 +104,16 @@ int wsc_session_create(int device, const wsc_config* cfg, uint32_t flags, wsc_se
     s->h_frames = (wsc_frame*)H((uint64_t)g.max_frames * sizeof(wsc_frame));
     s->h_frame_dst = (uint64_t*)H((uint64_t)g.max_frames * sizeof(uint64_t));
     if (rc) { wsc_session_destroy(s); return rc; }
+    if (const char* e = std::getenv("WSC_SESSION_TIMING"); e && e[0] == '1') s->timing = true;
     *out = s;
     return WSC_OK;
 }
 
 int wsc_session_destroy(wsc_session* s) {
     if (!s) return WSC_OK;
+    if (s->timing)
+        fprintf(stderr, "wsc_session: %llu decodes, %llu bytes: pack %.4f s, device (H2D+kernels+D2H) %.4f s, harvest %.4f s\n",
+                (unsigned long long)s->n_decodes, (unsigned long long)s->n_bytes, s->t_pack, s->t_device, s->t_harvest);
     void* ps[] = {s->h_wire, s->h_arena, s->h_seg_off, s->h_state_in, s->h_state_out,
                   s->h_seg_out, s->h_frames, s->h_frame_dst};
     for (void* p : ps)
@@ -134,8 +151,11 @@ int wsc_session_feed(wsc_session* s, uint32_t conn, const uint8_t* bytes, uint64
 }
 
 // turn one segment's frame records into the DecodePacket results the reference would return
+// zero_copy: the staging stays untouched until the next wsc_session_decode (this is the decode's
+// last device batch), so complete single-frame messages and PING payloads are handed out as views
+// into it instead of copies; wsc_event.data's lifetime is exactly that (include/wscodec.h).
 static void harvest(wsc_session* s, Conn& c, const uint8_t* seg, const wsc_seg_result& r,
-                    const wsc_conn_state& so, uint64_t seg_base) {
+                    const wsc_conn_state& so, uint64_t seg_base, bool zero_copy) {
     const bool compact = (s->flags & WSC_F_COMPACT) != 0;
     for (uint32_t i = r.frame_begin; i < r.frame_begin + r.frame_count; ++i) {
         const wsc_frame& f = s->h_frames[i];
@@ -151,6 +171,9 @@ static void harvest(wsc_session* s, Conn& c, const uint8_t* seg, const wsc_seg_r
             if (f.flags & WSC_FF_CONT_MSG) {
                 e.data.swap(c.cont);
                 e.data.insert(e.data.end(), p, p + f.payload_len);
+            } else if (zero_copy) {
+                e.view = p;
+                e.view_len = f.payload_len;
             } else {
                 e.data.assign(p, p + f.payload_len);
             }
@@ -159,7 +182,12 @@ static void harvest(wsc_session* s, Conn& c, const uint8_t* seg, const wsc_seg_r
             e.ev.opcode = f.mode;
             break;
         case WSC_FK_PING:                                     // websocket_ctrl.go:128-153
-            e.data.assign(p, p + f.payload_len);
+            if (zero_copy) {
+                e.view = p;
+                e.view_len = f.payload_len;
+            } else {
+                e.data.assign(p, p + f.payload_len);
+            }
             e.ev.type = WSC_EV_PONG;
             break;
         case WSC_FK_PONG:
@@ -199,11 +227,17 @@ int wsc_session_decode(wsc_session* s) {
     std::vector<uint32_t> ids;
     for (uint32_t i = 0; i < s->conns.size(); ++i) {
         Conn& c = s->conns[i];
+        for (Event& e : c.pending)   // undrained zero-copy views: the staging is about to be reused
+            if (e.view) {
+                e.data.assign(e.view, e.view + e.view_len);
+                e.view = nullptr;
+            }
         if (c.live && c.st.status == WSC_SEG_OPEN && !c.fed.empty()) ids.push_back(i);
     }
     size_t k = 0;
     while (k < ids.size()) {
         // pack as many connections as fit into one device batch
+        const double t0 = s->timing ? now_s() : 0;
         uint64_t bytes = 0;
         uint32_t n = 0;
         size_t j = k;
@@ -222,14 +256,25 @@ int wsc_session_decode(wsc_session* s) {
             ++j;
         }
         s->h_seg_off[n] = bytes;
+        const double t1 = s->timing ? now_s() : 0;
         wsc_summary sm;
         int rc = wsc_decode_host(s->ctx, s->h_wire, bytes, s->h_seg_off, n, s->flags, s->h_state_in,
                                  s->h_state_out, s->h_seg_out, s->h_frames, g.max_frames, s->h_arena,
                                  s->h_frame_dst, &sm);
         if (rc) return rc;
+        const double t2 = s->timing ? now_s() : 0;
         for (uint32_t q = 0; q < n; ++q) {
             Conn& c = s->conns[ids[k + q]];
-            harvest(s, c, s->h_wire + s->h_seg_off[q], s->h_seg_out[q], s->h_state_out[q], s->h_seg_off[q]);
+            harvest(s, c, s->h_wire + s->h_seg_off[q], s->h_seg_out[q], s->h_state_out[q], s->h_seg_off[q],
+                    j == ids.size());
+        }
+        if (s->timing) {
+            const double t3 = now_s();
+            s->t_pack += t1 - t0;
+            s->t_device += t2 - t1;
+            s->t_harvest += t3 - t2;
+            s->n_decodes += 1;
+            s->n_bytes += bytes;
         }
         k = j;
     }
@@ -244,8 +289,13 @@ int wsc_session_next(wsc_session* s, uint32_t conn, wsc_event* ev) {
     c.current = std::move(c.pending.front());
     c.pending.pop_front();
     *ev = c.current.ev;
-    ev->data = c.current.data.empty() ? nullptr : c.current.data.data();
-    ev->len = c.current.data.size();
+    if (c.current.view) {
+        ev->data = c.current.view_len ? c.current.view : nullptr;
+        ev->len = c.current.view_len;
+    } else {
+        ev->data = c.current.data.empty() ? nullptr : c.current.data.data();
+        ev->len = c.current.data.size();
+    }
     return WSC_OK;
 }
 

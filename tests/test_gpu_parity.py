@@ -308,3 +308,25 @@ def test_compact_decode_is_deterministic(codec_lib):
     sm = first[3].view(K.SUMMARY_DTYPE)[0]
     assert int(sm["overflow"]) == 0 and int(sm["n_frames"]) == cfg["n_frames"]
     c.close()
+
+
+def test_session_undrained_events_survive_next_decode(codec_lib):
+    """messages are handed out as zero-copy views into the pinned staging; events not drained
+    before the next wsc_session_decode must still carry their own bytes afterwards"""
+    sess = K.Session(0, max_batch_bytes=1 << 20, max_segs=16, max_frames=1024)
+    a, b = sess.open(), sess.open()
+    pa = [bytes([i]) * (100 + i) for i in range(5)]
+    sess.feed(a, b"".join(synth.frame(2, p, mask=0x01020304 + i) for i, p in enumerate(pa)))
+    sess.feed(b, synth.frame(9, b"ping-b"))
+    sess.decode()
+    first = sess.next_event(a)                        # drained: valid until the next decode
+    assert first.data == pa[0]
+    sess.feed(a, synth.frame(2, b"\xee" * 5000, mask=0xAABBCCDD))
+    sess.feed(b, synth.frame(1, "καλημέρα".encode()))
+    sess.decode()                                     # reuses the staging
+    rest = sess.events(a)
+    assert [e.data for e in rest] == pa[1:] + [b"\xee" * 5000]
+    eb = sess.events(b)
+    assert eb[0].type == K.EV_PONG and eb[0].data == b"ping-b"
+    assert eb[1].type == K.EV_MESSAGE and eb[1].data == "καλημέρα".encode()
+    sess.close()

@@ -14,7 +14,7 @@ struct GpuDecoder : echo::Decoder {
     explicit GpuDecoder(int conns) {
         wsc_config cfg;
         wsc_config_default(&cfg);
-        cfg.max_batch_bytes = 64ull << 20;
+        cfg.max_batch_bytes = 320ull << 20;   // one device batch per poller round (64 conns x 4 MiB reads)
         cfg.max_segs = (uint32_t)conns + 16;
         cfg.max_frames = 1u << 18;
         if (wsc_session_create(0, &cfg, 0, &s) != WSC_OK) {
