@@ -251,7 +251,11 @@ def other_configs(torch, K, synth):
     res = {}
     cases = [("configs[1] 1M x 1 KiB BIN, 16 frames/segment", lambda: synth.uniform_batch(1 << 20, 1024, 16, seed=synth.SEED_BASE + 1), False),
              ("configs[2] 256k mixed 125 B / 64 KiB / 1 MiB (p~1/size)", lambda: synth.mixed_batch(), False),
-             ("configs[4] 64k connections x fragmented message, reassembled (COMPACT)", lambda: synth.fragmented_batch(), True)]
+             ("configs[4] 64k connections x fragmented message, reassembled (COMPACT)", lambda: synth.fragmented_batch(), True),
+             ("TEXT 16384 x 64 KiB valid UTF-8 (1-4 byte characters), 4 frames/segment",
+              lambda: synth.text_batch(16384, 65536, 4, seed=synth.SEED_BASE + 7), False),
+             ("TEXT 262144 x 1 KiB valid UTF-8, 16 frames/segment",
+              lambda: synth.text_batch(262144, 1024, 16, seed=synth.SEED_BASE + 8), False)]
     for name, make, compact in cases:
         cfg = make()
         n = len(cfg["seg_off"]) - 1

@@ -122,7 +122,8 @@ typedef struct wsc_seg_result {
 typedef struct wsc_summary {
     uint64_t data_bytes;   /* COMPACT: data payload bytes in the arena (all segments)            */
     uint64_t ctrl_bytes;   /* COMPACT: control payload bytes in the arena                         */
-    uint32_t n_frames;     /* frames in `frames`                                                  */
+    uint32_t n_frames;     /* records written to `frames` (a segment's frame_count can be smaller:
+                              a late UTF-8 verdict stops a segment at its failing frame)          */
     uint32_t n_spans;      /* payload spans unmasked                                              */
     uint32_t overflow;     /* bit0: n_frames > frames_cap (records beyond the cap were dropped);
                               bit1: internal look-back timeout (results invalid)                  */
@@ -213,7 +214,8 @@ int wsc_encode_host(wsc_ctx* ctx, const wsc_out_msg* msgs, uint32_t n_msgs, cons
 
 /* Timing helper for the benchmark: run `iters` back-to-back decodes of a device batch and
  * return the per-kernel average device time (ms) measured with hipEvents on the launch stream.
- * out_ms[0] = fused header walk (incl. utf8), [1], [2], [4] = 0 (reserved), [3] = unmask,
+ * out_ms[0] = fused header walk (incl. inline utf8), [1] = chip-wide utf8 check of deferred text,
+ * [2], [4] = 0 (reserved), [3] = unmask,
  * [5] = whole decode.  A context runs one decode at a time (its scratch is shared). */
 int wsc_profile(wsc_ctx* ctx, const wsc_batch* batch, int iters, double* out_ms);
 

@@ -12,6 +12,7 @@
 
 namespace wsc {
 template <bool COMPACT> __global__ void k_walk_fused(WalkArgs);
+__global__ void k_u8_check(U8Args);
 template <bool COMPACT, int P, int NT, int MINW>
 __global__ void k_unmask(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*,
                          const wsc_summary*, uint32_t*, uint32_t);
@@ -49,13 +50,19 @@ struct wsc_ctx {
     wsc_config cfg{};
     uint32_t pieces = 8;          // 16 B pieces per lane -> window = pieces KiB
     SegCount* counts = nullptr;
-    uint32_t* lb_state = nullptr;    // [0] ticket, [1] spin-timeout flag, [2..] per-block flags
+    uint32_t* lb_state = nullptr;    // [0] ticket, [1] spin-timeout flag, [2] UTF-8 item count, [3..] per-block flags
     uint32_t* u8info = nullptr;      // per segment {utf8-failing frame ordinal, DFA state}
     uint64_t* lb_agg = nullptr;
     uint64_t* lb_incl = nullptr;
     uint64_t* dbg = nullptr;         // WSC_DEBUG_STAMPS=1: per-block walk timestamps
     Span* spans = nullptr;
     uint32_t* tile = nullptr;
+    // chip-wide UTF-8 (k_u8_check): deferred items, their maps, per-segment lists
+    U8Item* u8items = nullptr;
+    uint64_t* u8maps = nullptr;
+    uint32_t u8items_cap = 0;
+    U8Seg* u8seg = nullptr;
+    uint32_t u8_inline_max = 256;
     uint64_t tile_entries = 0;
     // host-staged path buffers (lazily allocated)
     uint8_t* d_wire = nullptr;
@@ -148,19 +155,26 @@ int wsc_create(int device, const wsc_config* cfg_in, wsc_ctx** out) {
     chk(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate");
     chk(hipMalloc(&c->counts, cfg.max_segs * sizeof(SegCount)), "hipMalloc counts");
     const uint64_t max_blocks = (cfg.max_segs + 255) / 256 + 1;
-    chk(hipMalloc(&c->lb_state, (max_blocks + 2) * sizeof(uint32_t)), "hipMalloc lb_state");
+    chk(hipMalloc(&c->lb_state, (max_blocks + 3) * sizeof(uint32_t)), "hipMalloc lb_state");
     chk(hipMalloc(&c->u8info, (uint64_t)cfg.max_segs * 2 * sizeof(uint32_t)), "hipMalloc u8info");
     chk(hipMalloc(&c->lb_agg, max_blocks * 4 * sizeof(uint64_t)), "hipMalloc lb_agg");
     chk(hipMalloc(&c->lb_incl, max_blocks * 4 * sizeof(uint64_t)), "hipMalloc lb_incl");
     if (const char* e = std::getenv("WSC_DEBUG_STAMPS"); e && e[0] == '1')
         chk(hipMalloc(&c->dbg, max_blocks * 4 * sizeof(uint64_t)), "hipMalloc dbg");
     if (rc == WSC_OK) {
-        chk(hipMemsetAsync(c->lb_state, 0, (max_blocks + 2) * sizeof(uint32_t), c->stream), "hipMemset lb_state");
+        chk(hipMemsetAsync(c->lb_state, 0, (max_blocks + 3) * sizeof(uint32_t), c->stream), "hipMemset lb_state");
         chk(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
     }
     chk(hipMalloc(&c->spans, (uint64_t)cfg.max_frames * sizeof(Span)), "hipMalloc spans");
     c->tile_entries = cfg.max_batch_bytes / 1024 + 2;
     chk(hipMalloc(&c->tile, c->tile_entries * sizeof(uint32_t)), "hipMalloc tile");
+    // every frame is at most ceil(len / U8_PIECE) items: frames + bytes / U8_PIECE bounds the total
+    c->u8items_cap = cfg.max_frames + (uint32_t)(cfg.max_batch_bytes / U8_PIECE) + 64;
+    chk(hipMalloc(&c->u8items, (uint64_t)c->u8items_cap * sizeof(U8Item)), "hipMalloc u8items");
+    chk(hipMalloc(&c->u8maps, (uint64_t)c->u8items_cap * sizeof(uint64_t)), "hipMalloc u8maps");
+    chk(hipMalloc(&c->u8seg, (uint64_t)cfg.max_segs * sizeof(U8Seg)), "hipMalloc u8seg");
+    if (const char* e = std::getenv("WSC_U8_INLINE_MAX"); e && *e)   // test knob: 0 sends all text chip-wide
+        c->u8_inline_max = (uint32_t)std::strtoul(e, nullptr, 10);
     c->enc_blocks = (cfg.max_frames + 255) / 256 + 1;
     c->enc_cap = cfg.max_batch_bytes + 16ull * cfg.max_frames;
     c->enc_tile_entries = c->enc_cap / ENC_WIN + 2;
@@ -187,7 +201,7 @@ int wsc_destroy(wsc_ctx* c) {
     void* ptrs[] = {c->dbg, c->counts, c->lb_state, c->u8info, c->lb_agg, c->lb_incl, c->spans, c->tile, c->d_wire, c->d_arena,
                     c->d_seg_off, c->d_state_in, c->d_state_out, c->d_seg_out, c->d_frames,
                     c->d_frame_dst, c->d_summary, c->enc_lb_state, c->enc_lb_agg, c->enc_lb_incl, c->enc_tile,
-                    c->d_enc_msgs, c->d_enc_src, c->d_enc_out, c->d_enc_off};
+                    c->d_enc_msgs, c->d_enc_src, c->d_enc_out, c->d_enc_off, c->u8items, c->u8maps, c->u8seg};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -240,7 +254,7 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     wa.max_frame_len = c->cfg.max_frame_len;
     wa.counts = c->counts;
     wa.lb_ticket = c->lb_state;
-    wa.lb_flag = c->lb_state + 2;
+    wa.lb_flag = c->lb_state + 3;
     wa.u8info = c->u8info;
     wa.lb_agg = c->lb_agg;
     wa.lb_incl = c->lb_incl;
@@ -255,6 +269,11 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     wa.state_out = b->state_out;
     wa.seg_out = b->seg_out;
     wa.summary = b->summary;
+    wa.u8items = c->u8items;
+    wa.u8items_cap = c->u8items_cap;
+    wa.u8count = c->lb_state + 2;
+    wa.u8seg = c->u8seg;
+    wa.u8_inline_max = c->u8_inline_max;
 
     const dim3 wblk(256), wgrid((n + 255) / 256);
     auto rec = [&](int i) {
@@ -265,6 +284,22 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     else hipLaunchKernelGGL((k_walk_fused<false>), wgrid, wblk, 0, st, wa);
     HIP_TRY(hipGetLastError());
     rec(1);
+    // deferred UTF-8 (large text): verdicts applied before the unmask; exits at once without text
+    U8Args ua{};
+    ua.wire = b->wire;
+    ua.n_bytes = b->n_bytes;
+    ua.seg_off = b->seg_off;
+    ua.items = c->u8items;
+    ua.count = c->lb_state + 2;
+    ua.maps = c->u8maps;
+    ua.seg = c->u8seg;
+    ua.frames = b->frames;
+    ua.spans = c->spans;
+    ua.seg_out = b->seg_out;
+    ua.state_out = b->state_out;
+    ua.summary = b->summary;
+    hipLaunchKernelGGL(k_u8_check, dim3((uint32_t)c->n_cu * 8), dim3(256), 0, st, ua);   // 32 waves per CU
+    HIP_TRY(hipGetLastError());
     rec(2);
     rec(3);
 
@@ -291,7 +326,7 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     UK kern = table[compact ? 1 : 0][pi][c->cfg.unmask_nt & 3];
     hipLaunchKernelGGL(kern, ugrid, ublk, 0, st, udst, (const uint8_t*)b->wire, b->n_bytes, udst_bytes,
                        (const Span*)c->spans, (const uint32_t*)c->tile, (const wsc_summary*)b->summary,
-                       c->lb_state, (n + 255) / 256);
+                       c->lb_state, (n + 255) / 256 + 1);   // re-arms ticket, timeout, item count, flags
     HIP_TRY(hipGetLastError());
     rec(4);
 

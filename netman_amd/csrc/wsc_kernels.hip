@@ -307,6 +307,8 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
     // state after the continueBuffer (carried to the next batch).
     uint32_t u8fail = 0xFFFFFFFFu;
     uint32_t u8dfa = cont ? st.cont_utf8 : 0u;
+    bool u8_pending = false;                      // a text chain has a deferred (chip-wide) part
+    uint32_t u8_head = 0xFFFFFFFFu, u8_last = 0xFFFFFFFFu, u8_n = 0;
     if constexpr (EMIT) {
         u8fail = a.u8info[2 * s];
         u8dfa = a.u8info[2 * s + 1];
@@ -457,13 +459,48 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
         if (fr.flags & (WSC_FF_U8_PART | WSC_FF_U8_SELF | WSC_FF_U8_CHAIN | WSC_FF_U8_REASON)) {
             sflags |= SEGF_UTF8;
             if constexpr (!EMIT) {
-                const uint64_t ps = pos + fr.hdr_len;
-                bool ok = true;
-                if (fr.flags & WSC_FF_U8_PART) u8dfa = u8_run_masked(u8dfa, w, ps, plen, fr.mask);
-                else if (fr.flags & WSC_FF_U8_CHAIN) ok = u8_run_masked(u8dfa, w, ps, plen, fr.mask) == 0;
-                else if (fr.flags & WSC_FF_U8_SELF) ok = u8_run_masked(0, w, ps, plen, fr.mask) == 0;
-                else ok = u8_run_masked(0, w, ps + 2, plen - 2, rotr32(fr.mask, 16)) == 0;
-                if (!ok) u8fail = nf;
+                const bool part = (fr.flags & WSC_FF_U8_PART) != 0, chain = (fr.flags & WSC_FF_U8_CHAIN) != 0;
+                uint64_t src = pos + fr.hdr_len, n = plen;
+                uint32_t mk = fr.mask;
+                if (fr.flags & WSC_FF_U8_REASON) { src += 2; n -= 2; mk = rotr32(mk, 16); }   // payload[2:]
+                if (n > a.u8_inline_max || ((part || chain) && u8_pending)) {
+                    // large text (or a chain already deferred): validated chip-wide by k_u8_check,
+                    // which also applies the verdict; the walk goes on as if it were valid
+                    const uint8_t kind = part ? U8K_PART : (chain ? U8K_CHAIN : U8K_SELF);
+                    const uint8_t s_in = (part || chain) ? (u8_pending ? 0xFF : (uint8_t)u8dfa) : 0;
+                    const uint32_t pieces = n ? (uint32_t)((n + U8_PIECE - 1) / U8_PIECE) : 1u;
+                    const uint32_t b0 = __hip_atomic_fetch_add(a.u8count, pieces, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    for (uint32_t p = 0; p < pieces; ++p) {   // capacity covers every frame + bytes / U8_PIECE
+                        const uint32_t idx = b0 + p;
+                        U8Item it;
+                        it.src = src + (uint64_t)p * U8_PIECE;
+                        const uint64_t rem = n - (uint64_t)p * U8_PIECE;
+                        it.len = (uint32_t)(rem < U8_PIECE ? rem : U8_PIECE);
+                        it.mask = mk;
+                        it.seg = s;
+                        it.ordinal = nf;
+                        it.next = 0xFFFFFFFFu;
+                        it.kind = kind;
+                        it.s_in = s_in;
+                        it.first = p == 0;
+                        it.last = p + 1 == pieces;
+                        if (idx < a.u8items_cap) {
+                            a.u8items[idx] = it;
+                            if (u8_last != 0xFFFFFFFFu) a.u8items[u8_last].next = idx;
+                            else u8_head = idx;
+                            u8_last = idx;
+                            u8_n += 1;
+                        }
+                    }
+                    if (part) u8_pending = true;
+                    if (chain) u8_pending = false;   // the message completes here
+                } else {
+                    bool ok = true;
+                    if (part) u8dfa = u8_run_masked(u8dfa, w, src, n, mk);
+                    else if (chain) ok = u8_run_masked(u8dfa, w, src, n, mk) == 0;
+                    else ok = u8_run_masked(0, w, src, n, mk) == 0;
+                    if (!ok) u8fail = nf;
+                }
             }
             if (nf == u8fail) {   // -> CloseCode(1007) (epoll.go:126-127); nothing after it is read
                 fr.kind = WSC_FK_ERROR;
@@ -527,6 +564,15 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
     if constexpr (!EMIT) {
         a.u8info[2 * s] = u8fail;
         a.u8info[2 * s + 1] = u8dfa;
+        if (u8_n) {
+            U8Seg g{};
+            g.head = u8_head;
+            g.n = u8_n;
+            g.done = 0;
+            g.pending_end = u8_pending ? 1u : 0u;
+            a.u8seg[s] = g;
+            c.flags |= SEGF_U8DEFER;
+        }
     }
     WalkEnd we;
     we.pos = pos; we.cont = cont; we.msg = msg; we.mode = mode; we.status = status;
@@ -679,6 +725,11 @@ __global__ __launch_bounds__(256) void k_walk_fused(WalkArgs a) {
     __syncthreads();
     if (a.dbg && threadIdx.x == 0) t2 = __builtin_amdgcn_s_memrealtime();
     const SegCount base = sc_add(sh_prefix, sc_add(wpre, excl));
+    if (s < a.n_segs && (own.flags & SEGF_U8DEFER)) {
+        a.u8seg[s].sbase = base.spans0 + base.spans1;
+        a.u8seg[s].nspans = own.spans0 + own.spans1;
+        a.u8seg[s].fbase = base.frames;
+    }
     if (s < a.n_segs) {
         if (own.frames <= KREC)   // replay from LDS: no second dependent walk, no loads at all
             emit_replay<COMPACT>(a, s, a.seg_off[s], a.seg_off[s + 1], base, own, sh_rec + threadIdx.x, msg0, wend);
@@ -705,6 +756,165 @@ __global__ __launch_bounds__(256) void k_walk_fused(WalkArgs a) {
         if (__hip_atomic_load(a.lb_err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) sm.overflow |= 2u;
         sm.pad = 0;
         *a.summary = sm;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Chip-wide UTF-8 (utf8.Valid, websocket_frame.go:71-73, websocket.go:170-172) for the text the
+// walk deferred.  A UTF-8 check is a 9-state DFA; what a run of bytes does to it is a map from
+// start state to end state (9 x 4 bits).  Each lane computes the map of its 16 bytes, a wave
+// composes 64 lanes' maps in order (shuffle tree), items are composed step by step.  Per item the
+// map is published (agent-scope store, drained, then an agent-scope counter); the wave that
+// completes a segment's last item composes the segment's items in frame order with the states the
+// walk recorded and applies the verdict: the first failing frame becomes WSC_FK_ERROR / 1007, the
+// segment stops there, and the spans of later frames get key 0 so the unmask leaves them as the
+// reference would (never read).  Runs between the walk and the unmask; exits at once when the
+// walk deferred nothing.
+// ---------------------------------------------------------------------------------------------
+// A map is 8 bytes: byte s = the state after the bytes when entering in state s (0..7), 0xFF =
+// reject; the reject state itself is absorbing and not stored.  With this encoding a map is a
+// v_perm_b32 table: applying map b after map a is two v_perm_b32 (a's bytes select from b; 0xFF
+// selects 0xFF), and one input byte is one 8-byte table row T[byte] from LDS.
+__device__ __forceinline__ uint64_t u8m_id() { return 0x0706050403020100ull; }
+__device__ __forceinline__ uint64_t u8m_ascii() { return 0xFFFFFFFFFFFFFF00ull; }   // 0 -> 0, mid-character -> reject
+__device__ __forceinline__ uint64_t u8m_then(uint64_t a, uint64_t b) {   // a, then b
+    const uint32_t bl = (uint32_t)b, bh = (uint32_t)(b >> 32);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_perm(bh, bl, (uint32_t)a);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_perm(bh, bl, (uint32_t)(a >> 32));
+    return (uint64_t)hi << 32 | lo;
+}
+__device__ __forceinline__ uint32_t u8m_get(uint64_t m, uint32_t st) {   // st: 0..7, or >= 8 = reject
+    return st > 7 ? 0xFFu : (uint32_t)(m >> (8 * st)) & 0xFFu;
+}
+
+__global__ __launch_bounds__(256) void k_u8_check(U8Args a) {
+    const uint32_t n_items = *a.count;
+    if (blockIdx.x * 4 >= n_items) return;   // nothing deferred (the common, binary case)
+    __shared__ uint64_t tab[256];            // T[byte]: the map of that single byte
+    {
+        const uint32_t byte = threadIdx.x;
+        uint64_t t = 0;
+        for (uint32_t st = 0; st < 8; ++st) {
+            const uint32_t ns = u8_step(st, byte);
+            t |= (uint64_t)(ns == 8 ? 0xFFu : ns) << (8 * st);
+        }
+        tab[byte] = t;
+    }
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+    const uint32_t nw = gridDim.x * 4;
+    for (uint32_t it = gw; it < n_items; it += nw) {
+        const U8Item item = a.items[it];
+        uint64_t acc = u8m_id();
+        for (uint32_t b0 = 0; b0 < item.len; b0 += 4096) {
+            uint64_t pm[4];
+            bool plain = true;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t off = b0 + k * 1024 + lane * 16;
+                const uint32_t nk = off < item.len ? (item.len - off >= 16 ? 16u : item.len - off) : 0u;
+                uint32_t d[4] = {0, 0, 0, 0};
+                if (nk) {
+                    const uint4 v = load16_unaligned(a.wire, (int64_t)(item.src + off), a.n_bytes);
+                    d[0] = v.x ^ item.mask; d[1] = v.y ^ item.mask; d[2] = v.z ^ item.mask; d[3] = v.w ^ item.mask;
+                }
+                uint32_t hib = 0;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const uint32_t lim = nk > 4u * j ? (nk - 4u * j >= 4 ? 4u : nk - 4u * j) : 0u;
+                    const uint32_t keep = lim >= 4 ? 0xFFFFFFFFu : ((1u << (8 * lim)) - 1u);
+                    hib |= d[j] & keep & 0x80808080u;
+                }
+                if (nk == 0) {
+                    pm[k] = u8m_id();
+                } else if (hib == 0) {
+                    pm[k] = u8m_ascii();
+                } else {
+                    uint32_t lo = 0x03020100u, hi = 0x07060504u;
+#pragma unroll
+                    for (uint32_t i = 0; i < 16; ++i) {
+                        if (i < nk) {
+                            const uint64_t t = tab[(d[i >> 2] >> (8 * (i & 3))) & 0xFFu];
+                            const uint32_t tl = (uint32_t)t, th = (uint32_t)(t >> 32);
+                            lo = (uint32_t)__builtin_amdgcn_perm(th, tl, lo);
+                            hi = (uint32_t)__builtin_amdgcn_perm(th, tl, hi);
+                        }
+                    }
+                    pm[k] = (uint64_t)hi << 32 | lo;
+                    plain = false;
+                }
+            }
+            uint64_t stepm;
+            if (__ballot(!plain) == 0) {          // ASCII (or empty) everywhere: one constant map
+                stepm = __ballot(pm[0] == u8m_ascii()) ? u8m_ascii() : u8m_id();
+            } else {
+                stepm = u8m_id();
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {     // lanes in order, then pieces in order
+                    uint64_t m = pm[k];
+#pragma unroll
+                    for (int dd = 1; dd < 64; dd <<= 1) {
+                        const uint32_t lo = __shfl_down((uint32_t)m, dd), hi = __shfl_down((uint32_t)(m >> 32), dd);
+                        if ((lane & (2 * dd - 1)) == 0) m = u8m_then(m, (uint64_t)hi << 32 | lo);
+                    }
+                    // readlane returns int: widen through uint32_t (no sign extension into the high word)
+                    const uint32_t m0lo = (uint32_t)__builtin_amdgcn_readlane((uint32_t)m, 0);
+                    const uint32_t m0hi = (uint32_t)__builtin_amdgcn_readlane((uint32_t)(m >> 32), 0);
+                    stepm = u8m_then(stepm, (uint64_t)m0hi << 32 | m0lo);
+                }
+            }
+            acc = u8m_then(acc, stepm);
+        }
+        if (lane != 0) continue;
+        __hip_atomic_store(a.maps + it, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t done = __hip_atomic_fetch_add(&a.seg[item.seg].done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+        const U8Seg g = a.seg[item.seg];
+        if (done != g.n) continue;
+        // the segment's last item: compose its items in frame order with the walk's states
+        uint32_t cur = 0, start = 0, fail = 0xFFFFFFFFu;   // states 0..7, 0xFF = reject
+        uint64_t fm = u8m_id();
+        uint32_t j = g.head;
+        for (uint32_t c = 0; c < g.n && j != 0xFFFFFFFFu; ++c) {
+            const U8Item x = a.items[j];
+            const uint64_t m = __hip_atomic_fetch_add(a.maps + j, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (x.first) {
+                start = x.kind == U8K_SELF ? 0u : (x.s_in != 0xFF ? (x.s_in > 7 ? 0xFFu : (uint32_t)x.s_in) : cur);
+                fm = u8m_id();
+            }
+            fm = u8m_then(fm, m);
+            if (x.last) {
+                const uint32_t end = u8m_get(fm, start);
+                if (x.kind == U8K_PART) {
+                    cur = end;
+                } else {
+                    if (end != 0) { fail = x.ordinal; break; }
+                    if (x.kind == U8K_CHAIN) cur = 0;
+                }
+            }
+            j = x.next;
+        }
+        const uint32_t s = item.seg;
+        if (fail == 0xFFFFFFFFu) {
+            if (g.pending_end && a.state_out[s].cont_len) a.state_out[s].cont_utf8 = (uint8_t)(cur > 7 ? 8u : cur);
+            continue;
+        }
+        // frame `fail` fails: CloseCode(1007) there (epoll.go:126-127), nothing after it is read
+        wsc_frame* f = a.frames + g.fbase + fail;
+        f->kind = WSC_FK_ERROR;
+        f->err = WSC_ERR_MUST_UTF8;
+        const uint64_t fend = f->hdr_off + f->hdr_len + f->payload_len;
+        wsc_seg_result r = a.seg_out[s];
+        r.consumed = fend - a.seg_off[s];
+        r.frame_count = fail + 1;
+        r.status = WSC_SEG_ERROR;
+        r.close_code = 1007;
+        r.err = WSC_ERR_MUST_UTF8;
+        a.seg_out[s] = r;
+        a.state_out[s].status = WSC_SEG_ERROR;
+        for (uint32_t k = 0; k < g.nspans; ++k)   // later frames stay masked (the reference never reads them)
+            if (a.spans[g.sbase + k].src >= fend) a.spans[g.sbase + k].key = 0;
     }
 }
 

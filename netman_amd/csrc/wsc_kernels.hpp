@@ -30,7 +30,30 @@ struct SegCountAdd {
     }
 };
 
-enum : uint32_t { SEGF_UTF8 = 1u };
+enum : uint32_t { SEGF_UTF8 = 1u, SEGF_U8DEFER = 2u };
+
+// ---- chip-wide UTF-8 (k_u8_check) ------------------------------------------------------------
+// The walk validates text payloads of at most u8_inline_max bytes itself (serial DFA per lane);
+// larger ones -- and every later frame of a text chain that has a deferred part -- become items of
+// at most U8_PIECE bytes, validated by k_u8_check across the whole chip before the unmask runs.
+constexpr uint32_t U8_PIECE = 65536;
+enum : uint8_t { U8K_SELF = 0, U8K_PART = 1, U8K_CHAIN = 2 };   // close reasons are SELF items
+struct U8Item {
+    uint64_t src;       // wire offset of the first (masked) byte
+    uint32_t len;
+    uint32_t mask;      // mask word, phase 0 at src
+    uint32_t seg;
+    uint32_t ordinal;   // frame ordinal within the segment
+    uint32_t next;      // next item of the same segment (0xFFFFFFFF = last)
+    uint8_t kind;       // U8K_*
+    uint8_t s_in;       // DFA state entering a chain frame, 0xFF = the previous chain item's result
+    uint8_t first, last;   // first / last piece of its frame
+};
+static_assert(sizeof(U8Item) == 32, "U8Item layout");
+struct U8Seg {          // per segment with deferred items (written by the walk)
+    uint32_t head, n, done, pending_end;   // pending_end: a text chain with a deferred part is still open
+    uint32_t sbase, nspans, fbase, pad;    // the segment's span and frame ranges (emit pass)
+};
 
 // One contiguous run of masked payload bytes to XOR: source in the wire, destination either the
 // same bytes (in place) or the arena (COMPACT).  `key` is the mask word rotated so that it XORs
@@ -68,6 +91,26 @@ struct WalkArgs {
     uint32_t* lb_err;            // bounded-spin timeout
     uint64_t* dbg;               // optional per-block timestamps (WSC_DEBUG_STAMPS=1)
     uint32_t* u8info;            // per segment: {first utf8-failing frame ordinal, DFA state}
+    U8Item* u8items;             // deferred UTF-8 items
+    uint32_t u8items_cap;
+    uint32_t* u8count;           // item counter (re-armed by k_unmask)
+    U8Seg* u8seg;
+    uint32_t u8_inline_max;      // text payloads up to this many bytes are validated in the walk
+};
+
+struct U8Args {
+    const uint8_t* wire;
+    uint64_t n_bytes;
+    const uint64_t* seg_off;
+    const U8Item* items;
+    const uint32_t* count;
+    uint64_t* maps;              // per item: DFA transition map (9 x 4 bits)
+    U8Seg* seg;
+    wsc_frame* frames;
+    Span* spans;
+    wsc_seg_result* seg_out;
+    wsc_conn_state* state_out;
+    wsc_summary* summary;
 };
 
 

@@ -111,6 +111,60 @@ def uniform_batch(n_frames, size, frames_per_seg, seed, opcode=OP_BIN):
                 n_frames=n_frames, payload_bytes=int(plen.sum()))
 
 
+def utf8_units(rng, n_units):
+    """n_units random 4-byte units, each valid UTF-8 on its own: 4 ASCII, 2 x 2-byte (Greek),
+    3-byte (CJK) + ASCII, or one 4-byte character (emoji) -- uint8[4 * n_units]."""
+    kind = rng.integers(0, 4, n_units)
+    u = rng.integers(0x20, 0x7F, (n_units, 4)).astype(np.uint8)
+    g = rng.integers(0x3B1, 0x3C9, (n_units, 2))                      # 2-byte: U+03B1..U+03C9
+    m2 = kind == 1
+    u[m2, 0] = (0xC0 | (g[m2, 0] >> 6)).astype(np.uint8)
+    u[m2, 1] = (0x80 | (g[m2, 0] & 0x3F)).astype(np.uint8)
+    u[m2, 2] = (0xC0 | (g[m2, 1] >> 6)).astype(np.uint8)
+    u[m2, 3] = (0x80 | (g[m2, 1] & 0x3F)).astype(np.uint8)
+    c = rng.integers(0x4E00, 0x9FFF, n_units)                        # 3-byte: CJK (+ 1 ASCII)
+    m3 = kind == 2
+    u[m3, 0] = (0xE0 | (c[m3] >> 12)).astype(np.uint8)
+    u[m3, 1] = (0x80 | ((c[m3] >> 6) & 0x3F)).astype(np.uint8)
+    u[m3, 2] = (0x80 | (c[m3] & 0x3F)).astype(np.uint8)
+    e = rng.integers(0x1F300, 0x1F5FF, n_units)                      # 4-byte: emoji
+    m4 = kind == 3
+    u[m4, 0] = (0xF0 | (e[m4] >> 18)).astype(np.uint8)
+    u[m4, 1] = (0x80 | ((e[m4] >> 12) & 0x3F)).astype(np.uint8)
+    u[m4, 2] = (0x80 | ((e[m4] >> 6) & 0x3F)).astype(np.uint8)
+    u[m4, 3] = (0x80 | (e[m4] & 0x3F)).astype(np.uint8)
+    return u.reshape(-1)
+
+
+def text_batch(n_frames, size, frames_per_seg, seed, ascii_only=False):
+    """n_frames masked TEXT frames whose unmasked payload is valid UTF-8 (`size` bytes each:
+    random 1-4 byte characters, or printable ASCII), grouped frames_per_seg per segment."""
+    rng = np.random.default_rng(seed)
+    b0 = np.full(n_frames, 0x80 | OP_TEXT, dtype=np.uint8)
+    plen = np.full(n_frames, size, dtype=np.uint64)
+    mask = rng.integers(0, 2**32, n_frames, dtype=np.uint64).astype(np.uint32)
+    nseg = (n_frames + frames_per_seg - 1) // frames_per_seg
+    segf = np.full(nseg, frames_per_seg, dtype=np.int64)
+    segf[-1] = n_frames - frames_per_seg * (nseg - 1)
+    wire, seg_off, poff = build_frames(b0, plen, mask, rng, seg_frames=segf, fill=False)
+    body_len = size - size % 4
+    pool_units = body_len // 4 + 1024
+    pool = (rng.integers(0x20, 0x7F, 4 * pool_units).astype(np.uint8) if ascii_only
+            else utf8_units(rng, pool_units))
+    starts = rng.integers(0, 1024, n_frames) * 4            # unit-aligned: every slice is valid
+    pad = np.full(size % 4, 0x61, np.uint8)                  # the tail is ASCII
+    # masked payload = body ^ mask bytes (phase restarts at each payload start)
+    mb = np.stack([(mask >> np.uint32(8 * k)) & 0xFF for k in range(4)], axis=1).astype(np.uint8)
+    for i in range(n_frames):
+        body = pool[starts[i]: starts[i] + body_len]
+        if len(pad):
+            body = np.concatenate([body, pad])
+        p = int(poff[i])
+        wire[p:p + size] = body ^ np.resize(mb[i], size)
+    return dict(wire=wire, seg_off=seg_off, payload_off=poff, plen=plen, mask=mask,
+                n_frames=n_frames, payload_bytes=int(plen.sum()))
+
+
 def mixed_batch(n_frames=262144, seed=SEED_BASE + 2, frames_per_seg=16):
     """configs[2]: sizes {125, 65536, 1048576} with p proportional to 1/size, shuffled."""
     rng = np.random.default_rng(seed)

@@ -1,0 +1,141 @@
+"""Chip-wide UTF-8 validation (k_u8_check) for text the walk defers: bit-exact against the oracle.
+
+By default text payloads above 256 B are deferred; WSC_U8_INLINE_MAX=0 (read at context creation)
+sends EVERY text check through k_u8_check, so the fuzz corpus (fragmented text chains, multi-byte
+characters split across fragments, PINGs inside text messages (Q6), close reasons, invalid
+sequences) exercises the deferred path end to end, including chains that span batches.
+Full-size: 64 KiB TEXT frames of 1-4 byte characters, valid and with injected errors."""
+import os
+
+import numpy as np
+import pytest
+
+import oracle_ref as O
+from fuzz_streams import random_stream, random_splits
+from gpu_helpers import pack_streams, compare_segment, events_of_session
+from netman_amd import codec as K
+from netman_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _with_inline_max(v, make):
+    old = os.environ.get("WSC_U8_INLINE_MAX")
+    os.environ["WSC_U8_INLINE_MAX"] = str(v)
+    try:
+        return make()
+    finally:
+        if old is None:
+            del os.environ["WSC_U8_INLINE_MAX"]
+        else:
+            os.environ["WSC_U8_INLINE_MAX"] = old
+
+
+@pytest.fixture(scope="module")
+def codec_all_deferred(codec_lib):
+    c = _with_inline_max(0, lambda: K.Codec(0, max_batch_bytes=64 << 20, max_segs=1 << 14, max_frames=1 << 18))
+    yield c
+    c.close()
+
+
+def _check(codec, streams, compact=False):
+    wire, off = pack_streams(streams)
+    res = codec.decode_host(wire, off, compact=compact)
+    assert int(res.summary["overflow"]) == 0
+    for i, s in enumerate(streams):
+        compare_segment(i, s, int(off[i]), res, O.run(s), wire_after=wire, compact=compact)
+    return res
+
+
+@pytest.mark.parametrize("compact", [False, True])
+def test_text_heavy_fuzz_all_deferred(codec_all_deferred, compact):
+    streams = [random_stream(7000 + i, n_units=30, text_p=0.9, err_p=0.03) for i in range(300)]
+    _check(codec_all_deferred, streams, compact=compact)
+
+
+def test_general_fuzz_all_deferred(codec_all_deferred):
+    streams = [random_stream(8000 + i, n_units=int(5 + i % 40)) for i in range(400)]
+    _check(codec_all_deferred, streams)
+
+
+def test_golden_streams_all_deferred(codec_all_deferred):
+    import golden_io
+    streams = [b for _, b, _ in golden_io.aiohttp_cases()] + [b for _, b, _ in golden_io.kat_cases()]
+    _check(codec_all_deferred, streams)
+
+
+@pytest.mark.parametrize("inline_max", [0, 40])
+def test_session_chains_across_batches_deferred(codec_lib, inline_max):
+    """text chains whose parts arrive in different decodes: the deferred DFA state is carried"""
+    rng = np.random.default_rng(11)
+    sess = _with_inline_max(inline_max, lambda: K.Session(0, max_batch_bytes=16 << 20, max_segs=1024,
+                                                          max_frames=1 << 16))
+    streams = [random_stream(9500 + i, n_units=25, text_p=0.9, err_p=0.02) for i in range(150)]
+    conns = [sess.open() for _ in streams]
+    splits = [random_splits(rng, len(s), int(rng.integers(1, 6))) for s in streams]
+    got = {c: [] for c in conns}
+    prev = [0] * len(streams)
+    for r in range(max(len(sp) for sp in splits)):
+        for i, (c, s, sp) in enumerate(zip(conns, streams, splits)):
+            if r < len(sp):
+                sess.feed(c, s[prev[i]:sp[r]])
+                prev[i] = sp[r]
+        sess.decode()
+        for c in conns:
+            got[c].extend(events_of_session(sess, c))
+    for i, (c, s) in enumerate(zip(conns, streams)):
+        ref = [e.key() for e in O.run(s).events]
+        assert got[c] == ref, f"stream {i}: {got[c][:4]} vs {ref[:4]}"
+    sess.close()
+
+
+def _unmask(cfg, i):
+    p, L, m = int(cfg["payload_off"][i]), int(cfg["plen"][i]), int(cfg["mask"][i])
+    mb = np.array([(m >> (8 * k)) & 0xFF for k in range(4)], np.uint8)
+    return p, L, mb
+
+
+def test_text_64k_frames_valid_and_invalid(codec_lib):
+    """1,024 connections x 4 x 64 KiB TEXT frames (chip-wide path by default); a 0xFF byte is
+    injected into ~6 % of the frames: each connection must stop at its first bad frame with 1007,
+    leave later frames masked, and match the oracle record for record, byte for byte."""
+    cfg = synth.text_batch(4096, 65536, 4, seed=synth.SEED_BASE + 31)
+    rng = np.random.default_rng(5)
+    bad = set(int(x) for x in rng.choice(4096, 256, replace=False))
+    for i in bad:   # write 0xFF (never valid UTF-8) at a random payload position, masked
+        p, L, mb = _unmask(cfg, i)
+        q = int(rng.integers(0, L))
+        cfg["wire"][p + q] = 0xFF ^ mb[q & 3]
+    c = K.Codec(0, max_batch_bytes=len(cfg["wire"]) + 4096, max_segs=2048, max_frames=8192)
+    wire = cfg["wire"].copy()
+    res = c.decode_host(wire, cfg["seg_off"])
+    assert int(res.summary["overflow"]) == 0
+    n_seg = len(cfg["seg_off"]) - 1
+    for s in range(n_seg):
+        a, b = int(cfg["seg_off"][s]), int(cfg["seg_off"][s + 1])
+        compare_segment(s, bytes(cfg["wire"][a:b]), a, res, O.run(bytes(cfg["wire"][a:b])), wire_after=wire)
+    n_err = int((res.seg["status"] == K.SEG_ERROR).sum())
+    assert n_err == len({i // 4 for i in bad}) and n_err > 0
+    assert int(res.summary["n_frames"]) >= int(res.seg["frame_count"].sum())
+    c.close()
+
+
+def test_text_large_frames_cross_piece_characters(codec_lib):
+    """frames larger than one 64 KiB item with multi-byte characters across the item boundary,
+    plus a TEXT chain of big fragments where a 4-byte character straddles two fragments"""
+    e = "😀".encode()                                        # 4 bytes
+    body = ("ab" + "é" * 40000 + "x").encode()               # 80003 bytes, 2-byte chars across 65536
+    body2 = b"a" * 65535 + e + b"z" * 100                    # emoji straddles the 64 KiB piece edge
+    frag = e * 30000                                         # 120000 B, cut inside a character
+    s1 = synth.frame(1, body) + synth.frame(1, body2)
+    s2 = synth.frame(1, frag[:70001], fin=False) + synth.frame(0, frag[70001:], fin=True)
+    s3 = synth.frame(1, frag[:70001], fin=False) + synth.frame(0, frag[70001:-1], fin=True)   # truncated char
+    s4 = synth.frame(8, (1000).to_bytes(2, "big") + ("ü" * 61).encode())   # close reason, 124 B
+    c = _with_inline_max(0, lambda: K.Codec(0, max_batch_bytes=8 << 20, max_segs=64, max_frames=4096))
+    streams = [s1, s2, s3, s4]
+    wire, off = pack_streams(streams)
+    res = c.decode_host(wire, off)
+    for i, s in enumerate(streams):
+        compare_segment(i, s, int(off[i]), res, O.run(s), wire_after=wire)
+    assert [int(x) for x in res.seg["status"]] == [K.SEG_OPEN, K.SEG_OPEN, K.SEG_ERROR, K.SEG_CLOSED]
+    c.close()
