@@ -807,7 +807,21 @@ __global__ __launch_bounds__(256) void k_u8_check(U8Args a) {
     for (uint32_t it = gw; it < n_items; it += nw) {
         const U8Item item = a.items[it];
         uint64_t acc = u8m_id();
+        // the next 4 KiB step's loads are issued before the current step is folded
+        uint4 nxt[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t off = k * 1024 + lane * 16;
+            nxt[k] = off < item.len ? load16_unaligned(a.wire, (int64_t)(item.src + off), a.n_bytes) : make_uint4(0, 0, 0, 0);
+        }
         for (uint32_t b0 = 0; b0 < item.len; b0 += 4096) {
+            uint4 cur4[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                cur4[k] = nxt[k];
+                const uint32_t off = b0 + 4096 + k * 1024 + lane * 16;
+                nxt[k] = off < item.len ? load16_unaligned(a.wire, (int64_t)(item.src + off), a.n_bytes) : make_uint4(0, 0, 0, 0);
+            }
             uint64_t pm[4];
             bool plain = true;
 #pragma unroll
@@ -816,7 +830,7 @@ __global__ __launch_bounds__(256) void k_u8_check(U8Args a) {
                 const uint32_t nk = off < item.len ? (item.len - off >= 16 ? 16u : item.len - off) : 0u;
                 uint32_t d[4] = {0, 0, 0, 0};
                 if (nk) {
-                    const uint4 v = load16_unaligned(a.wire, (int64_t)(item.src + off), a.n_bytes);
+                    const uint4 v = cur4[k];
                     d[0] = v.x ^ item.mask; d[1] = v.y ^ item.mask; d[2] = v.z ^ item.mask; d[3] = v.w ^ item.mask;
                 }
                 uint32_t hib = 0;
@@ -852,6 +866,7 @@ __global__ __launch_bounds__(256) void k_u8_check(U8Args a) {
                 stepm = u8m_id();
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {     // lanes in order, then pieces in order
+                    if (b0 + k * 1024 >= item.len) break;   // the rest of the step is past the item
                     uint64_t m = pm[k];
 #pragma unroll
                     for (int dd = 1; dd < 64; dd <<= 1) {
