@@ -162,6 +162,117 @@ __global__ __launch_bounds__(256) void k_encode_scan(EncArgs a) {
     }
 }
 
+// General output window, lane-parallel (the decoder's unmask_window_lanes, for frames): the wave
+// loads the frames overlapping the window into lanes (frame m + lane), each lane binary-searches
+// them (ds_bpermute) for the frame holding its 16-byte piece and assembles the piece from that
+// frame and the next -- header bytes from registers, payload bytes by unaligned gathers issued
+// together; pieces meeting 3+ frames (frames shorter than 16 B) take a uniform tail loop.  Returns
+// false (nothing written) when more than 64 frames overlap the window.
+template <int NT>
+__device__ __forceinline__ bool encode_window_lanes(const EncCopyArgs& a, uint32_t m, uint64_t wbase, uint64_t limit,
+                                                    uint32_t lane) {
+    constexpr uint32_t P = ENC_WIN / 1024;
+    constexpr int64_t WB = ENC_WIN;
+    auto clip = [](int64_t x) -> int32_t { return (int32_t)(x < -(1ll << 30) ? -(1ll << 30) : (x > WB + 64 ? WB + 64 : x)); };
+    const uint32_t fj = m + lane;
+    int32_t ro = (int32_t)WB + 64, rp = ro, re = ro;   // window-relative header start, payload start, end
+    uint32_t h[4] = {0, 0, 0, 0};
+    int64_t so = 0;                                    // source offset of output byte x: so + x
+    if (fj < a.n_msgs) {
+        const wsc_out_msg mj = a.msgs[fj];
+        const uint64_t o = a.out_off[fj];
+        const uint64_t p = o + enc_hlen(mj.len);
+        ro = clip((int64_t)o - (int64_t)wbase);
+        rp = clip((int64_t)p - (int64_t)wbase);
+        re = clip((int64_t)(p + mj.len) - (int64_t)wbase);
+        enc_header(mj.first_byte, mj.len, h);
+        so = (int64_t)mj.src_off - (int64_t)p;
+    }
+    const uint32_t nl = (uint32_t)__builtin_popcountll(__ballot(ro < (int32_t)WB));
+    if (nl == 64 && __shfl(re, 63) < (int32_t)WB && m + 64 < a.n_msgs) return false;
+    const uint32_t so_lo = (uint32_t)so, so_hi = (uint32_t)((uint64_t)so >> 32);
+
+    int32_t ta[P];
+#pragma unroll
+    for (uint32_t k = 0; k < P; ++k) {
+        const int32_t pr = (int32_t)(k * 1024 + lane * 16);
+        int32_t lo = -1;
+#pragma unroll
+        for (int st = 32; st >= 1; st >>= 1) {
+            const int32_t c = lo + st;
+            const int32_t dv = __shfl(ro, c & 63);
+            if (c < (int32_t)nl && dv <= pr) lo = c;
+        }
+        ta[k] = lo < 0 ? 0 : lo;
+    }
+    // one frame's contribution to a piece: header bytes from registers, payload by a gather
+    auto part = [&](int32_t t, int32_t pr, uint4& acc, bool& ends_inside) {
+        const int32_t fo = __shfl(ro, t & 63), fp = __shfl(rp, t & 63), fe = __shfl(re, t & 63);
+        const uint32_t hh[4] = {__shfl(h[0], t & 63), __shfl(h[1], t & 63), __shfl(h[2], t & 63), 0u};
+        const uint32_t sl = __shfl(so_lo, t & 63), sh = __shfl(so_hi, t & 63);
+        ends_inside = false;
+        if (t >= (int32_t)nl) return;
+        uint32_t msk[4];
+        int32_t lo = fo > pr ? fo : pr, hi = fp < pr + 16 ? fp : pr + 16;
+        if (lo < hi) {
+            piece_mask((uint32_t)(lo - pr), (uint32_t)(hi - pr), msk);
+            const uint4 t4 = and4(enc_place(hh, fo - pr), msk);
+            acc.x |= t4.x; acc.y |= t4.y; acc.z |= t4.z; acc.w |= t4.w;
+        }
+        lo = fp > pr ? fp : pr;
+        hi = fe < pr + 16 ? fe : pr + 16;
+        if (lo < hi) {
+            piece_mask((uint32_t)(lo - pr), (uint32_t)(hi - pr), msk);
+            const int64_t sof = (int64_t)((uint64_t)sh << 32 | sl) + (int64_t)wbase + pr;
+            const uint4 t4 = and4(load16_unaligned(a.src, sof, a.src_bytes), msk);
+            acc.x |= t4.x; acc.y |= t4.y; acc.z |= t4.z; acc.w |= t4.w;
+        }
+        ends_inside = fe < pr + 16;
+    };
+    uint4 acc[P];
+    bool more = false;
+#pragma unroll
+    for (uint32_t k = 0; k < P; ++k) {
+        const int32_t pr = (int32_t)(k * 1024 + lane * 16);
+        acc[k] = make_uint4(0, 0, 0, 0);
+        bool ea, eb;
+        part(ta[k], pr, acc[k], ea);
+        part(ta[k] + 1, pr, acc[k], eb);
+        more |= ea && eb && ta[k] + 2 < (int32_t)nl;
+    }
+    if (__ballot(more)) {   // rare: frames shorter than 16 B -> a third, fourth ... frame in a piece
+#pragma unroll
+        for (uint32_t k = 0; k < P; ++k) {
+            const int32_t pr = (int32_t)(k * 1024 + lane * 16);
+            int32_t t = ta[k] + 2;
+            bool act = true;
+            while (__ballot(act && t < (int32_t)nl)) {
+                const int32_t fo = __shfl(ro, t & 63);
+                act = act && t < (int32_t)nl && fo < pr + 16;
+                uint4 tmp = make_uint4(0, 0, 0, 0);
+                bool e;
+                part(t, pr, tmp, e);
+                if (act) { acc[k].x |= tmp.x; acc[k].y |= tmp.y; acc[k].z |= tmp.z; acc[k].w |= tmp.w; }
+                ++t;
+            }
+        }
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < P; ++k) {
+        const uint64_t pa = wbase + k * 1024u + lane * 16u;
+        if (pa >= limit) continue;
+        if (pa + 16 <= limit) {
+            st16v<NT>(a.out + pa, u32x4{acc[k].x, acc[k].y, acc[k].z, acc[k].w});
+        } else {   // the tail piece: never write at or past the total / out_cap
+            const uint32_t d[4] = {acc[k].x, acc[k].y, acc[k].z, acc[k].w};
+#pragma unroll
+            for (uint32_t b = 0; b < 16; ++b)
+                if (pa + b < limit) a.out[pa + b] = (uint8_t)(d[b >> 2] >> (8 * (b & 3)));
+        }
+    }
+    return true;
+}
+
 // ---------------------------------------------------------------------------------------------
 // Copy: one ENC_WIN-byte output window per wave.
 // ---------------------------------------------------------------------------------------------
@@ -193,7 +304,9 @@ __global__ __launch_bounds__(256) void k_encode_copy(EncCopyArgs a) {
         for (uint32_t k = 0; k < P; ++k) st16v<NT>(a.out + wbase + k * 1024u + lofs, u32x4{v[k].x, v[k].y, v[k].z, v[k].w});
         return;
     }
-    // general path: frame edges in the window -> assemble every piece from all overlapping frames
+    // general path: frame edges in the window -> lane-parallel frame lookup (serial walk over the
+    // frames only when more than 64 of them overlap the window)
+    if (encode_window_lanes<NT>(a, m, wbase, limit, lane)) return;
     uint4 acc[P];
 #pragma unroll
     for (uint32_t k = 0; k < P; ++k) acc[k] = make_uint4(0, 0, 0, 0);
