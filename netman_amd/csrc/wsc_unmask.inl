@@ -119,12 +119,6 @@ __device__ __forceinline__ u32x4 range_mask16(int32_t lo, int32_t hi) {
     return m;
 }
 
-// General window, lane-parallel: the wave loads the window's spans into lanes with one vector
-// load (span r0 + lane), then every lane finds the span holding its piece by a 6-step binary
-// search over the lanes (ds_bpermute) and takes that span and the next one -- at most 2 spans per
-// 16-byte piece unless spans are shorter than 16 B, which a uniform tail loop handles.  No
-// dependent scalar loads per span; in COMPACT mode all of a lane's gathers are issued together.
-// Returns false (nothing written) when more than 64 spans overlap the window.
 // lane 0's value, as a wave-uniform (scalar) value
 __device__ __forceinline__ uint64_t lane0_u64(uint64_t x) {
     const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)x, 0), hi = __builtin_amdgcn_readlane((uint32_t)(x >> 32), 0);
@@ -144,6 +138,12 @@ __device__ __forceinline__ bool load_span_lane(const Span* __restrict__ spans, u
     return false;
 }
 
+// General window, lane-parallel: the wave loads the window's spans into lanes with one vector
+// load (span r0 + lane), then every lane finds the span holding its piece by a 6-step binary
+// search over the lanes (ds_bpermute) and takes that span and the next one -- at most 2 spans per
+// 16-byte piece unless spans are shorter than 16 B, which a uniform tail loop handles.  No
+// dependent scalar loads per span; in COMPACT mode all of a lane's gathers are issued together.
+// Returns false (nothing written) when more than 64 spans overlap the window.
 template <bool COMPACT, int P, int NT>
 __device__ __forceinline__ bool unmask_window_lanes(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src,
                                                     uint64_t src_bytes, const Span& sp, bool valid,
