@@ -154,7 +154,8 @@ typedef struct wsc_config {
     uint64_t max_frame_len;    /* payloads above this -> WSC_ERR_TOO_LARGE (<= 0xFFFFFFFF)       */
     uint32_t unmask_window;    /* bytes per wave-window in the unmask kernel: 4096 / 8192 (0 = 4096) */
     uint32_t unmask_waves_per_cu; /* unmask grid sizing (0 = default)                            */
-    uint32_t unmask_nt;        /* bit0: non-temporal payload loads, bit1: non-temporal stores     */
+    uint32_t unmask_nt;        /* in place: bit0 non-temporal payload loads, bit1 non-temporal    */
+                               /* stores; COMPACT: bits 2 and 3 likewise                          */
     uint32_t unmask_minw;      /* reserved (0); was an occupancy hint, measured no gain        */
 } wsc_config;
 

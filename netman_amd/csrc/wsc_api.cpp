@@ -103,7 +103,8 @@ int wsc_config_default(wsc_config* cfg) {
     cfg->max_frame_len = 0x7FFFFFFFull;
     cfg->unmask_window = 4096;       // tools/tune_unmask.py, profiles/r01_tune_*.log
     cfg->unmask_waves_per_cu = 0;    // 0: one window per wave (grid = windows)
-    cfg->unmask_nt = 3;              // non-temporal loads and stores
+    cfg->unmask_nt = 3;              // in place: non-temporal loads and stores; COMPACT (bits 2-3): default
+                                     // policy (its byte-aligned arena stores merge in L2: measured faster)
     return WSC_OK;
 }
 
@@ -304,13 +305,10 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     rec(3);
 
     uint8_t* udst = compact ? b->arena : b->wire;
-    const uint64_t udst_bytes = compact ? 0 : b->n_bytes;
     const uint64_t wb = (uint64_t)c->pieces * 1024;
     const uint64_t n_win = (b->n_bytes + wb - 1) / wb;
-    // in place: one window per wave; COMPACT: a resident grid that strides over the windows so the
-    // span lookup of the next window is prefetched under the current one (wsc_unmask.inl)
-    uint64_t waves = c->cfg.unmask_waves_per_cu ? (uint64_t)c->n_cu * c->cfg.unmask_waves_per_cu
-                                                : (compact ? (uint64_t)c->n_cu * 12 : n_win);
+    // one wire window per wave (both modes read the wire window by window, wsc_unmask.inl)
+    uint64_t waves = c->cfg.unmask_waves_per_cu ? (uint64_t)c->n_cu * c->cfg.unmask_waves_per_cu : n_win;
     if (waves > n_win) waves = n_win;
     if (waves == 0) waves = 1;
     const dim3 ublk(256), ugrid((uint32_t)((waves + 3) / 4));
@@ -323,8 +321,8 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
         {{k_unmask<true, 4, 0, 1>, k_unmask<true, 4, 1, 1>, k_unmask<true, 4, 2, 1>, k_unmask<true, 4, 3, 1>},
          {k_unmask<true, 8, 0, 1>, k_unmask<true, 8, 1, 1>, k_unmask<true, 8, 2, 1>, k_unmask<true, 8, 3, 1>}}};
     const int pi = c->pieces == 4 ? 0 : 1;
-    UK kern = table[compact ? 1 : 0][pi][c->cfg.unmask_nt & 3];
-    hipLaunchKernelGGL(kern, ugrid, ublk, 0, st, udst, (const uint8_t*)b->wire, b->n_bytes, udst_bytes,
+    UK kern = table[compact ? 1 : 0][pi][compact ? (c->cfg.unmask_nt >> 2) & 3 : c->cfg.unmask_nt & 3];
+    hipLaunchKernelGGL(kern, ugrid, ublk, 0, st, udst, (const uint8_t*)b->wire, b->n_bytes, b->n_bytes,
                        (const Span*)c->spans, (const uint32_t*)c->tile, (const wsc_summary*)b->summary,
                        c->lb_state, (n + 255) / 256 + 1);   // re-arms ticket, timeout, item count, flags
     HIP_TRY(hipGetLastError());

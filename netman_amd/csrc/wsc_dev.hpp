@@ -62,6 +62,7 @@ __device__ __forceinline__ uint4 load16_unaligned(const uint8_t* __restrict__ sr
 }
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
 template <int NT>
 __device__ __forceinline__ u32x4 ld16v(const uint8_t* p) {
     if constexpr (NT & 1) return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
@@ -72,6 +73,60 @@ __device__ __forceinline__ void st16v(uint8_t* p, u32x4 v) {
     if constexpr (NT & 2) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
     else *reinterpret_cast<u32x4*>(p) = v;
 }
+// Byte-aligned stores (gfx950 global memory takes unaligned dword/dwordx2/dwordx4 addresses; the
+// compiler emits the same instructions for align-1 accesses).
+typedef unsigned int u32x4u __attribute__((ext_vector_type(4), aligned(1)));
+typedef unsigned int u32x2u __attribute__((ext_vector_type(2), aligned(1)));
+typedef unsigned int u32u __attribute__((aligned(1)));
+typedef unsigned short u16u __attribute__((aligned(1)));
+template <int NT>
+__device__ __forceinline__ void st16u(uint8_t* p, u32x4 v) {
+    const u32x4u t = {v.x, v.y, v.z, v.w};
+    if constexpr (NT & 2) __builtin_nontemporal_store(t, reinterpret_cast<u32x4u*>(p));
+    else *reinterpret_cast<u32x4u*>(p) = t;
+}
+
+// bytes [sh, sh + 16) of the 16-byte vector x followed by zeros (sh in [0, 16))
+__device__ __forceinline__ u32x4 shr_bytes16(u32x4 x, uint32_t sh) {
+    const uint32_t d[8] = {x.x, x.y, x.z, x.w, 0u, 0u, 0u, 0u};
+    const uint32_t q = sh >> 2, rb = sh & 3;
+    u32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        uint32_t lo = d[j], hi = d[j + 1];
+        if (q == 1) { lo = d[j + 1]; hi = d[j + 2]; }
+        else if (q == 2) { lo = d[j + 2]; hi = d[j + 3]; }
+        else if (q == 3) { lo = d[j + 3]; hi = d[j + 4]; }
+        o[j] = __builtin_amdgcn_alignbyte(hi, lo, rb);
+    }
+    return o;
+}
+
+// Store bytes [lo, hi) of the 16-byte vector x at p (p = where byte lo goes; 0 <= lo < hi <= 16):
+// at most four stores of 8, 4, 2 and 1 bytes (one of 16 for a whole piece); nothing else is touched.
+template <int NT>
+__device__ __forceinline__ void store_run(uint8_t* p, u32x4 x, uint32_t lo, uint32_t hi) {
+    const uint32_t n = hi - lo;
+    if (n == 16) { st16u<NT>(p, x); return; }
+    u32x4 y = shr_bytes16(x, lo);
+    if (n & 8) {
+        *reinterpret_cast<u32x2u*>(p) = u32x2u{y.x, y.y};
+        p += 8;
+        y = u32x4{y.z, y.w, 0u, 0u};
+    }
+    if (n & 4) {
+        *reinterpret_cast<u32u*>(p) = y.x;
+        p += 4;
+        y = u32x4{y.y, y.z, 0u, 0u};
+    }
+    if (n & 2) {
+        *reinterpret_cast<u16u*>(p) = (uint16_t)y.x;
+        p += 2;
+        y.x >>= 16;
+    }
+    if (n & 1) *p = (uint8_t)y.x;
+}
+
 template <int NT>
 __device__ __forceinline__ uint4 ld16(const uint8_t* p) {
     const u32x4 t = ld16v<NT>(p);

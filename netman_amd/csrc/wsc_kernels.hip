@@ -134,14 +134,11 @@ __device__ __forceinline__ EmitCtx emit_begin(const WalkArgs& a, uint32_t s, uin
     e.own_spans0 = own.spans0;
     e.nf = e.ns0 = e.ns1 = 0;
     e.nb0 = e.nb1 = 0;
+    // spans are emitted in stream order in both modes and the window index is keyed by wire
+    // offset: the unmask reads the wire window by window (COMPACT stores each run at its arena dst)
     const uint64_t W = 1ull << a.win_shift;
-    if constexpr (COMPACT) {
-        e.nx0 = (e.abase + W - 1) & ~(W - 1);
-        e.nx1 = (e.abase + own.bytes0 + W - 1) & ~(W - 1);
-    } else {
-        e.nx0 = (seg_start + W - 1) & ~(W - 1);
-        e.nx1 = 0;
-    }
+    e.nx0 = (seg_start + W - 1) & ~(W - 1);
+    e.nx1 = 0;
     return e;
 }
 
@@ -168,18 +165,14 @@ __device__ __forceinline__ void emit_frame(const WalkArgs& a, EmitCtx& e, const 
         Span sp;
         sp.src = fr.hdr_off + fr.hdr_len;
         sp.len = plen;
-        uint32_t idx;
-        if (COMPACT && region) {
-            sp.dst = e.abase + e.own_bytes0 + e.nb1;
-            idx = e.sbase + e.own_spans0 + e.ns1;
-        } else {
-            sp.dst = COMPACT ? e.abase + e.nb0 : sp.src;
-            idx = e.sbase + e.ns0;
-        }
-        sp.key = rotr32(fr.mask, 8u * ((uint32_t)(0u - (uint32_t)sp.dst) & 3u));
+        if (COMPACT && region) sp.dst = e.abase + e.own_bytes0 + e.nb1;
+        else sp.dst = COMPACT ? e.abase + e.nb0 : sp.src;
+        const uint32_t idx = e.sbase + e.ns0 + e.ns1;   // stream order
+        // the key is phased at the wire: every aligned wire dword XORs with one register
+        sp.key = rotr32(fr.mask, 8u * ((uint32_t)(0u - (uint32_t)sp.src) & 3u));
         if (idx < a.spans_cap) a.spans[idx] = sp;
-        const uint64_t dend = sp.dst + plen;
-        uint64_t& nx = (COMPACT && region) ? e.nx1 : e.nx0;
+        const uint64_t dend = sp.src + plen;
+        uint64_t& nx = e.nx0;
         if (nx < dend) {   // windows [nx, dend) start inside this span: consecutive entries
             uint64_t t = nx >> a.win_shift;
             const uint64_t t_end = ((dend - 1) >> a.win_shift) + 1;
@@ -205,13 +198,7 @@ template <bool COMPACT>
 __device__ __forceinline__ void emit_end(const WalkArgs& a, EmitCtx& e, const WalkEnd& w) {
     const uint64_t W = 1ull << a.win_shift;
     // windows that start in this segment's region(s) after its last span
-    if constexpr (COMPACT) {
-        const uint64_t e0 = e.abase + e.nb0, e1 = e0 + e.nb1;
-        for (; e.nx0 < e0; e.nx0 += W) a.tile_first[e.nx0 >> a.win_shift] = e.sbase + e.ns0;
-        for (; e.nx1 < e1; e.nx1 += W) a.tile_first[e.nx1 >> a.win_shift] = e.sbase + e.ns0 + e.ns1;
-    } else {
-        for (; e.nx0 < e.seg_end; e.nx0 += W) a.tile_first[e.nx0 >> a.win_shift] = e.sbase + e.ns0;
-    }
+    for (; e.nx0 < e.seg_end; e.nx0 += W) a.tile_first[e.nx0 >> a.win_shift] = e.sbase + e.ns0 + e.ns1;
     wsc_seg_result r;
     r.consumed = w.pos - e.seg_start;
     r.frame_begin = e.fbase;

@@ -79,7 +79,7 @@ struct WalkArgs {
     Span* spans;
     uint32_t spans_cap;
     uint32_t win_shift;          // log2(unmask window bytes)
-    uint32_t* tile_first;        // per window: first span whose dst end > window start
+    uint32_t* tile_first;        // per wire window: first span (stream order) whose wire end > window start
     uint64_t* frame_dst;         // COMPACT
     wsc_conn_state* state_out;
     wsc_seg_result* seg_out;

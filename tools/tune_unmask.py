@@ -53,7 +53,7 @@ codecs = {}
 for w, wpc, nt, mw in combos:
     codecs[(w, wpc, nt, mw)] = K.Codec(0, max_batch_bytes=len(cfg["wire"]) + 4096, max_segs=n_segs,
                                        max_frames=cfg["n_frames"] + 16, unmask_window=w,
-                                       unmask_waves_per_cu=wpc, unmask_nt=nt, unmask_minw=mw)
+                                       unmask_waves_per_cu=wpc, unmask_nt=(nt << 2) if compact else nt, unmask_minw=mw)
 res = {c: [] for c in combos}
 for r in range(a.rounds):
     for c in combos:
