@@ -18,47 +18,24 @@ __device__ __forceinline__ uint32_t bytes_to_mask(uint32_t lo, uint32_t hi) {
     return a & b;
 }
 
-// 16 bytes starting at src + off (off may be unaligned); bytes outside [0, n) read as 0
+typedef unsigned int u32x4u_ld __attribute__((ext_vector_type(4), aligned(1)));
+
+// 16 bytes starting at src + off (off may be unaligned); bytes outside [0, n) read as 0.  Inside
+// the buffer this is ONE byte-aligned 16-byte load (gfx950 global memory takes unaligned
+// addresses; a wave's 64 loads still cover one contiguous ~1 KiB range); at the edges, byte loads.
 __device__ __forceinline__ uint4 load16_unaligned(const uint8_t* __restrict__ src, int64_t off,
                                                   uint64_t n) {
-    const int64_t c0 = off & ~(int64_t)15;
-    const uint32_t sh = (uint32_t)(off - c0);
-    uint4 v0 = make_uint4(0, 0, 0, 0), v1 = make_uint4(0, 0, 0, 0);
-    if (c0 >= 0 && (uint64_t)c0 + 16 <= n) v0 = *reinterpret_cast<const uint4*>(src + c0);
-    else {
-        uint32_t t[4] = {0, 0, 0, 0};
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const int64_t q = c0 + j;
-            if (q >= 0 && (uint64_t)q < n) t[j >> 2] |= (uint32_t)src[q] << (8 * (j & 3));
-        }
-        v0 = make_uint4(t[0], t[1], t[2], t[3]);
+    if (off >= 0 && (uint64_t)off + 16 <= n) {
+        const u32x4u_ld t = *reinterpret_cast<const u32x4u_ld*>(src + off);
+        return make_uint4(t.x, t.y, t.z, t.w);
     }
-    if (sh == 0) return v0;
-    const int64_t c1 = c0 + 16;
-    if (c1 >= 0 && (uint64_t)c1 + 16 <= n) v1 = *reinterpret_cast<const uint4*>(src + c1);
-    else {
-        uint32_t t[4] = {0, 0, 0, 0};
+    uint32_t t[4] = {0, 0, 0, 0};
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const int64_t q = c1 + j;
-            if (q >= 0 && (uint64_t)q < n) t[j >> 2] |= (uint32_t)src[q] << (8 * (j & 3));
-        }
-        v1 = make_uint4(t[0], t[1], t[2], t[3]);
+    for (int j = 0; j < 16; ++j) {
+        const int64_t q = off + j;
+        if (q >= 0 && (uint64_t)q < n) t[j >> 2] |= (uint32_t)src[q] << (8 * (j & 3));
     }
-    const uint32_t d[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-    const uint32_t q = sh >> 2, rb = sh & 3;
-    uint32_t o[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        // select dwords q+j and q+j+1 without dynamic register indexing
-        uint32_t lo = d[j], hi = d[j + 1];
-        if (q == 1) { lo = d[j + 1]; hi = d[j + 2]; }
-        else if (q == 2) { lo = d[j + 2]; hi = d[j + 3]; }
-        else if (q == 3) { lo = d[j + 3]; hi = d[j + 4]; }
-        o[j] = __builtin_amdgcn_alignbyte(hi, lo, rb);
-    }
-    return make_uint4(o[0], o[1], o[2], o[3]);
+    return make_uint4(t[0], t[1], t[2], t[3]);
 }
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
