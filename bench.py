@@ -218,19 +218,20 @@ def main():
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "kernel": "k_unmask", "alg_bytes_per_launch": alg_bytes},
     }
-    if rank == 0 and not a.no_host_inclusive:
+    solo = world == 1   # the extra lines (host-inclusive, other configs, encode, echo, CPU baseline) are N=1 only
+    if solo and not a.no_host_inclusive:
         out["host_inclusive"] = host_inclusive(codec, cfg, K)
         out["host_inclusive_pipelined"] = host_inclusive_pipelined(torch, codecs, streams, cfg, K)
     for c in codecs:
         c.close()
-    if rank == 0 and not a.no_other_configs:
+    if solo and not a.no_other_configs:
         del keep, batches
         torch.cuda.empty_cache()
         out["other_configs"] = other_configs(torch, K, synth)
         out["encode"] = encode_configs(torch, K, synth)
-    if rank == 0 and not a.no_echo:
+    if solo and not a.no_echo:
         out["echo"] = echo_configs(with_cpu=not a.no_cpu)
-    if rank == 0 and not a.no_cpu and a.cpu_seconds > 0:
+    if solo and not a.no_cpu and a.cpu_seconds > 0:
         threads = min(16, len(os.sched_getaffinity(0)))
         v1, p1, e1 = cpu_baseline(cfg, a.cpu_seconds / 2, 1)
         vm, pm_, em = cpu_baseline(cfg, a.cpu_seconds / 2, threads)
@@ -251,6 +252,8 @@ def other_configs(torch, K, synth):
     res = {}
     cases = [("configs[1] 1M x 1 KiB BIN, 16 frames/segment", lambda: synth.uniform_batch(1 << 20, 1024, 16, seed=synth.SEED_BASE + 1), False),
              ("configs[2] 256k mixed 125 B / 64 KiB / 1 MiB (p~1/size)", lambda: synth.mixed_batch(), False),
+             ("configs[3] one GPU's shard: 1M x 4 KiB BIN, 16 frames/segment",
+              lambda: synth.uniform_batch(1 << 20, 4096, 16, seed=synth.SEED_BASE + 3), False),
              ("configs[4] 64k connections x fragmented message, reassembled (COMPACT)", lambda: synth.fragmented_batch(), True),
              ("TEXT 16384 x 64 KiB valid UTF-8 (1-4 byte characters), 4 frames/segment",
               lambda: synth.text_batch(16384, 65536, 4, seed=synth.SEED_BASE + 7), False),

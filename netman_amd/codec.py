@@ -19,7 +19,8 @@ from dataclasses import dataclass
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libwscodec.so")
+# WSC_LIB: an alternative build of the same library (A/B timing experiments in tools/ only)
+LIB_PATH = os.environ.get("WSC_LIB") or os.path.join(HERE, "libwscodec.so")
 
 # ---- constants (include/wscodec.h) -------------------------------------------------------------
 WSC_OK = 0

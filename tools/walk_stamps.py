@@ -11,14 +11,18 @@ from netman_amd import codec as K, synth
 wl = sys.argv[1] if len(sys.argv) > 1 else "64k"
 cfg = {"64k": lambda: synth.uniform_batch(16384, 65536, 4, seed=synth.SEED_BASE + 1),
        "1k": lambda: synth.uniform_batch(1 << 20, 1024, 16, seed=synth.SEED_BASE + 1),
-       "mixed": lambda: synth.mixed_batch()}[wl]()
+       "mixed": lambda: synth.mixed_batch(),
+       "frag": lambda: synth.fragmented_batch()}[wl]()
+compact = wl == "frag"
 dev = torch.device("cuda:0")
 n = len(cfg["seg_off"]) - 1
 c = K.Codec(0, max_batch_bytes=len(cfg["wire"]) + 4096, max_segs=n, max_frames=cfg["n_frames"] + 16)
 t = [torch.from_numpy(cfg["wire"]).to(dev), torch.from_numpy(cfg["seg_off"].view(np.int64)).to(dev),
      torch.zeros(n * 16, dtype=torch.uint8, device=dev), torch.zeros(n * 32, dtype=torch.uint8, device=dev),
      torch.zeros((cfg["n_frames"] + 16) * 32, dtype=torch.uint8, device=dev), torch.zeros(32, dtype=torch.uint8, device=dev)]
-b = c.make_batch(t[0], t[1], None, t[2], t[3], t[4], t[5])
+arena = torch.zeros(len(cfg["wire"]) + 64, dtype=torch.uint8, device=dev) if compact else None
+fdst = torch.zeros(cfg["n_frames"] + 16, dtype=torch.int64, device=dev) if compact else None
+b = c.make_batch(t[0], t[1], None, t[2], t[3], t[4], t[5], compact=compact, arena=arena, frame_dst=fdst)
 nb = (n + 255) // 256
 for it in range(3):
     c.decode(b)
