@@ -66,7 +66,8 @@ def test_fuzz_text_heavy(codec):
     _check_batch(codec, streams)
 
 
-def test_edge_lengths(codec):
+@pytest.mark.parametrize("compact", [False, True])
+def test_edge_lengths(codec, compact):
     streams = []
     for n in [0, 1, 2, 3, 4, 5, 15, 16, 17, 125, 126, 127, 1023, 1024, 1025, 65535, 65536, 65537, 1 << 20]:
         streams.append(synth.frame(2, bytes(np.random.default_rng(n).bytes(n)), mask=0xDEADBEEF))
@@ -75,7 +76,34 @@ def test_edge_lengths(codec):
     streams.append(b"")
     streams.append(b"\x82")                         # incomplete header
     streams.append(synth.frame(2, b"abc")[:-1])     # incomplete payload
-    _check_batch(codec, streams)
+    _check_batch(codec, streams, compact=compact)
+
+
+@pytest.mark.parametrize("compact", [False, True])
+def test_tiny_frames_many_per_piece(codec, compact):
+    """Frames of 0-40 B: several spans per 16-byte piece (the tail loop), more than 64 spans per
+    4 KiB window (the serial fallback), fragments of 0-8 B with PINGs between them, and runs that
+    end on the last bytes of the wire (the partial last window)."""
+    rng = np.random.default_rng(77)
+    streams = []
+    s = b"".join(synth.frame(2, rng.bytes(int(rng.integers(0, 9))), mask=int(rng.integers(0, 2**32)))
+                 for _ in range(2000))
+    streams.append(s)
+    for i in range(300):
+        fr = []
+        for _ in range(int(rng.integers(1, 21))):
+            fr.append(synth.frame(2, rng.bytes(int(rng.integers(0, 41))), mask=int(rng.integers(0, 2**32))))
+        streams.append(b"".join(fr))
+    for i in range(100):   # fragmented: 0x02 FIN=0, 0x00 ..., 0x00 FIN=1 with tiny parts and PINGs
+        parts = [rng.bytes(int(rng.integers(0, 9))) for _ in range(int(rng.integers(2, 12)))]
+        out = bytearray()
+        for j, p in enumerate(parts):
+            out += synth.frame(2 if j == 0 else 0, p, fin=j == len(parts) - 1, mask=int(rng.integers(0, 2**32)))
+            if rng.random() < 0.3:
+                out += synth.frame(9, rng.bytes(int(rng.integers(0, 6))), mask=int(rng.integers(0, 2**32)))
+        streams.append(bytes(out))
+    streams.append(b"".join(synth.frame(2, bytes([k]) * k, mask=0x01020304) for k in (15, 16, 17, 1, 31, 32, 33)))
+    _check_batch(codec, streams, compact=compact)
 
 
 def test_max_frame_len(codec_lib):
