@@ -770,11 +770,76 @@ __device__ __forceinline__ uint64_t u8m_then(uint64_t a, uint64_t b) {   // a, t
     const uint32_t hi = (uint32_t)__builtin_amdgcn_perm(bh, bl, (uint32_t)(a >> 32));
     return (uint64_t)hi << 32 | lo;
 }
+// one level of the in-row composition: lanes that are multiples of 2*DD take "own map, then the map
+// of lane + DD" (DPP row_shl:DD -- lane i reads lane i + DD of its 16-lane row)
+template <int DD>
+__device__ __forceinline__ void u8m_row_level(uint32_t& mlo, uint32_t& mhi, uint32_t lane) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mlo, 0x100 | DD, 0xF, 0xF, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mhi, 0x100 | DD, 0xF, 0xF, false);
+    if ((lane & (2 * DD - 1)) == 0) {
+        const uint64_t c = u8m_then((uint64_t)mhi << 32 | mlo, (uint64_t)hi << 32 | lo);
+        mlo = (uint32_t)c;
+        mhi = (uint32_t)(c >> 32);
+    }
+}
 __device__ __forceinline__ uint32_t u8m_get(uint64_t m, uint32_t st) {   // st: 0..7, or >= 8 = reject
     return st > 7 ? 0xFFu : (uint32_t)(m >> (8 * st)) & 0xFFu;
 }
 
-__global__ __launch_bounds__(256) void k_u8_check(U8Args a) {
+// Publish one item's map; the segment's last item composes the segment's items in frame order
+// with the walk's states and applies the verdict (one lane).
+__device__ __forceinline__ void u8_finish(const U8Args& a, uint32_t it, const U8Item& item, uint64_t acc) {
+    __hip_atomic_store(a.maps + it, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t done = __hip_atomic_fetch_add(&a.seg[item.seg].done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+    const U8Seg g = a.seg[item.seg];
+    if (done != g.n) return;
+    // the segment's last item: compose its items in frame order with the walk's states
+    uint32_t cur = 0, start = 0, fail = 0xFFFFFFFFu;   // states 0..7, 0xFF = reject
+    uint64_t fm = u8m_id();
+    uint32_t j = g.head;
+    for (uint32_t c = 0; c < g.n && j != 0xFFFFFFFFu; ++c) {
+        const U8Item x = a.items[j];
+        const uint64_t m = __hip_atomic_fetch_add(a.maps + j, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (x.first) {
+            start = x.kind == U8K_SELF ? 0u : (x.s_in != 0xFF ? (x.s_in > 7 ? 0xFFu : (uint32_t)x.s_in) : cur);
+            fm = u8m_id();
+        }
+        fm = u8m_then(fm, m);
+        if (x.last) {
+            const uint32_t end = u8m_get(fm, start);
+            if (x.kind == U8K_PART) {
+                cur = end;
+            } else {
+                if (end != 0) { fail = x.ordinal; break; }
+                if (x.kind == U8K_CHAIN) cur = 0;
+            }
+        }
+        j = x.next;
+    }
+    const uint32_t s = item.seg;
+    if (fail == 0xFFFFFFFFu) {
+        if (g.pending_end && a.state_out[s].cont_len) a.state_out[s].cont_utf8 = (uint8_t)(cur > 7 ? 8u : cur);
+        return;
+    }
+    // frame `fail` fails: CloseCode(1007) there (epoll.go:126-127), nothing after it is read
+    wsc_frame* f = a.frames + g.fbase + fail;
+    f->kind = WSC_FK_ERROR;
+    f->err = WSC_ERR_MUST_UTF8;
+    const uint64_t fend = f->hdr_off + f->hdr_len + f->payload_len;
+    wsc_seg_result r = a.seg_out[s];
+    r.consumed = fend - a.seg_off[s];
+    r.frame_count = fail + 1;
+    r.status = WSC_SEG_ERROR;
+    r.close_code = 1007;
+    r.err = WSC_ERR_MUST_UTF8;
+    a.seg_out[s] = r;
+    a.state_out[s].status = WSC_SEG_ERROR;
+    for (uint32_t k = 0; k < g.nspans; ++k)   // later frames stay masked (the reference never reads them)
+        if (a.spans[g.sbase + k].src >= fend) a.spans[g.sbase + k].key = 0;
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_u8_check(U8Args a) {
     const uint32_t n_items = *a.count;
     if (blockIdx.x * 4 >= n_items) return;   // nothing deferred (the common, binary case)
     __shared__ uint64_t tab[256];            // T[byte]: the map of that single byte
@@ -791,24 +856,33 @@ __global__ __launch_bounds__(256) void k_u8_check(U8Args a) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
     const uint32_t nw = gridDim.x * 4;
-    for (uint32_t it = gw; it < n_items; it += nw) {
-        const U8Item item = a.items[it];
-        uint64_t acc = u8m_id();
-        // the next 4 KiB step's loads are issued before the current step is folded
-        uint4 nxt[4];
+    // 4 KiB of item.src + b0 into q (bytes past the item read as 0)
+    auto fetch = [&](const U8Item& x, uint32_t b0, uint4 (&q)[4]) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const uint32_t off = k * 1024 + lane * 16;
-            nxt[k] = off < item.len ? load16_unaligned(a.wire, (int64_t)(item.src + off), a.n_bytes) : make_uint4(0, 0, 0, 0);
+            const uint32_t off = b0 + k * 1024 + lane * 16;
+            q[k] = off < x.len ? load16_unaligned(a.wire, (int64_t)(x.src + off), a.n_bytes) : make_uint4(0, 0, 0, 0);
         }
+    };
+    if (gw >= n_items) return;
+    uint32_t it = gw;
+    U8Item item = a.items[it];
+    // the next 4 KiB step's loads are issued before the current step is folded, across items too
+    // (the next item's first step is fetched under the current item's last step)
+    uint4 nxt[4];
+    fetch(item, 0, nxt);
+    while (it < n_items) {
+        const uint32_t it2 = it + nw;
+        U8Item item2 = item;
+        if (it2 < n_items) item2 = a.items[it2];
+        uint64_t acc = u8m_id();
+        if (item.len == 0 && it2 < n_items) fetch(item2, 0, nxt);
         for (uint32_t b0 = 0; b0 < item.len; b0 += 4096) {
             uint4 cur4[4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                cur4[k] = nxt[k];
-                const uint32_t off = b0 + 4096 + k * 1024 + lane * 16;
-                nxt[k] = off < item.len ? load16_unaligned(a.wire, (int64_t)(item.src + off), a.n_bytes) : make_uint4(0, 0, 0, 0);
-            }
+            for (int k = 0; k < 4; ++k) cur4[k] = nxt[k];
+            if (b0 + 4096 < item.len) fetch(item, b0 + 4096, nxt);
+            else if (it2 < n_items) fetch(item2, 0, nxt);
             uint64_t pm[4];
             bool plain = true;
 #pragma unroll
@@ -831,6 +905,34 @@ __global__ __launch_bounds__(256) void k_u8_check(U8Args a) {
                     pm[k] = u8m_id();
                 } else if (hib == 0) {
                     pm[k] = u8m_ascii();
+                } else if (nk == 16) {
+                    // Every entry state that survives the first 4 bytes is in ONE state X there:
+                    // a survivor must be in state 0 just before the first lead byte (a lead in a
+                    // non-zero state rejects), and 4 continuation bytes reject every state (at most
+                    // 3 are owed).  So the first 4 bytes compose full maps (2 v_perm per byte), the
+                    // other 12 step the single state X (1 v_perm per byte), and the piece's map is the
+                    // prefix map with every surviving entry sent to the final state.
+                    uint32_t lo = 0x03020100u, hi = 0x07060504u;
+#pragma unroll
+                    for (uint32_t i = 0; i < 4; ++i) {
+                        const uint64_t t = tab[(d[0] >> (8 * i)) & 0xFFu];
+                        const uint32_t tl = (uint32_t)t, th = (uint32_t)(t >> 32);
+                        lo = (uint32_t)__builtin_amdgcn_perm(th, tl, lo);
+                        hi = (uint32_t)__builtin_amdgcn_perm(th, tl, hi);
+                    }
+                    uint32_t x = lo & hi;             // non-rejected bytes all equal X, rejects are 0xFF
+                    x &= x >> 16;
+                    x &= x >> 8;
+#pragma unroll
+                    for (uint32_t i = 4; i < 16; ++i) {
+                        const uint64_t t = tab[(d[i >> 2] >> (8 * (i & 3))) & 0xFFu];
+                        x = (uint32_t)__builtin_amdgcn_perm((uint32_t)(t >> 32), (uint32_t)t, x);   // byte 0 = T[b][X]
+                    }
+                    const uint32_t fr = (x & 0xFFu) * 0x01010101u;
+                    lo = (uint32_t)__builtin_amdgcn_perm(fr, fr, lo);   // 0..7 -> final state, 0xFF stays
+                    hi = (uint32_t)__builtin_amdgcn_perm(fr, fr, hi);
+                    pm[k] = (uint64_t)hi << 32 | lo;
+                    plain = false;
                 } else {
                     uint32_t lo = 0x03020100u, hi = 0x07060504u;
 #pragma unroll
@@ -854,69 +956,27 @@ __global__ __launch_bounds__(256) void k_u8_check(U8Args a) {
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {     // lanes in order, then pieces in order
                     if (b0 + k * 1024 >= item.len) break;   // the rest of the step is past the item
-                    uint64_t m = pm[k];
+                    // compose the 16 lanes of each row in order with DPP row shifts (VALU, no LDS
+                    // crossbar: the table reads already keep the LDS pipe busy), then the 4 rows
+                    uint32_t mlo = (uint32_t)pm[k], mhi = (uint32_t)(pm[k] >> 32);
+                    u8m_row_level<1>(mlo, mhi, lane);
+                    u8m_row_level<2>(mlo, mhi, lane);
+                    u8m_row_level<4>(mlo, mhi, lane);
+                    u8m_row_level<8>(mlo, mhi, lane);
 #pragma unroll
-                    for (int dd = 1; dd < 64; dd <<= 1) {
-                        const uint32_t lo = __shfl_down((uint32_t)m, dd), hi = __shfl_down((uint32_t)(m >> 32), dd);
-                        if ((lane & (2 * dd - 1)) == 0) m = u8m_then(m, (uint64_t)hi << 32 | lo);
+                    for (int r = 0; r < 4; ++r) {
+                        // readlane returns int: widen through uint32_t (no sign extension into the high word)
+                        const uint32_t rlo = (uint32_t)__builtin_amdgcn_readlane(mlo, 16 * r);
+                        const uint32_t rhi = (uint32_t)__builtin_amdgcn_readlane(mhi, 16 * r);
+                        stepm = u8m_then(stepm, (uint64_t)rhi << 32 | rlo);
                     }
-                    // readlane returns int: widen through uint32_t (no sign extension into the high word)
-                    const uint32_t m0lo = (uint32_t)__builtin_amdgcn_readlane((uint32_t)m, 0);
-                    const uint32_t m0hi = (uint32_t)__builtin_amdgcn_readlane((uint32_t)(m >> 32), 0);
-                    stepm = u8m_then(stepm, (uint64_t)m0hi << 32 | m0lo);
                 }
             }
             acc = u8m_then(acc, stepm);
         }
-        if (lane != 0) continue;
-        __hip_atomic_store(a.maps + it, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const uint32_t done = __hip_atomic_fetch_add(&a.seg[item.seg].done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
-        const U8Seg g = a.seg[item.seg];
-        if (done != g.n) continue;
-        // the segment's last item: compose its items in frame order with the walk's states
-        uint32_t cur = 0, start = 0, fail = 0xFFFFFFFFu;   // states 0..7, 0xFF = reject
-        uint64_t fm = u8m_id();
-        uint32_t j = g.head;
-        for (uint32_t c = 0; c < g.n && j != 0xFFFFFFFFu; ++c) {
-            const U8Item x = a.items[j];
-            const uint64_t m = __hip_atomic_fetch_add(a.maps + j, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (x.first) {
-                start = x.kind == U8K_SELF ? 0u : (x.s_in != 0xFF ? (x.s_in > 7 ? 0xFFu : (uint32_t)x.s_in) : cur);
-                fm = u8m_id();
-            }
-            fm = u8m_then(fm, m);
-            if (x.last) {
-                const uint32_t end = u8m_get(fm, start);
-                if (x.kind == U8K_PART) {
-                    cur = end;
-                } else {
-                    if (end != 0) { fail = x.ordinal; break; }
-                    if (x.kind == U8K_CHAIN) cur = 0;
-                }
-            }
-            j = x.next;
-        }
-        const uint32_t s = item.seg;
-        if (fail == 0xFFFFFFFFu) {
-            if (g.pending_end && a.state_out[s].cont_len) a.state_out[s].cont_utf8 = (uint8_t)(cur > 7 ? 8u : cur);
-            continue;
-        }
-        // frame `fail` fails: CloseCode(1007) there (epoll.go:126-127), nothing after it is read
-        wsc_frame* f = a.frames + g.fbase + fail;
-        f->kind = WSC_FK_ERROR;
-        f->err = WSC_ERR_MUST_UTF8;
-        const uint64_t fend = f->hdr_off + f->hdr_len + f->payload_len;
-        wsc_seg_result r = a.seg_out[s];
-        r.consumed = fend - a.seg_off[s];
-        r.frame_count = fail + 1;
-        r.status = WSC_SEG_ERROR;
-        r.close_code = 1007;
-        r.err = WSC_ERR_MUST_UTF8;
-        a.seg_out[s] = r;
-        a.state_out[s].status = WSC_SEG_ERROR;
-        for (uint32_t k = 0; k < g.nspans; ++k)   // later frames stay masked (the reference never reads them)
-            if (a.spans[g.sbase + k].src >= fend) a.spans[g.sbase + k].key = 0;
+        if (lane == 0) u8_finish(a, it, item, acc);
+        it = it2;
+        item = item2;
     }
 }
 

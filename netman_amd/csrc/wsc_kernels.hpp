@@ -36,7 +36,7 @@ enum : uint32_t { SEGF_UTF8 = 1u, SEGF_U8DEFER = 2u };
 // The walk validates text payloads of at most u8_inline_max bytes itself (serial DFA per lane);
 // larger ones -- and every later frame of a text chain that has a deferred part -- become items of
 // at most U8_PIECE bytes, validated by k_u8_check across the whole chip before the unmask runs.
-constexpr uint32_t U8_PIECE = 65536;
+constexpr uint32_t U8_PIECE = 16384;   // 16 KiB: 64 KiB items left a 25 % tail (equal-sized items vs residency)
 enum : uint8_t { U8K_SELF = 0, U8K_PART = 1, U8K_CHAIN = 2 };   // close reasons are SELF items
 struct U8Item {
     uint64_t src;       // wire offset of the first (masked) byte

@@ -121,13 +121,14 @@ def test_text_64k_frames_valid_and_invalid(codec_lib):
 
 
 def test_text_large_frames_cross_piece_characters(codec_lib):
-    """frames larger than one 64 KiB item with multi-byte characters across the item boundary,
+    """frames larger than one item (U8_PIECE = 16 KiB) with multi-byte characters across item edges,
     plus a TEXT chain of big fragments where a 4-byte character straddles two fragments"""
     e = "😀".encode()                                        # 4 bytes
     body = ("ab" + "é" * 40000 + "x").encode()               # 80003 bytes, 2-byte chars across 65536
-    body2 = b"a" * 65535 + e + b"z" * 100                    # emoji straddles the 64 KiB piece edge
+    body2 = b"a" * 65535 + e + b"z" * 100                    # emoji straddles a piece edge (65536)
+    body3 = ("abc" + "é" * 30000).encode()                   # 2-byte chars straddle every 16 KiB edge
     frag = e * 30000                                         # 120000 B, cut inside a character
-    s1 = synth.frame(1, body) + synth.frame(1, body2)
+    s1 = synth.frame(1, body) + synth.frame(1, body2) + synth.frame(1, body3)
     s2 = synth.frame(1, frag[:70001], fin=False) + synth.frame(0, frag[70001:], fin=True)
     s3 = synth.frame(1, frag[:70001], fin=False) + synth.frame(0, frag[70001:-1], fin=True)   # truncated char
     s4 = synth.frame(8, (1000).to_bytes(2, "big") + ("ü" * 61).encode())   # close reason, 124 B
