@@ -45,6 +45,12 @@ def parse():
     ap.add_argument("--pipeline", type=int, default=2,
                     help="batches in flight: each has its own context, wire buffer and HIP stream, so the "
                          "header walk of batch k+1 overlaps the unmask of batch k")
+    ap.add_argument("--walk-cus", type=int, default=16,
+                    help="split pipeline (wsc_decode_split): the header walk runs on a stream masked to this "
+                         "many CUs, the UTF-8 check + unmask on --unmask-streams streams over every CU "
+                         "(0 = every stage of a batch in order on its own stream)")
+    ap.add_argument("--unmask-streams", type=int, default=1)
+    ap.add_argument("--unmask-rest", action="store_true", help="mask the unmask streams to the CUs the walk does not use")
     ap.add_argument("--no-echo", action="store_true", help="skip the configs[0] loopback echo lines")
     ap.add_argument("--no-other-configs", action="store_true",
                     help="skip the device-time lines for BASELINE.json configs[1], [2], [4]")
@@ -142,12 +148,27 @@ def main():
         summ_h = t["summ"].cpu().numpy().copy().view(K.SUMMARY_DTYPE)[0]
         ok = ok and int(summ_h["n_frames"]) == a.frames and int(summ_h["n_spans"]) == a.frames
 
+    # split pipeline: one walk stream on the first walk_cus CUs, one unmask stream per in-flight
+    # batch on the rest, so batch k+1's walk runs beside batch k's unmask and the unmasks' ramp
+    # and tail overlap (tools/split_probe.py, profiles/r01_split_probe.log)
+    n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
+    split = P > 1 and 0 < a.walk_cus < n_cu
+    n_dec = [1] * P   # decodes issued per in-flight buffer (the gate above did one each)
+    if split:
+        walk_st = codec.stream_create(K.cu_mask(range(a.walk_cus), n_cu))
+        um = K.cu_mask(range(a.walk_cus, n_cu), n_cu) if a.unmask_rest else None
+        unmask_st = [codec.stream_create(um) for _ in range(max(1, a.unmask_streams))]
+
     def run(steps, depth):
-        # batch i goes to context/stream i % depth: independent batches, no cross-stream waits
-        # (chaining the unmasks with events measured slower: 0.361 vs 0.352 ms per step)
+        # batch i goes to context i % depth: independent batches (chaining the unmasks with
+        # events measured slower: 0.361 vs 0.352 ms per step)
         for i in range(steps):
             j = i % depth
-            codecs[j].decode(batches[j], streams[j].cuda_stream)
+            if split and depth == P:
+                codecs[j].decode_split(batches[j], walk_st, unmask_st[j % len(unmask_st)])
+            else:
+                codecs[j].decode(batches[j], streams[j].cuda_stream)
+            n_dec[j] += 1
 
     def timed(depth):
         run(a.warmup, depth)
@@ -167,6 +188,19 @@ def main():
 
     el_single = timed(1) if P > 1 else None   # one batch in flight: the per-batch latency
     el = timed(P)
+    # after the timed runs: each buffer was XORed n_dec times in place, so it must be the masked
+    # wire (even) or the unmasked reference (odd) on the sampled frames
+    for j, t in enumerate(keep):
+        host = t["wire"][: min(n_bytes, 64 * (a.frame_bytes + 14))].cpu().numpy().copy()
+        k = int(np.searchsorted(cfg["payload_off"] + cfg["plen"], len(host), side="right"))
+        end = int(cfg["payload_off"][k - 1] + cfg["plen"][k - 1])
+        want = synth.unmask_reference(cfg["wire"][: len(host)], cfg["payload_off"][:k], cfg["plen"][:k],
+                                      cfg["mask"][:k]) if n_dec[j] % 2 else cfg["wire"][: len(host)]
+        ok = ok and bool(np.array_equal(host[:end], want[:end]))
+    if split:
+        torch.cuda.synchronize()
+        for s_ in [walk_st] + unmask_st:
+            codec.stream_destroy(s_)
     if world > 1:
         okt = torch.tensor([1 if ok else 0], dtype=torch.int32, device=cdev)
         dist.all_reduce(okt, op=dist.ReduceOp.MIN)
@@ -208,7 +242,11 @@ def main():
                                f"{a.frames_per_seg} frames per connection segment), in-place unmask",
                    "frames_per_gpu": a.frames, "frame_bytes": a.frame_bytes,
                    "segments_per_gpu": n_segs, "parallelism": f"shard{world}",
-                   "batches_in_flight": P},
+                   "batches_in_flight": P,
+                   "pipeline": (f"split: walk on a stream masked to {a.walk_cus} CUs, UTF-8 check + unmask on "
+                                f"{len(unmask_st)} stream(s) over "
+                                f"{'the other ' + str(n_cu - a.walk_cus) if a.unmask_rest else 'all ' + str(n_cu)} CUs") if split
+                               else "each batch in order on its own stream"},
         "parity_ok": ok,
         "single_batch": None if el_single is None else {
             "ms_per_step": round(el_single / a.steps * 1e3, 4),

@@ -179,6 +179,20 @@ int wsc_host_free(void* p);
 int wsc_decode(wsc_ctx* ctx, const wsc_batch* batch, void* hip_stream);
 int wsc_sync(wsc_ctx* ctx, void* hip_stream);
 
+/* Split pipeline: the header walk runs on `walk_stream`, the UTF-8 check and unmask on
+ * `unmask_stream`, joined by the context's events.  The walk waits for this context's previous
+ * split decode to finish, so batches of different contexts overlap: the walk of one batch runs
+ * beside the unmask of the other.  Inputs must be ready on `walk_stream`; results are valid once
+ * `unmask_stream` is synchronised.  Pair it with CU-masked streams (wsc_stream_create) so that
+ * the walk has CUs the unmask grid does not occupy.  As with wsc_decode, a context runs one
+ * decode at a time: order a split decode and any other call on the same context yourself.     */
+int wsc_decode_split(wsc_ctx* ctx, const wsc_batch* batch, void* walk_stream, void* unmask_stream);
+
+/* A non-blocking stream on the context's device, restricted to the CUs whose bits are set in
+ * cu_mask[0..mask_words) (hipExtStreamCreateWithCUMask); cu_mask NULL = all CUs.             */
+int wsc_stream_create(wsc_ctx* ctx, const uint32_t* cu_mask, uint32_t mask_words, void** out);
+int wsc_stream_destroy(wsc_ctx* ctx, void* stream);
+
 /* Host-buffer path: copies wire/offsets/state to the device through the context's pinned
  * staging, decodes, and copies results back (synchronous).  In-place mode rewrites `wire`;
  * COMPACT mode fills `arena` (host, >= n_bytes + 64).  `frames` has room for `frames_cap`. */

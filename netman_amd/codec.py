@@ -94,6 +94,9 @@ SIGNATURES = {
     "wsc_host_free": (_I, [_P]),
     "wsc_decode": (_I, [_P, C.POINTER(WscBatch), _P]),
     "wsc_sync": (_I, [_P, _P]),
+    "wsc_decode_split": (_I, [_P, C.POINTER(WscBatch), _P, _P]),
+    "wsc_stream_create": (_I, [_P, _P, _U32, C.POINTER(_P)]),
+    "wsc_stream_destroy": (_I, [_P, _P]),
     "wsc_decode_host": (_I, [_P, _P, _U64, _P, _U32, _U32, _P, _P, _P, _P, _U32, _P, _P, _P]),
     "wsc_encode": (_I, [_P, _P, _U32, _P, _U64, _P, _U64, _P, _P]),
     "wsc_encode_host": (_I, [_P, _P, _U32, _P, _U64, _P, _U64, _P]),
@@ -176,6 +179,16 @@ class DecodeResult:
     arena: np.ndarray | None = None
 
 
+def cu_mask(cus, n_cu: int) -> list:
+    """u32 words of a hipExtStreamCreateWithCUMask mask with the bits of `cus` set"""
+    w = [0] * ((n_cu + 31) // 32)
+    for i in cus:
+        if not 0 <= i < n_cu:
+            raise ValueError(f"CU {i} out of range 0..{n_cu - 1}")
+        w[i // 32] |= 1 << (i % 32)
+    return w
+
+
 class Codec:
     """One device context (wsc_ctx)."""
 
@@ -230,6 +243,23 @@ class Codec:
 
     def decode(self, batch: WscBatch, stream=None):
         _check(self.lib.wsc_decode(self.h, C.byref(batch), self._stream(stream)), "wsc_decode")
+
+    def decode_split(self, batch: WscBatch, walk_stream: int, unmask_stream: int):
+        """walk on walk_stream, UTF-8 check + unmask on unmask_stream (wsc_decode_split)"""
+        _check(self.lib.wsc_decode_split(self.h, C.byref(batch), walk_stream, unmask_stream), "wsc_decode_split")
+
+    def stream_create(self, cu_mask=None) -> int:
+        """a raw hipStream_t (int), restricted to the CUs set in cu_mask (list of u32 words)"""
+        out = C.c_void_p()
+        if cu_mask is None:
+            _check(self.lib.wsc_stream_create(self.h, None, 0, C.byref(out)), "wsc_stream_create")
+        else:
+            arr = (C.c_uint32 * len(cu_mask))(*cu_mask)
+            _check(self.lib.wsc_stream_create(self.h, arr, len(cu_mask), C.byref(out)), "wsc_stream_create")
+        return out.value
+
+    def stream_destroy(self, stream: int):
+        _check(self.lib.wsc_stream_destroy(self.h, stream), "wsc_stream_destroy")
 
     def sync(self, stream=None):
         _check(self.lib.wsc_sync(self.h, self._stream(stream)), "wsc_sync")

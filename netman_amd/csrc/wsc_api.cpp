@@ -47,6 +47,8 @@ struct wsc_ctx {
     int device = 0;
     int n_cu = 256;
     hipStream_t stream = nullptr;
+    hipEvent_t ev_walked = nullptr;   // wsc_decode_split: walk done (unmask stream waits on it)
+    hipEvent_t ev_done = nullptr;     // wsc_decode_split: unmask done (the next walk on this ctx waits)
     wsc_config cfg{};
     uint32_t pieces = 8;          // 16 B pieces per lane -> window = pieces KiB
     SegCount* counts = nullptr;
@@ -155,6 +157,8 @@ int wsc_create(int device, const wsc_config* cfg_in, wsc_ctx** out) {
         if (e != hipSuccess && rc == WSC_OK) rc = fail(WSC_E_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
     };
     chk(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate");
+    chk(hipEventCreateWithFlags(&c->ev_walked, hipEventDisableTiming), "hipEventCreate");
+    chk(hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming), "hipEventCreate");
     chk(hipMalloc(&c->counts, cfg.max_segs * sizeof(SegCount)), "hipMalloc counts");
     const uint64_t max_blocks = (cfg.max_segs + 255) / 256 + 1;
     chk(hipMalloc(&c->lb_state, (max_blocks + 3) * sizeof(uint32_t)), "hipMalloc lb_state");
@@ -207,6 +211,8 @@ int wsc_destroy(wsc_ctx* c) {
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->ev_walked) (void)hipEventDestroy(c->ev_walked);
+    if (c->ev_done) (void)hipEventDestroy(c->ev_done);
     delete c;
     return WSC_OK;
 }
@@ -233,8 +239,11 @@ int wsc_host_free(void* p) {
     return WSC_OK;
 }
 
-// The launch sequence.  `ev` (optional, 6 pairs) brackets each stage for wsc_profile.
-static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev) {
+// The launch sequence.  `ev` (optional, 6 pairs) brackets each stage for wsc_profile.  With
+// sw != st (wsc_decode_split) the walk runs on sw and the UTF-8 check + unmask on st, joined by
+// the context's events; otherwise everything runs in order on st.
+static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev, hipStream_t sw = nullptr,
+                  bool split = false) {
     const bool compact = (b->flags & WSC_F_COMPACT) != 0;
     const uint32_t n = b->n_segs;
     if (n == 0) return fail(WSC_E_INVAL, "n_segs == 0");
@@ -282,9 +291,17 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
         if (ev) (void)hipEventRecord(ev[i], st);
     };
     rec(0);
-    if (compact) hipLaunchKernelGGL((k_walk_fused<true>), wgrid, wblk, 0, st, wa);
-    else hipLaunchKernelGGL((k_walk_fused<false>), wgrid, wblk, 0, st, wa);
+    // split: the walk reuses this context's scratch, so it waits for the context's previous unmask
+    // (an event never recorded is a no-op wait)
+    const hipStream_t ws = split ? sw : st;
+    if (split) HIP_TRY(hipStreamWaitEvent(ws, c->ev_done, 0));
+    if (compact) hipLaunchKernelGGL((k_walk_fused<true>), wgrid, wblk, 0, ws, wa);
+    else hipLaunchKernelGGL((k_walk_fused<false>), wgrid, wblk, 0, ws, wa);
     HIP_TRY(hipGetLastError());
+    if (split) {
+        HIP_TRY(hipEventRecord(c->ev_walked, ws));
+        HIP_TRY(hipStreamWaitEvent(st, c->ev_walked, 0));
+    }
     rec(1);
     // deferred UTF-8 (large text): verdicts applied before the unmask; exits at once without text
     U8Args ua{};
@@ -330,6 +347,7 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     rec(4);
 
     HIP_TRY(hipGetLastError());
+    if (split) HIP_TRY(hipEventRecord(c->ev_done, st));
     rec(5);
     return WSC_OK;
 }
@@ -339,6 +357,31 @@ int wsc_decode(wsc_ctx* c, const wsc_batch* b, void* hip_stream) {
     HIP_TRY(hipSetDevice(c->device));
     // like every HIP API: NULL is the default (null) stream
     return launch(c, b, static_cast<hipStream_t>(hip_stream), nullptr);
+}
+
+int wsc_decode_split(wsc_ctx* c, const wsc_batch* b, void* walk_stream, void* unmask_stream) {
+    if (!c || !b) return fail(WSC_E_INVAL, "NULL argument");
+    if (walk_stream == unmask_stream) return fail(WSC_E_INVAL, "walk_stream == unmask_stream: use wsc_decode");
+    HIP_TRY(hipSetDevice(c->device));
+    return launch(c, b, static_cast<hipStream_t>(unmask_stream), nullptr, static_cast<hipStream_t>(walk_stream), true);
+}
+
+int wsc_stream_create(wsc_ctx* c, const uint32_t* cu_mask, uint32_t mask_words, void** out) {
+    if (!c || !out) return fail(WSC_E_INVAL, "NULL argument");
+    *out = nullptr;
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t s = nullptr;
+    if (cu_mask && mask_words) HIP_TRY(hipExtStreamCreateWithCUMask(&s, mask_words, cu_mask));
+    else HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    *out = s;
+    return WSC_OK;
+}
+
+int wsc_stream_destroy(wsc_ctx* c, void* stream) {
+    if (!c) return fail(WSC_E_INVAL, "NULL ctx");
+    HIP_TRY(hipSetDevice(c->device));
+    if (stream) HIP_TRY(hipStreamDestroy(static_cast<hipStream_t>(stream)));
+    return WSC_OK;
 }
 
 int wsc_sync(wsc_ctx* c, void* hip_stream) {

@@ -358,3 +358,70 @@ def test_session_undrained_events_survive_next_decode(codec_lib):
     assert eb[0].type == K.EV_PONG and eb[0].data == b"ping-b"
     assert eb[1].type == K.EV_MESSAGE and eb[1].data == "καλημέρα".encode()
     sess.close()
+
+
+# ---- split pipeline (wsc_decode_split): walk on a CU-masked stream, unmask on others ----------
+@pytest.mark.parametrize("compact,layout", [(False, "bench"), (True, "bench"), (False, "rest2"), (True, "rest2")])
+def test_decode_split_pipeline_matches_oracle(codec_lib, compact, layout):
+    """two contexts in flight, walk stream on 16 CUs; the unmasks on one stream over every CU (the
+    bench's pipeline) or on one stream per context over the other CUs; every round re-arms the
+    wires and decodes both batches back to back, so one batch's walk runs beside the other's
+    unmask; each is compared with the oracle"""
+    torch = pytest.importorskip("torch")
+    dev = torch.device("cuda:0")
+    sets = [[random_stream(7000 + 400 * j + i, n_units=10) for i in range(300)] for j in range(2)]
+    ctxs, bats, ts, packed = [], [], [], []
+    for streams in sets:
+        wire, off = pack_streams(streams)
+        c = K.Codec(0, max_batch_bytes=len(wire) + 4096, max_segs=len(streams), max_frames=1 << 15)
+        n = len(streams)
+        t = dict(wire=torch.from_numpy(wire.copy()).to(dev), seg_off=torch.from_numpy(off.view(np.int64)).to(dev),
+                 st_out=torch.zeros(n * 16, dtype=torch.uint8, device=dev),
+                 seg_out=torch.zeros(n * 32, dtype=torch.uint8, device=dev),
+                 frames=torch.zeros((1 << 15) * 32, dtype=torch.uint8, device=dev),
+                 summ=torch.zeros(32, dtype=torch.uint8, device=dev))
+        if compact:
+            t["arena"] = torch.zeros(len(wire) + 64, dtype=torch.uint8, device=dev)
+            t["frame_dst"] = torch.zeros(1 << 15, dtype=torch.int64, device=dev)
+        ctxs.append(c)
+        ts.append(t)
+        packed.append((wire, off, streams))
+        bats.append(c.make_batch(t["wire"], t["seg_off"], None, t["st_out"], t["seg_out"], t["frames"], t["summ"],
+                                 compact=compact, arena=t.get("arena"), frame_dst=t.get("frame_dst")))
+    n_cu = torch.cuda.get_device_properties(0).multi_processor_count
+    ws = ctxs[0].stream_create(K.cu_mask(range(16), n_cu))
+    if layout == "bench":
+        us = [ctxs[0].stream_create(None)]
+    else:
+        us = [ctxs[0].stream_create(K.cu_mask(range(16, n_cu), n_cu)) for _ in range(2)]
+    with pytest.raises(K.WscError):
+        ctxs[0].decode_split(bats[0], ws, ws)
+    try:
+        for _ in range(3):
+            for t, (wire, _, _) in zip(ts, packed):
+                t["wire"].copy_(torch.from_numpy(wire))
+            torch.cuda.synchronize()
+            for j in range(2):
+                ctxs[j].decode_split(bats[j], ws, us[j % len(us)])
+            torch.cuda.synchronize()
+            for j, (wire, off, streams) in enumerate(packed):
+                t = ts[j]
+                summ = t["summ"].cpu().numpy().copy().view(K.SUMMARY_DTYPE)[0]
+                nf = int(summ["n_frames"])
+                res = K.DecodeResult(
+                    seg=t["seg_out"].cpu().numpy().copy().view(K.SEG_RESULT_DTYPE),
+                    state=t["st_out"].cpu().numpy().copy().view(K.CONN_STATE_DTYPE),
+                    frames=t["frames"].cpu().numpy().copy().view(K.FRAME_DTYPE)[:nf], summary=summ,
+                    frame_dst=t["frame_dst"].cpu().numpy().copy().view(np.uint64)[:nf] if compact else None,
+                    arena=t["arena"].cpu().numpy().copy() if compact else None)
+                after = t["wire"].cpu().numpy().copy()
+                if compact:
+                    assert np.array_equal(after, wire)
+                for i, s in enumerate(streams):
+                    compare_segment(i, s, int(off[i]), res, O.run(s), wire_after=after, compact=compact)
+    finally:
+        torch.cuda.synchronize()
+        for s in [ws] + us:
+            ctxs[0].stream_destroy(s)
+        for c in ctxs:
+            c.close()
