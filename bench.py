@@ -285,8 +285,12 @@ def main():
 
 def other_configs(torch, K, synth):
     """Device time of the full decode for the other single-GPU BASELINE.json configs (hipEvents,
-    median of 10), reported beside the headline; parity for each is in tests/test_gpu_parity.py."""
+    median of 10), reported beside the headline; parity for each is in tests/test_gpu_parity.py.
+    `pipelined_gib_s`: two batches in flight through the split pipeline, as the headline runs
+    (walk on a stream masked to max(16, walk blocks) CUs, at most half the chip; unmask over all
+    CUs), wall time of 20 steps after 5 warm-up steps."""
     dev = torch.device("cuda", torch.cuda.current_device())
+    n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
     res = {}
     cases = [("configs[1] 1M x 1 KiB BIN, 16 frames/segment", lambda: synth.uniform_batch(1 << 20, 1024, 16, seed=synth.SEED_BASE + 1), False),
              ("configs[2] 256k mixed 125 B / 64 KiB / 1 MiB (p~1/size)", lambda: synth.mixed_batch(), False),
@@ -300,16 +304,22 @@ def other_configs(torch, K, synth):
     for name, make, compact in cases:
         cfg = make()
         n = len(cfg["seg_off"]) - 1
-        c = K.Codec(dev.index, max_batch_bytes=len(cfg["wire"]) + 4096, max_segs=n, max_frames=cfg["n_frames"] + 16)
-        t = dict(wire=torch.from_numpy(cfg["wire"]).to(dev), seg_off=torch.from_numpy(cfg["seg_off"].view(np.int64)).to(dev),
-                 st=torch.zeros(n * 16, dtype=torch.uint8, device=dev), so=torch.zeros(n * 32, dtype=torch.uint8, device=dev),
-                 fr=torch.zeros((cfg["n_frames"] + 16) * 32, dtype=torch.uint8, device=dev),
-                 sm=torch.zeros(32, dtype=torch.uint8, device=dev))
-        if compact:
-            t["arena"] = torch.zeros(len(cfg["wire"]) + 64, dtype=torch.uint8, device=dev)
-            t["fd"] = torch.zeros(cfg["n_frames"] + 16, dtype=torch.int64, device=dev)
-        b = c.make_batch(t["wire"], t["seg_off"], None, t["st"], t["so"], t["fr"], t["sm"], compact=compact,
-                         arena=t.get("arena"), frame_dst=t.get("fd"))
+
+        def one():
+            c = K.Codec(dev.index, max_batch_bytes=len(cfg["wire"]) + 4096, max_segs=n, max_frames=cfg["n_frames"] + 16)
+            t = dict(wire=torch.from_numpy(cfg["wire"]).to(dev),
+                     seg_off=torch.from_numpy(cfg["seg_off"].view(np.int64)).to(dev),
+                     st=torch.zeros(n * 16, dtype=torch.uint8, device=dev), so=torch.zeros(n * 32, dtype=torch.uint8, device=dev),
+                     fr=torch.zeros((cfg["n_frames"] + 16) * 32, dtype=torch.uint8, device=dev),
+                     sm=torch.zeros(32, dtype=torch.uint8, device=dev))
+            if compact:
+                t["arena"] = torch.zeros(len(cfg["wire"]) + 64, dtype=torch.uint8, device=dev)
+                t["fd"] = torch.zeros(cfg["n_frames"] + 16, dtype=torch.int64, device=dev)
+            b = c.make_batch(t["wire"], t["seg_off"], None, t["st"], t["so"], t["fr"], t["sm"], compact=compact,
+                             arena=t.get("arena"), frame_dst=t.get("fd"))
+            return c, t, b
+
+        c, t, b = one()
         c.decode(b)
         torch.cuda.synchronize()
         p = [c.profile(b, 1) for _ in range(10)]
@@ -317,11 +327,31 @@ def other_configs(torch, K, synth):
         um = float(np.median([q["unmask"] for q in p]))
         hdr = np.where(cfg["plen"] <= 125, 6, np.where(cfg["plen"] <= 65535, 8, 14))
         alg = int((2 * cfg["plen"].astype(np.int64) + hdr + 32).sum())
+        # two batches in flight through the split pipeline
+        torch.cuda.synchronize()
+        c2, t2, b2 = one()
+        wcus = min(n_cu // 2, max(16, (n + 255) // 256))
+        ws = c.stream_create(K.cu_mask(range(wcus), n_cu))
+        us = c.stream_create(None)
+        pair = [(c, b), (c2, b2)]
+        for i in range(5):
+            pair[i % 2][0].decode_split(pair[i % 2][1], ws, us)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(20):
+            pair[i % 2][0].decode_split(pair[i % 2][1], ws, us)
+        torch.cuda.synchronize()
+        pms = (time.perf_counter() - t0) / 20 * 1e3
+        c.stream_destroy(ws)
+        c.stream_destroy(us)
         res[name] = {"gib_s": round(cfg["payload_bytes"] / (tot * 1e-3) / 2**30, 1), "ms": round(tot, 4),
                      "unmask_ms": round(um, 4), "unmask_gb_s": round(alg / (um * 1e-3) / 1e9, 1),
+                     "pipelined_gib_s": round(cfg["payload_bytes"] / (pms * 1e-3) / 2**30, 1),
+                     "pipelined_ms_per_batch": round(pms, 4), "pipelined_walk_cus": wcus,
                      "frames": int(cfg["n_frames"]), "payload_bytes": int(cfg["payload_bytes"])}
         c.close()
-        del t
+        c2.close()
+        del t, t2
         torch.cuda.empty_cache()
     return res
 

@@ -361,19 +361,30 @@ def test_session_undrained_events_survive_next_decode(codec_lib):
 
 
 # ---- split pipeline (wsc_decode_split): walk on a CU-masked stream, unmask on others ----------
-@pytest.mark.parametrize("compact,layout", [(False, "bench"), (True, "bench"), (False, "rest2"), (True, "rest2")])
-def test_decode_split_pipeline_matches_oracle(codec_lib, compact, layout):
+@pytest.mark.parametrize("compact,layout,inline_max", [(False, "bench", 256), (True, "bench", 256), (False, "rest2", 256),
+                                                     (True, "rest2", 256), (False, "bench", 0), (True, "rest2", 0)])
+def test_decode_split_pipeline_matches_oracle(codec_lib, compact, layout, inline_max):
     """two contexts in flight, walk stream on 16 CUs; the unmasks on one stream over every CU (the
     bench's pipeline) or on one stream per context over the other CUs; every round re-arms the
     wires and decodes both batches back to back, so one batch's walk runs beside the other's
-    unmask; each is compared with the oracle"""
+    unmask; each is compared with the oracle.  inline_max 0 sends every text check to the
+    chip-wide UTF-8 kernel (which runs on the unmask stream)"""
+    import os
     torch = pytest.importorskip("torch")
     dev = torch.device("cuda:0")
     sets = [[random_stream(7000 + 400 * j + i, n_units=10) for i in range(300)] for j in range(2)]
     ctxs, bats, ts, packed = [], [], [], []
     for streams in sets:
         wire, off = pack_streams(streams)
-        c = K.Codec(0, max_batch_bytes=len(wire) + 4096, max_segs=len(streams), max_frames=1 << 15)
+        old = os.environ.get("WSC_U8_INLINE_MAX")
+        os.environ["WSC_U8_INLINE_MAX"] = str(inline_max)
+        try:
+            c = K.Codec(0, max_batch_bytes=len(wire) + 4096, max_segs=len(streams), max_frames=1 << 15)
+        finally:
+            if old is None:
+                del os.environ["WSC_U8_INLINE_MAX"]
+            else:
+                os.environ["WSC_U8_INLINE_MAX"] = old
         n = len(streams)
         t = dict(wire=torch.from_numpy(wire.copy()).to(dev), seg_off=torch.from_numpy(off.view(np.int64)).to(dev),
                  st_out=torch.zeros(n * 16, dtype=torch.uint8, device=dev),
