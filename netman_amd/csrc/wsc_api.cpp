@@ -317,7 +317,7 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     ua.seg_out = b->seg_out;
     ua.state_out = b->state_out;
     ua.summary = b->summary;
-    hipLaunchKernelGGL(k_u8_check, dim3((uint32_t)c->n_cu * 5), dim3(256), 0, st, ua);   // resident: 5 waves/SIMD (92 VGPRs)
+    hipLaunchKernelGGL(k_u8_check, dim3((uint32_t)c->n_cu * 5), dim3(256), 0, st, ua);   // resident: 5 waves/SIMD (96 VGPRs)
     HIP_TRY(hipGetLastError());
     rec(2);
     rec(3);

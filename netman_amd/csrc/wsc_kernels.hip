@@ -788,11 +788,11 @@ __device__ __forceinline__ uint32_t u8m_get(uint64_t m, uint32_t st) {   // st: 
 
 // Publish one item's map; the segment's last item composes the segment's items in frame order
 // with the walk's states and applies the verdict (one lane).
-__device__ __forceinline__ void u8_finish(const U8Args& a, uint32_t it, const U8Item& item, uint64_t acc) {
+__device__ __forceinline__ void u8_finish(const U8Args& a, uint32_t it, uint32_t seg, uint64_t acc) {
     __hip_atomic_store(a.maps + it, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const uint32_t done = __hip_atomic_fetch_add(&a.seg[item.seg].done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
-    const U8Seg g = a.seg[item.seg];
+    const uint32_t done = __hip_atomic_fetch_add(&a.seg[seg].done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+    const U8Seg g = a.seg[seg];
     if (done != g.n) return;
     // the segment's last item: compose its items in frame order with the walk's states
     uint32_t cur = 0, start = 0, fail = 0xFFFFFFFFu;   // states 0..7, 0xFF = reject
@@ -817,7 +817,7 @@ __device__ __forceinline__ void u8_finish(const U8Args& a, uint32_t it, const U8
         }
         j = x.next;
     }
-    const uint32_t s = item.seg;
+    const uint32_t s = seg;
     if (fail == 0xFFFFFFFFu) {
         if (g.pending_end && a.state_out[s].cont_len) a.state_out[s].cont_utf8 = (uint8_t)(cur > 7 ? 8u : cur);
         return;
@@ -839,6 +839,7 @@ __device__ __forceinline__ void u8_finish(const U8Args& a, uint32_t it, const U8
         if (a.spans[g.sbase + k].src >= fend) a.spans[g.sbase + k].key = 0;
 }
 
+// 5 waves per SIMD (96 VGPRs, a few spilled): 4 waves without spills measured 8-30 % slower
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_u8_check(U8Args a) {
     const uint32_t n_items = *a.count;
     if (blockIdx.x * 4 >= n_items) return;   // nothing deferred (the common, binary case)
@@ -856,7 +857,84 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
     const uint32_t nw = gridDim.x * 4;
-    // 4 KiB of item.src + b0 into q (bytes past the item read as 0)
+    // The map of one lane's 16-byte piece (nk valid bytes, masked with `mask`); plain = no
+    // non-ASCII byte among them.
+    auto piece_map = [&](const uint4 v, uint32_t mask, uint32_t nk, bool& plain) -> uint64_t {
+        uint32_t d[4] = {0, 0, 0, 0};
+        if (nk) { d[0] = v.x ^ mask; d[1] = v.y ^ mask; d[2] = v.z ^ mask; d[3] = v.w ^ mask; }
+        uint32_t hib = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t lim = nk > 4u * j ? (nk - 4u * j >= 4 ? 4u : nk - 4u * j) : 0u;
+            const uint32_t keep = lim >= 4 ? 0xFFFFFFFFu : ((1u << (8 * lim)) - 1u);
+            hib |= d[j] & keep & 0x80808080u;
+        }
+        plain = true;
+        if (nk == 0) return u8m_id();
+        if (hib == 0) return u8m_ascii();
+        plain = false;
+        if (nk == 16) {
+            // Every entry state that survives the first 4 bytes is in ONE state X there: a survivor
+            // must be in state 0 just before the first lead byte (a lead in a non-zero state
+            // rejects), and 4 continuation bytes reject every state (at most 3 are owed).  So the
+            // first 4 bytes compose full maps (2 v_perm per byte), the other 12 step the single
+            // state X (1 v_perm per byte), and the piece's map is the prefix map with every
+            // surviving entry sent to the final state.
+            uint32_t lo = 0x03020100u, hi = 0x07060504u;
+#pragma unroll
+            for (uint32_t i = 0; i < 4; ++i) {
+                const uint64_t t = tab[(d[0] >> (8 * i)) & 0xFFu];
+                const uint32_t tl = (uint32_t)t, th = (uint32_t)(t >> 32);
+                lo = (uint32_t)__builtin_amdgcn_perm(th, tl, lo);
+                hi = (uint32_t)__builtin_amdgcn_perm(th, tl, hi);
+            }
+            uint32_t x = lo & hi;             // non-rejected bytes all equal X, rejects are 0xFF
+            x &= x >> 16;
+            x &= x >> 8;
+#pragma unroll
+            for (uint32_t i = 4; i < 16; ++i) {
+                const uint64_t t = tab[(d[i >> 2] >> (8 * (i & 3))) & 0xFFu];
+                x = (uint32_t)__builtin_amdgcn_perm((uint32_t)(t >> 32), (uint32_t)t, x);   // byte 0 = T[b][X]
+            }
+            const uint32_t fr = (x & 0xFFu) * 0x01010101u;
+            lo = (uint32_t)__builtin_amdgcn_perm(fr, fr, lo);   // 0..7 -> final state, 0xFF stays
+            hi = (uint32_t)__builtin_amdgcn_perm(fr, fr, hi);
+            return (uint64_t)hi << 32 | lo;
+        }
+        uint32_t lo = 0x03020100u, hi = 0x07060504u;
+#pragma unroll
+        for (uint32_t i = 0; i < 16; ++i) {
+            if (i < nk) {
+                const uint64_t t = tab[(d[i >> 2] >> (8 * (i & 3))) & 0xFFu];
+                const uint32_t tl = (uint32_t)t, th = (uint32_t)(t >> 32);
+                lo = (uint32_t)__builtin_amdgcn_perm(th, tl, lo);
+                hi = (uint32_t)__builtin_amdgcn_perm(th, tl, hi);
+            }
+        }
+        return (uint64_t)hi << 32 | lo;
+    };
+    // The map of one 1 KiB wave piece (the 64 lanes' maps in lane order), wave-uniform.
+    auto wave_map = [&](uint64_t pm, bool plain) -> uint64_t {
+        if (__ballot(!plain) == 0)            // ASCII (or empty) everywhere: one constant map
+            return __ballot(pm == u8m_ascii()) ? u8m_ascii() : u8m_id();
+        // compose the 16 lanes of each row in order with DPP row shifts (VALU, no LDS crossbar:
+        // the table reads already keep the LDS pipe busy), then the 4 rows
+        uint32_t mlo = (uint32_t)pm, mhi = (uint32_t)(pm >> 32);
+        u8m_row_level<1>(mlo, mhi, lane);
+        u8m_row_level<2>(mlo, mhi, lane);
+        u8m_row_level<4>(mlo, mhi, lane);
+        u8m_row_level<8>(mlo, mhi, lane);
+        uint64_t m = u8m_id();
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            // readlane returns int: widen through uint32_t (no sign extension into the high word)
+            const uint32_t rlo = (uint32_t)__builtin_amdgcn_readlane(mlo, 16 * r);
+            const uint32_t rhi = (uint32_t)__builtin_amdgcn_readlane(mhi, 16 * r);
+            m = u8m_then(m, (uint64_t)rhi << 32 | rlo);
+        }
+        return m;
+    };
+    // 4 KiB of x.src + b0 into q (bytes past the item read as 0)
     auto fetch = [&](const U8Item& x, uint32_t b0, uint4 (&q)[4]) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -864,119 +942,86 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
             q[k] = off < x.len ? load16_unaligned(a.wire, (int64_t)(x.src + off), a.n_bytes) : make_uint4(0, 0, 0, 0);
         }
     };
-    if (gw >= n_items) return;
-    uint32_t it = gw;
-    U8Item item = a.items[it];
-    // the next 4 KiB step's loads are issued before the current step is folded, across items too
-    // (the next item's first step is fetched under the current item's last step)
-    uint4 nxt[4];
-    fetch(item, 0, nxt);
-    while (it < n_items) {
-        const uint32_t it2 = it + nw;
-        U8Item item2 = item;
-        if (it2 < n_items) item2 = a.items[it2];
-        uint64_t acc = u8m_id();
-        if (item.len == 0 && it2 < n_items) fetch(item2, 0, nxt);
-        for (uint32_t b0 = 0; b0 < item.len; b0 += 4096) {
-            uint4 cur4[4];
+    // A unit is 4 consecutive items.  Units of small items (<= 1 KiB each: 1 KiB text frames) take
+    // one step: piece k is item k's first KiB, and lanes 0..3 publish the 4 items' maps at once
+    // (a 1 KiB item alone would leave 3/4 of the step's loads idle and serialise the per-item
+    // hand-off).  Other units walk their items' 4 KiB steps in order, the next step's loads -- the
+    // next item's first step too -- issued before the current step is folded.
+    const uint32_t n_units = (n_items + 3) / 4;
+    for (uint32_t u = gw; u < n_units; u += nw) {
+        const uint32_t i0 = 4 * u;
+        const uint32_t cnt = n_items - i0 < 4 ? n_items - i0 : 4u;
+        U8Item x[4];
+        bool small = true;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) cur4[k] = nxt[k];
-            if (b0 + 4096 < item.len) fetch(item, b0 + 4096, nxt);
-            else if (it2 < n_items) fetch(item2, 0, nxt);
-            uint64_t pm[4];
-            bool plain = true;
+        for (uint32_t j = 0; j < 4; ++j) {
+            if (j < cnt) {
+                x[j] = a.items[i0 + j];
+                small = small && x[j].len <= 1024;
+            } else {
+                x[j] = x[0];
+                x[j].len = 0;
+            }
+        }
+        if (small) {
+            uint4 q[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                q[k] = lane * 16 < x[k].len ? load16_unaligned(a.wire, (int64_t)(x[k].src + lane * 16), a.n_bytes)
+                                            : make_uint4(0, 0, 0, 0);
+            uint64_t mine = u8m_id();
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                const uint32_t off = b0 + k * 1024 + lane * 16;
-                const uint32_t nk = off < item.len ? (item.len - off >= 16 ? 16u : item.len - off) : 0u;
-                uint32_t d[4] = {0, 0, 0, 0};
-                if (nk) {
-                    const uint4 v = cur4[k];
-                    d[0] = v.x ^ item.mask; d[1] = v.y ^ item.mask; d[2] = v.z ^ item.mask; d[3] = v.w ^ item.mask;
-                }
-                uint32_t hib = 0;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const uint32_t lim = nk > 4u * j ? (nk - 4u * j >= 4 ? 4u : nk - 4u * j) : 0u;
-                    const uint32_t keep = lim >= 4 ? 0xFFFFFFFFu : ((1u << (8 * lim)) - 1u);
-                    hib |= d[j] & keep & 0x80808080u;
-                }
-                if (nk == 0) {
-                    pm[k] = u8m_id();
-                } else if (hib == 0) {
-                    pm[k] = u8m_ascii();
-                } else if (nk == 16) {
-                    // Every entry state that survives the first 4 bytes is in ONE state X there:
-                    // a survivor must be in state 0 just before the first lead byte (a lead in a
-                    // non-zero state rejects), and 4 continuation bytes reject every state (at most
-                    // 3 are owed).  So the first 4 bytes compose full maps (2 v_perm per byte), the
-                    // other 12 step the single state X (1 v_perm per byte), and the piece's map is the
-                    // prefix map with every surviving entry sent to the final state.
-                    uint32_t lo = 0x03020100u, hi = 0x07060504u;
-#pragma unroll
-                    for (uint32_t i = 0; i < 4; ++i) {
-                        const uint64_t t = tab[(d[0] >> (8 * i)) & 0xFFu];
-                        const uint32_t tl = (uint32_t)t, th = (uint32_t)(t >> 32);
-                        lo = (uint32_t)__builtin_amdgcn_perm(th, tl, lo);
-                        hi = (uint32_t)__builtin_amdgcn_perm(th, tl, hi);
-                    }
-                    uint32_t x = lo & hi;             // non-rejected bytes all equal X, rejects are 0xFF
-                    x &= x >> 16;
-                    x &= x >> 8;
-#pragma unroll
-                    for (uint32_t i = 4; i < 16; ++i) {
-                        const uint64_t t = tab[(d[i >> 2] >> (8 * (i & 3))) & 0xFFu];
-                        x = (uint32_t)__builtin_amdgcn_perm((uint32_t)(t >> 32), (uint32_t)t, x);   // byte 0 = T[b][X]
-                    }
-                    const uint32_t fr = (x & 0xFFu) * 0x01010101u;
-                    lo = (uint32_t)__builtin_amdgcn_perm(fr, fr, lo);   // 0..7 -> final state, 0xFF stays
-                    hi = (uint32_t)__builtin_amdgcn_perm(fr, fr, hi);
-                    pm[k] = (uint64_t)hi << 32 | lo;
-                    plain = false;
-                } else {
-                    uint32_t lo = 0x03020100u, hi = 0x07060504u;
-#pragma unroll
-                    for (uint32_t i = 0; i < 16; ++i) {
-                        if (i < nk) {
-                            const uint64_t t = tab[(d[i >> 2] >> (8 * (i & 3))) & 0xFFu];
-                            const uint32_t tl = (uint32_t)t, th = (uint32_t)(t >> 32);
-                            lo = (uint32_t)__builtin_amdgcn_perm(th, tl, lo);
-                            hi = (uint32_t)__builtin_amdgcn_perm(th, tl, hi);
-                        }
-                    }
-                    pm[k] = (uint64_t)hi << 32 | lo;
-                    plain = false;
-                }
+                const uint32_t off = lane * 16;
+                const uint32_t nk = off < x[k].len ? (x[k].len - off >= 16 ? 16u : x[k].len - off) : 0u;
+                bool plain;
+                const uint64_t pm = piece_map(q[k], x[k].mask, nk, plain);
+                const uint64_t m = wave_map(pm, plain);
+                if (lane == (uint32_t)k) mine = m;
             }
-            uint64_t stepm;
-            if (__ballot(!plain) == 0) {          // ASCII (or empty) everywhere: one constant map
-                stepm = __ballot(pm[0] == u8m_ascii()) ? u8m_ascii() : u8m_id();
-            } else {
-                stepm = u8m_id();
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {     // lanes in order, then pieces in order
-                    if (b0 + k * 1024 >= item.len) break;   // the rest of the step is past the item
-                    // compose the 16 lanes of each row in order with DPP row shifts (VALU, no LDS
-                    // crossbar: the table reads already keep the LDS pipe busy), then the 4 rows
-                    uint32_t mlo = (uint32_t)pm[k], mhi = (uint32_t)(pm[k] >> 32);
-                    u8m_row_level<1>(mlo, mhi, lane);
-                    u8m_row_level<2>(mlo, mhi, lane);
-                    u8m_row_level<4>(mlo, mhi, lane);
-                    u8m_row_level<8>(mlo, mhi, lane);
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        // readlane returns int: widen through uint32_t (no sign extension into the high word)
-                        const uint32_t rlo = (uint32_t)__builtin_amdgcn_readlane(mlo, 16 * r);
-                        const uint32_t rhi = (uint32_t)__builtin_amdgcn_readlane(mhi, 16 * r);
-                        stepm = u8m_then(stepm, (uint64_t)rhi << 32 | rlo);
-                    }
-                }
-            }
-            acc = u8m_then(acc, stepm);
+            const uint32_t seg = lane == 0 ? x[0].seg : lane == 1 ? x[1].seg : lane == 2 ? x[2].seg : x[3].seg;
+            if (lane < cnt) u8_finish(a, i0 + lane, seg, mine);
+            continue;
         }
-        if (lane == 0) u8_finish(a, it, item, acc);
-        it = it2;
-        item = item2;
+        uint4 nxt[4];
+        fetch(x[0], 0, nxt);
+        U8Item item2 = x[0];   // (items re-read by index: no dynamically indexed register array)
+        for (uint32_t j = 0; j < cnt; ++j) {
+            const U8Item item = item2;
+            if (j + 1 < cnt) item2 = a.items[i0 + j + 1];
+            uint64_t acc = u8m_id();
+            if (item.len == 0 && j + 1 < cnt) fetch(item2, 0, nxt);
+            for (uint32_t b0 = 0; b0 < item.len; b0 += 4096) {
+                uint4 cur4[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) cur4[k] = nxt[k];
+                if (b0 + 4096 < item.len) fetch(item, b0 + 4096, nxt);
+                else if (j + 1 < cnt) fetch(item2, 0, nxt);
+                uint64_t pm[4];
+                bool plain = true;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t off = b0 + k * 1024 + lane * 16;
+                    const uint32_t nk = off < item.len ? (item.len - off >= 16 ? 16u : item.len - off) : 0u;
+                    bool pl;
+                    pm[k] = piece_map(cur4[k], item.mask, nk, pl);
+                    plain = plain && pl;
+                }
+                uint64_t stepm;
+                if (__ballot(!plain) == 0) {      // ASCII (or empty) everywhere: one constant map
+                    stepm = __ballot(pm[0] == u8m_ascii()) ? u8m_ascii() : u8m_id();
+                } else {
+                    stepm = u8m_id();
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {     // pieces in order
+                        if (b0 + k * 1024 >= item.len) break;   // the rest of the step is past the item
+                        stepm = u8m_then(stepm, wave_map(pm[k], false));
+                    }
+                }
+                acc = u8m_then(acc, stepm);
+            }
+            if (lane == 0) u8_finish(a, i0 + j, item.seg, acc);
+        }
     }
 }
 
