@@ -293,7 +293,9 @@ def other_configs(torch, K, synth):
     n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
     res = {}
     cases = [("configs[1] 1M x 1 KiB BIN, 16 frames/segment", lambda: synth.uniform_batch(1 << 20, 1024, 16, seed=synth.SEED_BASE + 1), False),
+             ("configs[1] 1M x 1 KiB BIN, 1 frame/segment", lambda: synth.uniform_batch(1 << 20, 1024, 1, seed=synth.SEED_BASE + 1), False),
              ("configs[2] 256k mixed 125 B / 64 KiB / 1 MiB (p~1/size)", lambda: synth.mixed_batch(), False),
+             ("configs[2] 256k mixed, 1 frame/segment", lambda: synth.mixed_batch(frames_per_seg=1), False),
              ("configs[3] one GPU's shard: 1M x 4 KiB BIN, 16 frames/segment",
               lambda: synth.uniform_batch(1 << 20, 4096, 16, seed=synth.SEED_BASE + 3), False),
              ("configs[4] 64k connections x fragmented message, reassembled (COMPACT)", lambda: synth.fragmented_batch(), True),

@@ -232,10 +232,11 @@ def _device_batch(c, cfg, torch, compact=False):
     return b, t
 
 
-def test_config1_1m_x_1k_frames(codec_lib):
+@pytest.mark.parametrize("per_seg", [16, 1])   # 64 k connections x 16 frames, and 1 frame per segment
+def test_config1_1m_x_1k_frames(codec_lib, per_seg):
     torch = pytest.importorskip("torch")
-    cfg = synth.uniform_batch(1 << 20, 1024, 16, seed=synth.SEED_BASE + 1)
-    c = K.Codec(0, max_batch_bytes=len(cfg["wire"]) + 4096, max_segs=1 << 16, max_frames=(1 << 20) + 16)
+    cfg = synth.uniform_batch(1 << 20, 1024, per_seg, seed=synth.SEED_BASE + 1)
+    c = K.Codec(0, max_batch_bytes=len(cfg["wire"]) + 4096, max_segs=(1 << 20) // per_seg, max_frames=(1 << 20) + 16)
     b, t = _device_batch(c, cfg, torch)
     c.decode(b)
     c.sync()
@@ -245,10 +246,11 @@ def test_config1_1m_x_1k_frames(codec_lib):
     c.close()
 
 
-def test_config2_mixed_power_law(codec_lib):
+@pytest.mark.parametrize("per_seg", [16, 1])
+def test_config2_mixed_power_law(codec_lib, per_seg):
     torch = pytest.importorskip("torch")
-    cfg = synth.mixed_batch()
-    c = K.Codec(0, max_batch_bytes=len(cfg["wire"]) + 4096, max_segs=1 << 15, max_frames=cfg["n_frames"] + 16)
+    cfg = synth.mixed_batch(frames_per_seg=per_seg)
+    c = K.Codec(0, max_batch_bytes=len(cfg["wire"]) + 4096, max_segs=len(cfg["seg_off"]) - 1, max_frames=cfg["n_frames"] + 16)
     b, t = _device_batch(c, cfg, torch)
     c.decode(b)
     c.sync()
