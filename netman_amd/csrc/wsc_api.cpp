@@ -11,7 +11,7 @@
 #include "wsc_kernels.hpp"
 
 namespace wsc {
-template <bool COMPACT> __global__ void k_walk_fused(WalkArgs);
+template <bool COMPACT, uint32_t KR> __global__ void k_walk_fused(WalkArgs);
 __global__ void k_u8_check(U8Args);
 template <bool COMPACT, int P, int NT, int MINW>
 __global__ void k_unmask(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*,
@@ -65,6 +65,7 @@ struct wsc_ctx {
     uint32_t u8items_cap = 0;
     U8Seg* u8seg = nullptr;
     uint32_t u8_inline_max = 256;
+    int walk_krec = 0;                  // WSC_WALK_KREC: 16 or 4 pins that walk instance (A/B, tests); 0 = auto
     uint64_t tile_entries = 0;
     // host-staged path buffers (lazily allocated)
     uint8_t* d_wire = nullptr;
@@ -179,6 +180,8 @@ int wsc_create(int device, const wsc_config* cfg_in, wsc_ctx** out) {
     chk(hipMalloc(&c->u8items, (uint64_t)c->u8items_cap * sizeof(U8Item)), "hipMalloc u8items");
     chk(hipMalloc(&c->u8maps, (uint64_t)c->u8items_cap * sizeof(uint64_t)), "hipMalloc u8maps");
     chk(hipMalloc(&c->u8seg, (uint64_t)cfg.max_segs * sizeof(U8Seg)), "hipMalloc u8seg");
+    if (const char* e = std::getenv("WSC_WALK_KREC"); e && *e)
+        c->walk_krec = std::atoi(e) == 4 ? 4 : 16;
     if (const char* e = std::getenv("WSC_U8_INLINE_MAX"); e && *e)   // test knob: 0 sends all text chip-wide
         c->u8_inline_max = (uint32_t)std::strtoul(e, nullptr, 10);
     c->enc_blocks = (cfg.max_frames + 255) / 256 + 1;
@@ -295,8 +298,15 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     // (an event never recorded is a no-op wait)
     const hipStream_t ws = split ? sw : st;
     if (split) HIP_TRY(hipStreamWaitEvent(ws, c->ev_done, 0));
-    if (compact) hipLaunchKernelGGL((k_walk_fused<true>), wgrid, wblk, 0, ws, wa);
-    else hipLaunchKernelGGL((k_walk_fused<false>), wgrid, wblk, 0, ws, wa);
+    // more walk blocks than 2 per CU (the KR = 16 instance's LDS residency): the KR = 4 instance
+    const bool short_segs = c->walk_krec ? c->walk_krec == 4 : wgrid.x > 2u * (uint32_t)c->n_cu;
+    if (compact) {
+        if (short_segs) hipLaunchKernelGGL((k_walk_fused<true, 4>), wgrid, wblk, 0, ws, wa);
+        else hipLaunchKernelGGL((k_walk_fused<true, 16>), wgrid, wblk, 0, ws, wa);
+    } else {
+        if (short_segs) hipLaunchKernelGGL((k_walk_fused<false, 4>), wgrid, wblk, 0, ws, wa);
+        else hipLaunchKernelGGL((k_walk_fused<false, 16>), wgrid, wblk, 0, ws, wa);
+    }
     HIP_TRY(hipGetLastError());
     if (split) {
         HIP_TRY(hipEventRecord(c->ev_walked, ws));

@@ -270,7 +270,7 @@ __device__ __forceinline__ void emit_replay(const WalkArgs& a, uint32_t s, uint6
 // one round trip per SPEC_D frames.  All loads of a round are waited together.
 constexpr int SPEC_D = 4;
 
-template <bool EMIT, bool COMPACT>
+template <bool EMIT, bool COMPACT, uint32_t KR = KREC>
 __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, const SegCount& base,
                                                  const SegCount& own, uint4* lrec, WalkEnd* wend) {
     const uint8_t* __restrict__ w = a.wire;
@@ -500,7 +500,7 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
 
         if constexpr (EMIT) {
             emit_frame<COMPACT>(a, e, fr, (uint32_t)plen, have_span, region);
-        } else if (lrec && nf < KREC) {
+        } else if (lrec && nf < KR) {
             const bool inc = fr.kind == WSC_FK_MESSAGE || fr.kind == WSC_FK_PING || fr.kind == WSC_FK_PONG;
             lrec[nf * 256] = rec_pack(fr, seg_start, have_span, region, inc);
         }
@@ -611,12 +611,16 @@ __device__ __forceinline__ SegCount lb_load(uint64_t* p) {
     return v;
 }
 
-template <bool COMPACT>
+// KR: frame records kept in LDS per lane for the emit replay (segments with more frames walk
+// their chain a second time).  KR = 16 is 64 KiB of LDS per block = 2 resident blocks per CU;
+// batches of many short segments launch the KR = 4 instance (4 blocks per CU, VGPR-bound) so that
+// twice as many blocks of the ticketed look-back run at once.
+template <bool COMPACT, uint32_t KR>
 __global__ __launch_bounds__(256) void k_walk_fused(WalkArgs a) {
     __shared__ uint32_t sh_bid;
     __shared__ SegCount sh_wave[4];
     __shared__ SegCount sh_prefix;
-    __shared__ uint4 sh_rec[KREC * 256];   // [frame ordinal][lane]: conflict-free 16 B per lane
+    __shared__ uint4 sh_rec[KR * 256];   // [frame ordinal][lane]: conflict-free 16 B per lane
     if (threadIdx.x == 0)
         sh_bid = __hip_atomic_fetch_add(a.lb_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
@@ -632,7 +636,7 @@ __global__ __launch_bounds__(256) void k_walk_fused(WalkArgs a) {
     WalkEnd wend = {};
     uint32_t msg0 = 0;
     if (s < a.n_segs) {
-        own = walk_segment<false, COMPACT>(a, s, zero, zero, sh_rec + threadIdx.x, &wend);
+        own = walk_segment<false, COMPACT, KR>(a, s, zero, zero, sh_rec + threadIdx.x, &wend);
         a.counts[s] = own;
         msg0 = a.state_in ? a.state_in[s].msg_id : 0u;
     }
@@ -718,7 +722,7 @@ __global__ __launch_bounds__(256) void k_walk_fused(WalkArgs a) {
         a.u8seg[s].fbase = base.frames;
     }
     if (s < a.n_segs) {
-        if (own.frames <= KREC)   // replay from LDS: no second dependent walk, no loads at all
+        if (own.frames <= KR)   // replay from LDS: no second dependent walk, no loads at all
             emit_replay<COMPACT>(a, s, a.seg_off[s], a.seg_off[s + 1], base, own, sh_rec + threadIdx.x, msg0, wend);
         else                      // long segment: re-walk the (cache-warm) headers
             walk_segment<true, COMPACT>(a, s, base, own, nullptr, nullptr);
@@ -1026,7 +1030,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
 }
 
 // explicit instantiations used by the host code
-template __global__ void k_walk_fused<false>(WalkArgs);
-template __global__ void k_walk_fused<true>(WalkArgs);
+template __global__ void k_walk_fused<false, KREC>(WalkArgs);
+template __global__ void k_walk_fused<true, KREC>(WalkArgs);
+template __global__ void k_walk_fused<false, 4>(WalkArgs);
+template __global__ void k_walk_fused<true, 4>(WalkArgs);
 
 }  // namespace wsc

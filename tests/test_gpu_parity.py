@@ -61,6 +61,21 @@ def test_fuzz_single_batch(codec, compact):
     _check_batch(codec, streams, compact=compact)
 
 
+@pytest.mark.parametrize("compact", [False, True])
+def test_fuzz_walk_4_records(codec_lib, monkeypatch, compact):
+    """The walk instance batches of many short segments launch (4 LDS frame records per lane, the
+    rest re-walked by the emit pass), forced on fuzz streams of 5..44 units with text and errors."""
+    monkeypatch.setenv("WSC_WALK_KREC", "4")
+    c = K.Codec(0, max_batch_bytes=64 << 20, max_segs=1 << 14, max_frames=1 << 18)
+    try:
+        streams = [random_stream(7000 + i, n_units=int(5 + i % 40), text_p=0.5) for i in range(400)]
+        _check_batch(c, streams, compact=compact)
+        streams = [random_stream(7500 + i, n_units=int(1 + i % 6)) for i in range(300)]
+        _check_batch(c, streams, compact=compact)
+    finally:
+        c.close()
+
+
 def test_fuzz_text_heavy(codec):
     streams = [random_stream(5000 + i, n_units=30, text_p=0.9, err_p=0.02) for i in range(300)]
     _check_batch(codec, streams)

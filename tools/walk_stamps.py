@@ -11,7 +11,9 @@ from netman_amd import codec as K, synth
 wl = sys.argv[1] if len(sys.argv) > 1 else "64k"
 cfg = {"64k": lambda: synth.uniform_batch(16384, 65536, 4, seed=synth.SEED_BASE + 1),
        "1k": lambda: synth.uniform_batch(1 << 20, 1024, 16, seed=synth.SEED_BASE + 1),
+       "1k1": lambda: synth.uniform_batch(1 << 20, 1024, 1, seed=synth.SEED_BASE + 1),
        "mixed": lambda: synth.mixed_batch(),
+       "mixed1": lambda: synth.mixed_batch(frames_per_seg=1),
        "frag": lambda: synth.fragmented_batch()}[wl]()
 compact = wl == "frag"
 dev = torch.device("cuda:0")
