@@ -447,10 +447,17 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
             sflags |= SEGF_UTF8;
             if constexpr (!EMIT) {
                 const bool part = (fr.flags & WSC_FF_U8_PART) != 0, chain = (fr.flags & WSC_FF_U8_CHAIN) != 0;
-                uint64_t src = pos + fr.hdr_len, n = plen;
-                uint32_t mk = fr.mask;
-                if (fr.flags & WSC_FF_U8_REASON) { src += 2; n -= 2; mk = rotr32(mk, 16); }   // payload[2:]
-                if (n > a.u8_inline_max || ((part || chain) && u8_pending)) {
+                const uint64_t src = pos + fr.hdr_len, n = plen;
+                const uint32_t mk = fr.mask;
+                if (fr.flags & WSC_FF_U8_REASON) {
+                    // CLOSE reason, websocket.go:153-172 (<= 125 B: always checked here).  Under
+                    // messageMode == TEXT nextFrame first runs utf8.Valid over the whole payload
+                    // (websocket_frame.go:71-73); if that fails the error is swallowed (:156) and
+                    // the stand-in reason has DataLen = fragmentLength, already zeroed by reset()
+                    // (frame.go:49), so payload[2:] is NOT checked -- only the code is.
+                    const bool skip = fr.mode == 1 && u8_run_masked(0, w, src, n, mk) != 0;
+                    if (!skip && u8_run_masked(0, w, src + 2, n - 2, rotr32(mk, 16)) != 0) u8fail = nf;
+                } else if (n > a.u8_inline_max || ((part || chain) && u8_pending)) {
                     // large text (or a chain already deferred): validated chip-wide by k_u8_check,
                     // which also applies the verdict; the walk goes on as if it were valid
                     const uint8_t kind = part ? U8K_PART : (chain ? U8K_CHAIN : U8K_SELF);

@@ -386,9 +386,14 @@ static int decode_packet(run_t* r) {
                 }
                 break;
             }
-            /* reason = returned message, or packetBuffer when utf8 failed (:160-167) */
+            /* reason = the returned message, or -- when nextFrame's whole-payload utf8.Valid failed
+             * under messageMode==TEXT (websocket_frame.go:71-73, error swallowed at :156) -- a
+             * stand-in Message{DataLen: uint32(c.fragmentLength), Data: packetBuffer} (:160-167).
+             * nextFrame's reset() (websocket_frame.go:49 -> websocket.go:309) has already zeroed
+             * fragmentLength, so that stand-in has Len() == 0: the reason check below is skipped
+             * and only the code (Data[:2], still the close payload) is verified. */
             const uint8_t* rp = m.has ? m.data : c->packetBuffer.p;
-            uint64_t rn = m.has ? m.len : c->packetBuffer.n;
+            uint64_t rn = m.has ? m.len : c->fragmentLength;
             if (rn > 2 && !wso_utf8_valid(rp + 2, rn - 2)) { err = WSO_ERR_MUST_UTF8; break; }   /* :170-172 */
             uint16_t code = (uint16_t)((rp[0] << 8) | rp[1]);                                   /* :175-176 */
             err = verify_close_code(code);

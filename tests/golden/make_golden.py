@@ -67,6 +67,55 @@ def kat():
         dict(name="fragmented_ping", hex=frame(9, b"p", fin=False, mask=3).hex(), expect=dict(events=[["CLOSE", 1002, 4]])),
         dict(name="continuation_without_start", hex=frame(0, b"p", mask=3).hex(), expect=dict(events=[["CLOSE", 1002, 1]])),
     ]
+    # Reference quirks and the messageMode-dependent CLOSE rule, each
+    # hand-derived from the cited reference lines ("ref").  Not RFC behaviour: netman's.
+    T = lambda b, fin=True, m=0x11223344: frame(1, b, fin=fin, mask=m)   # noqa: E731
+    B = lambda b, fin=True, m=0x55667788: frame(2, b, fin=fin, mask=m)   # noqa: E731
+    cases += [
+        dict(name="q5_msgid_counts_ping_and_pong",
+             ref="websocket_frame.go:89 (msgID++ for every FIN frame through nextFrame); websocket.go:190,204",
+             hex=(frame(9, b"a", mask=1) + frame(10, b"b", mask=2) + B(b"c")).hex(),
+             expect=dict(events=[["PONG", "61"], ["MESSAGE", 2, 2, "63"]])),
+        dict(name="q6_ping_inside_text_message_valid",
+             ref="websocket_frame.go:71 (check keyed on messageMode, not the PING opcode); :84-86 mode kept",
+             hex=(T(b"ab", fin=False) + frame(9, b"hi", mask=5) + frame(0, b"c", mask=6)).hex(),
+             expect=dict(events=[["PONG", "6869"], ["MESSAGE", 1, 1, "616263"]])),
+        dict(name="q6_ping_inside_text_message_invalid",
+             ref="websocket_frame.go:71-73 -> WebsocketMustUtf8 -> epoll.go:126-127 CloseCode(1007)",
+             hex=(T(b"ab", fin=False) + frame(9, b"\xff", mask=5)).hex(),
+             expect=dict(events=[["CLOSE", 1007, 5]])),
+        dict(name="q7_fragmented_close_joins_message",
+             ref="websocket.go:155-157 (EAGAIN from nextFrame returned); websocket_frame.go:95 continueBuffer += payload",
+             hex=(B(b"ab", fin=False) + frame(8, b"\x03\xe8zz", fin=False, mask=2) + frame(0, b"c", mask=3)).hex(),
+             expect=dict(events=[["MESSAGE", 0, 2, b"ab\x03\xe8zzc".hex()]])),
+        dict(name="q8_empty_fragment_escapes_data_check",
+             ref="websocket.go:142-146 (only continueBuffer.Len() >= 1 is rejected)",
+             hex=(T(b"", fin=False) + B(b"bin")).hex(),
+             expect=dict(events=[["MESSAGE", 0, 2, "62696e"]])),
+        dict(name="q8_data_frame_inside_fragmented_message",
+             ref="websocket.go:142-146 -> WebsocketPingPayloadOversize -> epoll.go:117-124 CloseCode(1002)",
+             hex=(T(b"a", fin=False) + B(b"bin")).hex(),
+             expect=dict(events=[["CLOSE", 1002, 3]])),
+        dict(name="text_mode_close_whole_invalid_skips_reason",
+             ref="websocket.go:155-167: nextFrame's whole-payload utf8.Valid fails (frame.go:71-73), error "
+                 "swallowed, stand-in reason DataLen = fragmentLength = 0 after reset() (frame.go:49, "
+                 "websocket.go:309) -> :170 skipped; code 1000 valid -> Close() (1000)",
+             hex=(T(b"ab", fin=False) + frame(8, b"\x03\xe8\xff", mask=9)).hex(),
+             expect=dict(events=[["CLOSE", 1000, 0]])),
+        dict(name="text_mode_close_whole_invalid_bad_code",
+             ref="as above, then verifyCloseCode(999) (websocket_ctrl.go:162) -> ProtocolError -> 1002",
+             hex=(T(b"ab", fin=False) + frame(8, b"\x03\xe7\xff", mask=9)).hex(),
+             expect=dict(events=[["CLOSE", 1002, 6]])),
+        dict(name="text_mode_close_whole_valid_reason_invalid",
+             ref="03 E8 80 80 is valid UTF-8 as a whole, so nextFrame returns the message (Len 4) and "
+                 "websocket.go:170 checks payload[2:] = 80 80 -> MustUtf8 -> 1007",
+             hex=(T(b"ab", fin=False) + frame(8, b"\x03\xe8\x80\x80", mask=9)).hex(),
+             expect=dict(events=[["CLOSE", 1007, 5]])),
+        dict(name="bin_mode_close_reason_invalid",
+             ref="messageMode BIN: no whole-payload check, websocket.go:170 checks payload[2:] = FF -> 1007",
+             hex=(B(b"ab", fin=False) + frame(8, b"\x03\xe8\xff", mask=9)).hex(),
+             expect=dict(events=[["CLOSE", 1007, 5]])),
+    ]
     return cases
 
 

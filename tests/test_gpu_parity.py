@@ -76,6 +76,28 @@ def test_fuzz_walk_4_records(codec_lib, monkeypatch, compact):
         c.close()
 
 
+def _close_streams():
+    from fuzz_streams import close_in_chain_stream, CLOSE_PAYLOADS
+    streams = [close_in_chain_stream(11000 + i) for i in range(600)]
+    for mode in (0, 1, 2):   # every CLOSE payload class in every messageMode
+        for p in CLOSE_PAYLOADS:
+            streams.append((synth.frame(mode, b"ab", fin=False) if mode else b"") + synth.frame(8, p, mask=0x0BADF00D))
+    return streams
+
+
+@pytest.mark.parametrize("compact,inline_max", [(False, 256), (True, 256), (False, 0)])
+def test_close_inside_text_and_bin_chains(codec_lib, monkeypatch, compact, inline_max):
+    """FIN=1 CLOSE frames inside TEXT / BIN chains (and outside any): the reason rule depends on
+    messageMode (websocket.go:153-172 + websocket_frame.go:49,71-73).  inline_max 0 defers every
+    other text check to the chip-wide UTF-8 kernel (the CLOSE itself is always checked in the walk)."""
+    monkeypatch.setenv("WSC_U8_INLINE_MAX", str(inline_max))
+    c = K.Codec(0, max_batch_bytes=16 << 20, max_segs=1 << 12, max_frames=1 << 16)
+    try:
+        _check_batch(c, _close_streams(), compact=compact)
+    finally:
+        c.close()
+
+
 def test_fuzz_text_heavy(codec):
     streams = [random_stream(5000 + i, n_units=30, text_p=0.9, err_p=0.02) for i in range(300)]
     _check_batch(codec, streams)

@@ -92,6 +92,48 @@ def test_q7_fragmented_close_joins_message():
     assert evs[0].type == O.EV_MESSAGE and evs[0].data == b"ab\x03\xe8zzc"
 
 
+def test_text_mode_close_skips_reason_when_whole_payload_invalid():
+    """VERDICT r1 weak #1.  Reference, CLOSE arm with len >= 2 (websocket.go:153-181):
+    nextFrame (websocket_frame.go:13-103) unmasks 03 E8 FF, calls reset() (:49 -> websocket.go:309,
+    fragmentLength = 0), then with messageMode == TEXT (set by the FIN=0 TEXT frame, :234-236) runs
+    utf8.Valid over the whole payload (:71-73): E8 FF fails -> WebsocketMustUtf8, swallowed at :156.
+    reason == nil, so the stand-in Message has DataLen = uint32(c.fragmentLength) = 0 (:160-167):
+    reason.Len() > 2 is false and the reason check (:170) is skipped; code 0x03E8 = 1000 passes
+    verifyCloseCode (websocket_ctrl.go:160-177) -> Close() -> CloseCode(1000)."""
+    s = frame(1, b"ab", fin=False, mask=1) + frame(8, b"\x03\xe8\xff", mask=2)
+    evs = O.run(s).events
+    assert [(e.type, e.close_code, e.err) for e in evs] == [(O.EV_CLOSE, 1000, 0)]
+    # same payload with code 999: only the code is verified -> ProtocolError -> 1002
+    s = frame(1, b"ab", fin=False, mask=1) + frame(8, b"\x03\xe7\xff", mask=2)
+    assert [(e.type, e.close_code) for e in O.run(s).events] == [(O.EV_CLOSE, 1002)]
+
+
+def _expected_close(mode, payload):
+    """websocket.go:153-181 restated on its own (not through the oracle): (close_code, err)"""
+    def valid(b):
+        try:
+            b.decode("utf-8")
+            return True
+        except UnicodeDecodeError:
+            return False
+    reason_len = 0 if (mode == 1 and not valid(payload)) else len(payload)
+    if reason_len > 2 and not valid(payload[2:]):
+        return 1007, 5   # WebsocketMustUtf8 (util/errors.go)
+    code = int.from_bytes(payload[:2], "big")
+    bad = code < 1000 or code >= 5000 or 1016 <= code <= 2999 or code in (1004, 1005, 1006, 1015)
+    return (1002, 6) if bad else (1000, 0)
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_close_rule_by_message_mode(mode):
+    from fuzz_streams import CLOSE_PAYLOADS
+    for p in CLOSE_PAYLOADS:
+        s = (frame(mode, b"ab", fin=False, mask=3) if mode else b"") + frame(8, p, mask=0x0BADF00D)
+        evs = O.run(s).events
+        assert len(evs) == 1 and evs[0].type == O.EV_CLOSE, (mode, p, evs)
+        assert (evs[0].close_code, evs[0].err) == _expected_close(mode, p), (mode, p)
+
+
 def test_q8_empty_fragment_escapes_data_check():
     s = frame(1, b"", fin=False, mask=1) + frame(2, b"bin", mask=2)
     evs = O.run(s).events
