@@ -52,19 +52,34 @@ def parse():
     ap.add_argument("--unmask-streams", type=int, default=1)
     ap.add_argument("--unmask-rest", action="store_true", help="mask the unmask streams to the CUs the walk does not use")
     ap.add_argument("--no-echo", action="store_true", help="skip the configs[0] loopback echo lines")
+    ap.add_argument("--no-config3", action="store_true",
+                    help="skip the BASELINE configs[3] line (1 M x 4 KiB frames per GPU dealt round-robin)")
     ap.add_argument("--no-other-configs", action="store_true",
                     help="skip the device-time lines for BASELINE.json configs[1], [2], [4]")
     return ap.parse_args()
 
 
+def cpu_model():
+    """the host CPU's model name (lscpu's "Model name", read from /proc/cpuinfo)"""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.lower().startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(cfg, seconds, threads):
     """The reference's hot loop (websocket_frame.go:33-42) ported to C (oracle/go_unmask_port.c),
-    on a bounded sample of the same frames: repeated passes over the first 256 frames (16 MiB)
-    until `seconds` of wall time have elapsed."""
+    over the WHOLE batch (every frame, 1 GiB of payload at the headline: far larger than the
+    host's last-level cache, so it streams from DRAM like the reference would), in passes until
+    `seconds` of wall time have elapsed.  threads > 1: frames split over that many threads (one
+    poller goroutine per core)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_ref as O
     lib = O.goport()
-    ns = min(256, cfg["n_frames"])
+    ns = cfg["n_frames"]
     wire = cfg["wire"]
     off = np.ascontiguousarray(cfg["payload_off"][:ns], dtype=np.uint64)
     ln = np.ascontiguousarray(cfg["plen"][:ns], dtype=np.uint32)
@@ -197,6 +212,13 @@ def main():
         want = synth.unmask_reference(cfg["wire"][: len(host)], cfg["payload_off"][:k], cfg["plen"][:k],
                                       cfg["mask"][:k]) if n_dec[j] % 2 else cfg["wire"][: len(host)]
         ok = ok and bool(np.array_equal(host[:end], want[:end]))
+    # every decode of the run (gate, warm-up, timed) on every context: no capacity overflow and no
+    # look-back timeout (sticky device bits, wsc_error_flags), and each buffer's last summary is OK
+    err_bits = 0
+    for c, t in zip(codecs, keep):
+        err_bits |= c.error_flags()
+        ok = ok and K.Codec.summary_status(t["summ"].cpu().numpy().copy()) == K.WSC_OK
+    ok = ok and err_bits == 0
     if split:
         torch.cuda.synchronize()
         for s_ in [walk_st] + unmask_st:
@@ -248,6 +270,7 @@ def main():
                                 f"{'the other ' + str(n_cu - a.walk_cus) if a.unmask_rest else 'all ' + str(n_cu)} CUs") if split
                                else "each batch in order on its own stream"},
         "parity_ok": ok,
+        "device_error_flags": err_bits,
         "single_batch": None if el_single is None else {
             "ms_per_step": round(el_single / a.steps * 1e3, 4),
             "gib_s": round(cfg["payload_bytes"] * world * a.steps / el_single / 2**30, 2)},
@@ -257,6 +280,8 @@ def main():
                      "kernel": "k_unmask", "alg_bytes_per_launch": alg_bytes},
     }
     solo = world == 1   # the extra lines (host-inclusive, other configs, encode, echo, CPU baseline) are N=1 only
+    if not a.no_config3:
+        out["configs3_dealt"] = config3_dealt(a, torch, dist, K, synth, world, rank, dev, cdev)
     if solo and not a.no_host_inclusive:
         out["host_inclusive"] = host_inclusive(codec, cfg, K)
         out["host_inclusive_pipelined"] = host_inclusive_pipelined(torch, codecs, streams, cfg, K)
@@ -270,17 +295,99 @@ def main():
     if solo and not a.no_echo:
         out["echo"] = echo_configs(with_cpu=not a.no_cpu)
     if solo and not a.no_cpu and a.cpu_seconds > 0:
-        threads = min(16, len(os.sched_getaffinity(0)))
-        v1, p1, e1 = cpu_baseline(cfg, a.cpu_seconds / 2, 1)
-        vm, pm_, em = cpu_baseline(cfg, a.cpu_seconds / 2, threads)
+        # every core this process may run on (the box's CPU share); 1 core = one poller goroutine
+        threads = min(256, len(os.sched_getaffinity(0)))
+        v1, p1, e1 = cpu_baseline(cfg, a.cpu_seconds / 3, 1)
+        vm, pm_, em = cpu_baseline(cfg, a.cpu_seconds * 2 / 3, threads)
         out["cpu_baseline"] = {"value": round(vm, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
-                               "sample": f"first 256 frames (16 MiB payload) of the same batch, {pm_} passes "
-                                         f"in {em:.1f} s; C port of websocket_frame.go:33-42 (Go absent)",
-                               "value_1core": round(v1, 3)}
+                               "sample": f"the whole headline batch ({a.frames} frames, "
+                                         f"{cfg['payload_bytes'] / 2**30:.2f} GiB payload, DRAM-resident), "
+                                         f"{pm_} passes in {em:.1f} s on {threads} threads; "
+                                         f"C port of websocket_frame.go:33-42 (Go absent)",
+                               "value_1core": round(v1, 3), "cpu_model": cpu_model(),
+                               "host_cpus": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0))}
     if rank == 0:
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()
+
+
+def config3_dealt(a, torch, dist, K, synth, world, rank, dev, cdev):
+    """BASELINE.json configs[3] at N GPUs: ONE global batch of N x 1 M masked 4 KiB BIN frames
+    (16 frames per connection segment; 8 M frames = 32 GiB at N = 8) whose segments are dealt
+    round-robin to the ranks (shard.assign_segments: segment g -> rank g mod N), so every rank
+    decodes its own 1 M-frame, 4 GiB shard -- independent, no collective on the data path.  Each
+    rank runs the headline's pipeline (2 contexts, split walk/unmask streams); the step time is
+    the max over ranks; value = all ranks' payload x steps / that time.  Per-rank times are
+    reported.  torch.distributed is used for the barriers, the max and the gather only."""
+    per_rank, size, fps = 1 << 20, 4096, 16
+    cfg = synth.dealt_uniform_batch(per_rank * world, size, fps, seed=synth.SEED_BASE + 3, world=world, rank=rank)
+    n_bytes, n_segs, nf = len(cfg["wire"]), len(cfg["seg_off"]) - 1, cfg["n_frames"]
+    n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
+    cs, bs, ts = [], [], []
+    for j in range(2):
+        c = K.Codec(dev.index, max_batch_bytes=n_bytes + 4096, max_segs=n_segs, max_frames=nf + 16)
+        t = dict(wire=torch.from_numpy(cfg["wire"]).to(dev),
+                 seg_off=torch.from_numpy(cfg["seg_off"].view(np.int64)).to(dev),
+                 st=torch.zeros(n_segs * 16, dtype=torch.uint8, device=dev),
+                 so=torch.zeros(n_segs * 32, dtype=torch.uint8, device=dev),
+                 fr=torch.zeros((nf + 16) * 32, dtype=torch.uint8, device=dev),
+                 sm=torch.zeros(32, dtype=torch.uint8, device=dev))
+        cs.append(c)
+        ts.append(t)
+        bs.append(c.make_batch(t["wire"], t["seg_off"], None, t["st"], t["so"], t["fr"], t["sm"]))
+    ws = cs[0].stream_create(K.cu_mask(range(min(n_cu // 2, max(16, (n_segs + 255) // 256))), n_cu))
+    us = cs[0].stream_create(None)
+    n_dec = [0, 0]
+
+    def run(k):
+        for i in range(k):
+            cs[i % 2].decode_split(bs[i % 2], ws, us)
+            n_dec[i % 2] += 1
+
+    run(a.warmup)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(a.steps)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    # parity on a sample (the first 64 frames of each buffer: unmasked after an odd number of
+    # decodes, the masked wire after an even one) + every decode's device error bits
+    m = int(cfg["payload_off"][63] + cfg["plen"][63])
+    ref = synth.unmask_reference(cfg["wire"][:m], cfg["payload_off"][:64], cfg["plen"][:64], cfg["mask"][:64])
+    ok = True
+    for j in range(2):
+        got = ts[j]["wire"][:m].cpu().numpy()
+        ok = ok and bool(np.array_equal(got, ref if n_dec[j] % 2 else cfg["wire"][:m]))
+        ok = ok and cs[j].error_flags() == 0
+        summ = ts[j]["sm"].cpu().numpy().copy().view(K.SUMMARY_DTYPE)[0]
+        ok = ok and int(summ["n_frames"]) == nf
+    cs[0].stream_destroy(ws)
+    cs[0].stream_destroy(us)
+    for c in cs:
+        c.close()
+    del ts, bs
+    torch.cuda.empty_cache()
+    times = [el]
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=cdev)
+        g = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(g, t)
+        times = [float(x.item()) for x in g]
+        okt = torch.tensor([1 if ok else 0], dtype=torch.int32, device=cdev)
+        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+        ok = bool(okt.item())
+    tmax = max(times)
+    return {"workload": f"{per_rank * world} x {size} B masked BIN frames ({fps} per connection segment), "
+                        f"segments dealt round-robin to {world} GPU(s): {per_rank} frames = "
+                        f"{cfg['payload_bytes'] / 2**30:.1f} GiB per GPU",
+            "gib_s": round(cfg["payload_bytes"] * world * a.steps / tmax / 2**30, 1),
+            "ms_per_step": round(tmax / a.steps * 1e3, 4),
+            "per_rank_ms_per_step": [round(x / a.steps * 1e3, 4) for x in times],
+            "n_gpus": world, "scaling": "weak", "parity_ok": ok}
 
 
 def other_configs(torch, K, synth):

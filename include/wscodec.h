@@ -38,6 +38,8 @@ extern "C" {
 #define WSC_E_CAPACITY (-4)  /* batch exceeds the context's configured capacity */
 #define WSC_E_NODEVICE (-5)  /* no usable gfx950 device */
 #define WSC_E_STATE (-6)     /* session misuse (unknown / closed connection) */
+#define WSC_E_INTERNAL (-7)  /* device-side look-back timeout: the batch's results are INVALID (never
+                                silently reported as capacity; see wsc_summary.overflow bit 1)     */
 
 /* ---- per-frame error sentinels: util/errors.go:9-14 (same order/values as the oracle) -------- */
 #define WSC_ERR_NONE 0
@@ -48,6 +50,8 @@ extern "C" {
 #define WSC_ERR_MUST_UTF8 5              /* WebsocketMustUtf8                       -> 1007 */
 #define WSC_ERR_PROTOCOL_ERROR 6         /* WebsocketProtocolError                  -> 1002 */
 #define WSC_ERR_TOO_LARGE 7              /* payload > max_frame_len (reference would panic, Q4) -> 1002 */
+#define WSC_ERR_DEVICE 8                 /* session only: the connection's batch hit a device error
+                                            -> CloseCode(1011); see wsc_session_* below           */
 
 /* ---- what the decoder did with a frame (websocket.go:136-208 / websocket_frame.go:52-102) --- */
 #define WSC_FK_FRAG 0        /* FIN=0 through nextFrame: payload appended to continueBuffer      */
@@ -126,7 +130,9 @@ typedef struct wsc_summary {
                               a late UTF-8 verdict stops a segment at its failing frame)          */
     uint32_t n_spans;      /* payload spans unmasked                                              */
     uint32_t overflow;     /* bit0: n_frames > frames_cap (records beyond the cap were dropped);
-                              bit1: internal look-back timeout (results invalid)                  */
+                              bit1: internal look-back timeout (results invalid).  Callers of the
+                              async wsc_decode check it with wsc_summary_status() or, for many
+                              batches at once, wsc_error_flags()                                  */
     uint32_t pad;
 } wsc_summary;
 
@@ -178,6 +184,16 @@ int wsc_host_free(void* p);
  * synchronised (wsc_sync with the same stream).  Inputs must be ready on that stream. */
 int wsc_decode(wsc_ctx* ctx, const wsc_batch* batch, void* hip_stream);
 int wsc_sync(wsc_ctx* ctx, void* hip_stream);
+
+/* Map a batch's (host copy of) wsc_summary to a return code: WSC_OK, WSC_E_INTERNAL (bit 1:
+ * results invalid) or WSC_E_CAPACITY (bit 0: records dropped).  Pure host function.            */
+int wsc_summary_status(const wsc_summary* summary);
+
+/* Sticky error bits of every decode / encode run on this context since it was created or last
+ * cleared: bit0 frame capacity exceeded, bit1 decode look-back timeout, bit2 encode look-back
+ * timeout.  Synchronises the device.  `clear` != 0 resets them.  Lets a caller that pipelines
+ * many async batches (bench, a poller) verify all of them with one call.                        */
+int wsc_error_flags(wsc_ctx* ctx, uint32_t* flags, int clear);
 
 /* Split pipeline: the header walk runs on `walk_stream`, the UTF-8 check and unmask on
  * `unmask_stream`, joined by the context's events.  The walk waits for this context's previous
@@ -238,7 +254,32 @@ int wsc_profile(wsc_ctx* ctx, const wsc_batch* batch, int iters, double* out_ms)
  * records per block 4 s_memrealtime stamps (100 MHz): start, counted, look-back done, emitted. */
 int wsc_debug_stamps(wsc_ctx* ctx, uint64_t* out, uint32_t max_blocks);
 
-/* ---- session: the per-connection DecodePacket() mirror (C++ host side above the ABI) --------- */
+/* ---- session: the per-connection DecodePacket() mirror (C++ host side above the ABI) ---------
+ * One session per poller thread (eventloop/epoll.go:36-143).  Per round the poller reads each
+ * ready connection once -- straight into the session's pinned staging with wsc_session_reserve +
+ * recv + wsc_session_commit (the only host copy is the kernel's socket copy), or with
+ * wsc_session_feed (one memcpy) -- then wsc_session_decode (= submit + complete), and drains every
+ * connection with wsc_session_next, which yields what DecodePacket + epoll.go:104-140 would have
+ * (one message / PONG reply / close per call, in order).  Double-buffered variant: submit round
+ * r+1 and send round r's replies while its H2D + kernels run, then complete it.
+ *
+ * Threading: wsc_session_remove may be called from ANY thread at any time (netman calls Close()
+ * -> remove() from handler and heartbeat goroutines, websocket_ctrl.go:73-96); it only queues the
+ * handle and the owning poller thread applies it at its next session call, after which the handle
+ * is invalid (WSC_E_STATE) and nothing more is delivered for it.  All other functions belong to
+ * the single thread that owns the session.  Handles carry a generation: a stale handle of a
+ * removed connection never touches a newer connection in the same slot.
+ *
+ * Capacity is per connection: max_frame_len is clamped to max_batch_bytes - 14 at create (a
+ * longer frame could never fit one batch: it closes ITS connection with WSC_ERR_TOO_LARGE / 1002,
+ * Q4); a connection with more bytes than a batch holds is decoded from a prefix and continues in
+ * the next batch; a batch with more frame records than max_frames is re-decoded in halves.
+ *
+ * Device failure (WSC_E_DEVICE / WSC_E_INTERNAL from decode/complete): the connections of the
+ * failed batch get WSC_EV_CLOSE with close_code 1011 and err WSC_ERR_DEVICE, keep their carried
+ * bytes (wsc_session_state) and decode nothing more; other connections are untouched.  There is
+ * no CPU fallback.  (The reference drops all of a poller's connections when epoll_wait fails,
+ * eventloop/epoll.go:41-49.)                                                                      */
 typedef struct wsc_session wsc_session;
 
 /* events popped by wsc_session_next(); mirrors what DecodePacket + epoll.go:104-140 produce   */
@@ -255,17 +296,27 @@ typedef struct wsc_event {
     uint32_t close_code;  /* CLOSE */
     uint32_t err;         /* CLOSE: WSC_ERR_* */
     uint32_t pad;
-    const uint8_t* data;  /* MESSAGE / PONG payload, owned by the session until the next
-                             wsc_session_decode() */
+    const uint8_t* data;  /* MESSAGE / PONG payload.  Valid until the FIRST of: the next
+                             wsc_session_next on the same connection, the next
+                             wsc_session_complete / wsc_session_decode, or the connection's
+                             removal being applied.  Copy it to keep it (the reference hands
+                             each handler a fresh buffer, websocket_frame.go:90).              */
     uint64_t len;
 } wsc_event;
 
 int wsc_session_create(int device, const wsc_config* cfg, uint32_t flags, wsc_session** out);
 int wsc_session_destroy(wsc_session* s);
 int wsc_session_open(wsc_session* s, uint32_t* conn_out);            /* newWebsocketProtocol */
-int wsc_session_remove(wsc_session* s, uint32_t conn);               /* remove() */
-int wsc_session_feed(wsc_session* s, uint32_t conn, const uint8_t* bytes, uint64_t n);
-int wsc_session_decode(wsc_session* s);                              /* one batched device pass */
+int wsc_session_remove(wsc_session* s, uint32_t conn);               /* remove(): any thread */
+/* Room for up to max_bytes of conn's next socket read: *ptr / *avail (avail may be smaller when
+ * the staging is nearly full; *ptr == NULL when the connection is closed: read nothing).  Follow
+ * with wsc_session_commit(conn, bytes actually read) before any other call for this session.   */
+int wsc_session_reserve(wsc_session* s, uint32_t conn, uint64_t max_bytes, uint8_t** ptr, uint64_t* avail);
+int wsc_session_commit(wsc_session* s, uint32_t conn, uint64_t n);
+int wsc_session_feed(wsc_session* s, uint32_t conn, const uint8_t* bytes, uint64_t n);   /* reserve+memcpy+commit */
+int wsc_session_submit(wsc_session* s);    /* async device pass over everything fed (one batch)  */
+int wsc_session_complete(wsc_session* s);  /* wait for it, queue each connection's events        */
+int wsc_session_decode(wsc_session* s);    /* submit + complete until everything fed is decoded  */
 int wsc_session_next(wsc_session* s, uint32_t conn, wsc_event* ev);  /* DecodePacket() */
 int wsc_session_state(wsc_session* s, uint32_t conn, wsc_conn_state* st, uint64_t* carry_bytes);
 

@@ -25,9 +25,11 @@ LIB_PATH = os.environ.get("WSC_LIB") or os.path.join(HERE, "libwscodec.so")
 # ---- constants (include/wscodec.h) -------------------------------------------------------------
 WSC_OK = 0
 WSC_E_INVAL, WSC_E_DEVICE, WSC_E_NOMEM, WSC_E_CAPACITY, WSC_E_NODEVICE, WSC_E_STATE = -1, -2, -3, -4, -5, -6
+WSC_E_INTERNAL = -7
 
 ERR_NONE, ERR_OPCODE_FAIL, ERR_RSV_FAIL, ERR_PING_PAYLOAD_OVERSIZE = 0, 1, 2, 3
 ERR_CTRL_FRAGMENTED, ERR_MUST_UTF8, ERR_PROTOCOL_ERROR, ERR_TOO_LARGE = 4, 5, 6, 7
+ERR_DEVICE = 8   # session: the connection's batch hit a device error -> CloseCode(1011)
 
 FK_FRAG, FK_MESSAGE, FK_PING, FK_PONG, FK_CLOSE, FK_PONG_EMPTY, FK_ERROR, FK_STALL = range(8)
 FF_UNMASKED, FF_CONT_MSG, FF_CTRL_ARENA = 0x01, 0x02, 0x40
@@ -94,6 +96,8 @@ SIGNATURES = {
     "wsc_host_free": (_I, [_P]),
     "wsc_decode": (_I, [_P, C.POINTER(WscBatch), _P]),
     "wsc_sync": (_I, [_P, _P]),
+    "wsc_summary_status": (_I, [_P]),
+    "wsc_error_flags": (_I, [_P, C.POINTER(_U32), _I]),
     "wsc_decode_split": (_I, [_P, C.POINTER(WscBatch), _P, _P]),
     "wsc_stream_create": (_I, [_P, _P, _U32, C.POINTER(_P)]),
     "wsc_stream_destroy": (_I, [_P, _P]),
@@ -106,7 +110,11 @@ SIGNATURES = {
     "wsc_session_destroy": (_I, [_P]),
     "wsc_session_open": (_I, [_P, C.POINTER(_U32)]),
     "wsc_session_remove": (_I, [_P, _U32]),
+    "wsc_session_reserve": (_I, [_P, _U32, _U64, C.POINTER(_P), C.POINTER(_U64)]),
+    "wsc_session_commit": (_I, [_P, _U32, _U64]),
     "wsc_session_feed": (_I, [_P, _U32, _P, _U64]),
+    "wsc_session_submit": (_I, [_P]),
+    "wsc_session_complete": (_I, [_P]),
     "wsc_session_decode": (_I, [_P]),
     "wsc_session_next": (_I, [_P, _U32, C.POINTER(WscEvent)]),
     "wsc_session_state": (_I, [_P, _U32, C.POINTER(WscConnState), C.POINTER(_U64)]),
@@ -248,6 +256,22 @@ class Codec:
         """walk on walk_stream, UTF-8 check + unmask on unmask_stream (wsc_decode_split)"""
         _check(self.lib.wsc_decode_split(self.h, C.byref(batch), walk_stream, unmask_stream), "wsc_decode_split")
 
+    def error_flags(self, clear: bool = False) -> int:
+        """sticky error bits of every decode/encode on this context (wsc_error_flags): bit0 frame
+        capacity exceeded, bit1 decode look-back timeout, bit2 encode look-back timeout"""
+        v = C.c_uint32()
+        _check(self.lib.wsc_error_flags(self.h, C.byref(v), 1 if clear else 0), "wsc_error_flags")
+        return v.value
+
+    @staticmethod
+    def summary_status(summary) -> int:
+        """wsc_summary_status of a host copy of wsc_summary (SUMMARY_DTYPE record or 32 bytes)"""
+        a = np.asarray(summary)
+        if a.dtype == SUMMARY_DTYPE:
+            a = a.reshape(1)          # a record scalar (e.g. summary[0]) -> 1-element array
+        a = np.ascontiguousarray(np.ascontiguousarray(a).view(np.uint8).reshape(-1)[:32])
+        return load_library().wsc_summary_status(a.ctypes.data)
+
     def stream_create(self, cu_mask=None) -> int:
         """a raw hipStream_t (int), restricted to the CUs set in cu_mask (list of u32 words)"""
         out = C.c_void_p()
@@ -358,6 +382,7 @@ WebsocketCtrlMessageMustNotFragmented = NetmanError("websocket control message M
 WebsocketMustUtf8 = NetmanError("websocket text message must utf-8")
 WebsocketProtocolError = NetmanError("websocket protocol error")
 WebsocketFrameTooLarge = NetmanError("websocket frame exceeds max_frame_len")  # Q4 divergence
+DeviceFailure = NetmanError("websocket decode device failure")                  # session policy -> 1011
 EAGAIN = NetmanError("resource temporarily unavailable")
 
 SENTINELS = {
@@ -368,6 +393,7 @@ SENTINELS = {
     ERR_MUST_UTF8: WebsocketMustUtf8,
     ERR_PROTOCOL_ERROR: WebsocketProtocolError,
     ERR_TOO_LARGE: WebsocketFrameTooLarge,
+    ERR_DEVICE: DeviceFailure,
 }
 
 
@@ -378,6 +404,8 @@ def close_code_for(err) -> int | None:
         return 1002
     if err is WebsocketMustUtf8:
         return 1007
+    if err is DeviceFailure:
+        return 1011
     return None
 
 
@@ -424,6 +452,24 @@ class Session:
     def feed(self, conn: int, data: bytes):
         buf = (C.c_uint8 * len(data)).from_buffer_copy(data) if data else None
         _check(self.lib.wsc_session_feed(self.h, conn, buf, len(data)), "wsc_session_feed")
+
+    def reserve_commit(self, conn: int, data: bytes) -> int:
+        """one socket read the zero-copy way: reserve room in the pinned staging, write into it
+        (here: from `data`, standing in for recv()), commit what was written; returns bytes taken"""
+        p, avail = C.c_void_p(), C.c_uint64()
+        _check(self.lib.wsc_session_reserve(self.h, conn, len(data), C.byref(p), C.byref(avail)), "wsc_session_reserve")
+        if not p.value:
+            return 0
+        k = min(len(data), avail.value)
+        C.memmove(p.value, data, k)
+        _check(self.lib.wsc_session_commit(self.h, conn, k), "wsc_session_commit")
+        return k
+
+    def submit(self):
+        _check(self.lib.wsc_session_submit(self.h), "wsc_session_submit")
+
+    def complete(self):
+        _check(self.lib.wsc_session_complete(self.h), "wsc_session_complete")
 
     def decode(self):
         _check(self.lib.wsc_session_decode(self.h), "wsc_session_decode")

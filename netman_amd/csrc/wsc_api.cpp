@@ -52,6 +52,7 @@ struct wsc_ctx {
     wsc_config cfg{};
     uint32_t pieces = 8;          // 16 B pieces per lane -> window = pieces KiB
     SegCount* counts = nullptr;
+    uint32_t* sticky = nullptr;      // error bits of every decode/encode (wsc_error_flags), never re-armed
     uint32_t* lb_state = nullptr;    // [0] ticket, [1] spin-timeout flag, [2] UTF-8 item count, [3..] per-block flags
     uint32_t* u8info = nullptr;      // per segment {utf8-failing frame ordinal, DFA state}
     uint64_t* lb_agg = nullptr;
@@ -65,6 +66,7 @@ struct wsc_ctx {
     uint32_t u8items_cap = 0;
     U8Seg* u8seg = nullptr;
     uint32_t u8_inline_max = 256;
+    uint32_t u8_grid = 0;               // WSC_U8_GRID: k_u8_check workgroups (A/B experiments; 0 = 5 per CU)
     int walk_krec = 0;                  // WSC_WALK_KREC: 16 or 4 pins that walk instance (A/B, tests); 0 = auto
     uint64_t tile_entries = 0;
     // host-staged path buffers (lazily allocated)
@@ -161,6 +163,8 @@ int wsc_create(int device, const wsc_config* cfg_in, wsc_ctx** out) {
     chk(hipEventCreateWithFlags(&c->ev_walked, hipEventDisableTiming), "hipEventCreate");
     chk(hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming), "hipEventCreate");
     chk(hipMalloc(&c->counts, cfg.max_segs * sizeof(SegCount)), "hipMalloc counts");
+    chk(hipMalloc(&c->sticky, sizeof(uint32_t)), "hipMalloc sticky");
+    if (rc == WSC_OK) chk(hipMemsetAsync(c->sticky, 0, sizeof(uint32_t), c->stream), "hipMemset sticky");
     const uint64_t max_blocks = (cfg.max_segs + 255) / 256 + 1;
     chk(hipMalloc(&c->lb_state, (max_blocks + 3) * sizeof(uint32_t)), "hipMalloc lb_state");
     chk(hipMalloc(&c->u8info, (uint64_t)cfg.max_segs * 2 * sizeof(uint32_t)), "hipMalloc u8info");
@@ -180,6 +184,7 @@ int wsc_create(int device, const wsc_config* cfg_in, wsc_ctx** out) {
     chk(hipMalloc(&c->u8items, (uint64_t)c->u8items_cap * sizeof(U8Item)), "hipMalloc u8items");
     chk(hipMalloc(&c->u8maps, (uint64_t)c->u8items_cap * sizeof(uint64_t)), "hipMalloc u8maps");
     chk(hipMalloc(&c->u8seg, (uint64_t)cfg.max_segs * sizeof(U8Seg)), "hipMalloc u8seg");
+    if (const char* e = std::getenv("WSC_U8_GRID"); e && *e) c->u8_grid = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("WSC_WALK_KREC"); e && *e)
         c->walk_krec = std::atoi(e) == 4 ? 4 : 16;
     if (const char* e = std::getenv("WSC_U8_INLINE_MAX"); e && *e)   // test knob: 0 sends all text chip-wide
@@ -207,7 +212,7 @@ int wsc_destroy(wsc_ctx* c) {
     if (!c) return WSC_OK;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    void* ptrs[] = {c->dbg, c->counts, c->lb_state, c->u8info, c->lb_agg, c->lb_incl, c->spans, c->tile, c->d_wire, c->d_arena,
+    void* ptrs[] = {c->dbg, c->sticky, c->counts, c->lb_state, c->u8info, c->lb_agg, c->lb_incl, c->spans, c->tile, c->d_wire, c->d_arena,
                     c->d_seg_off, c->d_state_in, c->d_state_out, c->d_seg_out, c->d_frames,
                     c->d_frame_dst, c->d_summary, c->enc_lb_state, c->enc_lb_agg, c->enc_lb_incl, c->enc_tile,
                     c->d_enc_msgs, c->d_enc_src, c->d_enc_out, c->d_enc_off, c->u8items, c->u8maps, c->u8seg};
@@ -288,6 +293,7 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     wa.u8count = c->lb_state + 2;
     wa.u8seg = c->u8seg;
     wa.u8_inline_max = c->u8_inline_max;
+    wa.sticky = c->sticky;
 
     const dim3 wblk(256), wgrid((n + 255) / 256);
     auto rec = [&](int i) {
@@ -327,7 +333,7 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     ua.seg_out = b->seg_out;
     ua.state_out = b->state_out;
     ua.summary = b->summary;
-    hipLaunchKernelGGL(k_u8_check, dim3((uint32_t)c->n_cu * 5), dim3(256), 0, st, ua);   // resident: 5 waves/SIMD (96 VGPRs)
+    hipLaunchKernelGGL(k_u8_check, dim3(c->u8_grid ? c->u8_grid : (uint32_t)c->n_cu * 5), dim3(256), 0, st, ua);   // resident: 5 waves/SIMD (96 VGPRs)
     HIP_TRY(hipGetLastError());
     rec(2);
     rec(3);
@@ -450,7 +456,22 @@ int wsc_decode_host(wsc_ctx* c, uint8_t* wire, uint64_t n_bytes, const uint64_t*
         HIP_TRY(hipMemcpyAsync(wire, c->d_wire, n_bytes, hipMemcpyDeviceToHost, st));
     }
     HIP_TRY(hipStreamSynchronize(st));
-    if (summary->overflow) return fail(WSC_E_CAPACITY, "frame capacity exceeded");
+    return wsc_summary_status(summary);
+}
+
+int wsc_summary_status(const wsc_summary* summary) {
+    if (!summary) return fail(WSC_E_INVAL, "NULL summary");
+    if (summary->overflow & 2u) return fail(WSC_E_INTERNAL, "device look-back timeout: batch results are invalid");
+    if (summary->overflow & 1u) return fail(WSC_E_CAPACITY, "frame capacity exceeded: records beyond frames_cap dropped");
+    return WSC_OK;
+}
+
+int wsc_error_flags(wsc_ctx* c, uint32_t* flags, int clear) {
+    if (!c || !flags) return fail(WSC_E_INVAL, "NULL argument");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(flags, c->sticky, sizeof(uint32_t), hipMemcpyDeviceToHost));
+    if (clear) HIP_TRY(hipMemset(c->sticky, 0, sizeof(uint32_t)));
     return WSC_OK;
 }
 
@@ -477,6 +498,7 @@ static int launch_encode(wsc_ctx* c, const wsc_out_msg* msgs, uint32_t n, const 
     ea.lb_flag = c->enc_lb_state + 2;
     ea.lb_agg = c->enc_lb_agg;
     ea.lb_incl = c->enc_lb_incl;
+    ea.sticky = c->sticky;
     const uint32_t sblocks = (n + 255) / 256;
     hipLaunchKernelGGL(k_encode_scan, dim3(sblocks), dim3(256), 0, st, ea);
     HIP_TRY(hipGetLastError());
@@ -530,6 +552,7 @@ int wsc_encode_host(wsc_ctx* c, const wsc_out_msg* msgs, uint32_t n_msgs, const 
     HIP_TRY(hipMemcpyAsync(out_off, c->d_enc_off, ((uint64_t)n_msgs + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     const uint64_t total = out_off[n_msgs];
+    if (total == ~0ull) return fail(WSC_E_INTERNAL, "device look-back timeout in the encode scan: output invalid");
     if (total > out_cap) return fail(WSC_E_CAPACITY, "encoded frames exceed out_cap");
     if (total) HIP_TRY(hipMemcpyAsync(out, c->d_enc_out, total, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));

@@ -156,7 +156,10 @@ __global__ __launch_bounds__(256) void k_encode_scan(EncArgs a) {
         for (; w < w_end; ++w) a.tile[w] = i;
         if (i == a.n_msgs - 1) {
             uint64_t total = off + sz;
-            if (__hip_atomic_load(a.lb_err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) total = ~0ull;   // invalid
+            if (__hip_atomic_load(a.lb_err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                total = ~0ull;   // invalid
+                __hip_atomic_fetch_or(a.sticky, 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
             a.out_off[a.n_msgs] = total;
         }
     }

@@ -754,6 +754,7 @@ __global__ __launch_bounds__(256) void k_walk_fused(WalkArgs a) {
         if (__hip_atomic_load(a.lb_err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) sm.overflow |= 2u;
         sm.pad = 0;
         *a.summary = sm;
+        if (sm.overflow) __hip_atomic_fetch_or(a.sticky, sm.overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 

@@ -96,6 +96,7 @@ struct WalkArgs {
     uint32_t* u8count;           // item counter (re-armed by k_unmask)
     U8Seg* u8seg;
     uint32_t u8_inline_max;      // text payloads up to this many bytes are validated in the walk
+    uint32_t* sticky;            // context error bits, never re-armed by a kernel (wsc_error_flags)
 };
 
 struct U8Args {
@@ -129,6 +130,7 @@ struct EncArgs {
     uint64_t* lb_agg;
     uint64_t* lb_incl;
     uint32_t* lb_err;
+    uint32_t* sticky;            // context error bits (bit2: encode look-back timeout)
 };
 
 struct EncCopyArgs {

@@ -2,25 +2,49 @@
 //
 // In netman every poller goroutine calls conn.DecodePacket() once per readiness event
 // (eventloop/epoll.go:105) and gets back at most one (IMessage, error) (server/websocket.go:82-212).
-// Here a poller instead feeds each ready connection's bulk read into the session
-// (wsc_session_feed), runs ONE batched device decode over all of them (wsc_session_decode), and
-// then drains each connection's results one at a time with wsc_session_next(), which returns
-// exactly what the reference's DecodePacket + epoll.go:104-140 would have produced, in order:
+// Here a poller instead reads each ready connection ONCE, straight into pinned staging
+// (wsc_session_reserve + recv + wsc_session_commit, or wsc_session_feed), runs ONE batched device
+// decode over all of them (wsc_session_submit / wsc_session_complete, or wsc_session_decode =
+// both), and then drains each connection's results one at a time with wsc_session_next(), which
+// returns exactly what the reference's DecodePacket + epoll.go:104-140 would have produced:
 //   WSC_EV_MESSAGE  (Message, nil)          -> IWebsocketHandler.Message   (routermgr.go:101)
 //   WSC_EV_PONG     pong() echo             -> push(encode(0x8A, payload)) (websocket_ctrl.go:128-153)
 //   WSC_EV_CLOSE    CloseCode(code)         -> epoll.go:106-129 mapping of the sentinel
 //   WSC_EV_STALL    unmasked frame (Q3)     -> nothing more is delivered
 //   WSC_EV_NONE     (nil, syscall.EAGAIN)
-// The per-connection state a goroutine kept in websocketProtocol (websocket.go:38-56) lives in
-// Conn: the carried partial frame (the reference keeps it in the kernel socket buffer / rBuffer),
-// continueBuffer for fragmented messages, and the device-visible wsc_conn_state.
+//
+// Data path (per poller round): socket -> pinned staging (the one host copy, done by recv) -> H2D
+// -> header walk + unmask (HBM) -> D2H into a pinned result buffer -> messages handed out as views
+// into it.  Two staging sets, each with its own device context and HIP stream, so round r+1's
+// H2D + kernels run while the poller sends round r's replies (submit/complete).  A connection's
+// undecoded tail (an incomplete frame) is kept on the host (Conn::carry) and placed in front of
+// its next bytes.
+//
+// Capacity is handled per connection, never per session (one connection cannot stall the others):
+//   * frames longer than max_batch_bytes - 14 cannot ever fit a batch: max_frame_len is clamped to
+//     that at create, so such a frame closes ITS connection with WSC_ERR_TOO_LARGE -> 1002 (Q4);
+//   * a connection whose bytes do not fit the batch is decoded from a prefix (it always leads a
+//     batch then, so its first frame fits) and the rest follows in the next batch;
+//   * a batch whose frame records exceed max_frames is re-decoded in halves (one connection: a
+//     prefix ending at a frame boundary the device reported).
+// Device failure policy (the reference drops a poller's connections when epoll_wait
+// fails, eventloop/epoll.go:41-49): the connections of the failed batch get WSC_EV_CLOSE with
+// close_code 1011 and err WSC_ERR_DEVICE, keep their carried bytes (wsc_session_state), and
+// decode nothing more; the other connections are untouched; the call returns the error.  There
+// is no CPU fallback.
+// Threading: wsc_session_remove may be called from ANY thread at any time (netman's handler and
+// heartbeat goroutines call Close() -> remove(), websocket_ctrl.go:73-96); it only queues the
+// handle, and the poller thread applies queued removals at its next session call.  Every other
+// function belongs to the one poller thread that owns the session.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -28,139 +52,196 @@
 
 namespace {
 
+constexpr uint32_t SLOT_BITS = 22;                  // handle = slot | generation << 22
+constexpr uint32_t SLOT_MASK = (1u << SLOT_BITS) - 1;
+constexpr uint32_t GEN_MASK = (1u << (32 - SLOT_BITS)) - 1;
+constexpr uint32_t DEAD_SEG = 0xFFFFFFFFu;          // staging region of no connection (decodes nothing)
+constexpr uint64_t MIN_RESERVE = 64 << 10;          // staging room worth handing to recv()
+
 struct Event {
     wsc_event ev;
-    std::vector<uint8_t> data;     // owned copy (fragmented messages, earlier batches of a decode)
-    const uint8_t* view = nullptr; // zero-copy: points into the pinned staging of the last batch
+    std::vector<uint8_t> data;     // owned copy (fragmented messages, materialised views)
+    const uint8_t* view = nullptr; // zero-copy: points into a staging set's pinned result buffer
     uint64_t view_len = 0;
+    int set = -1;                  // staging set of the view
 };
 
 struct Conn {
     bool live = false;
+    uint32_t gen = 0;
     wsc_conn_state st{};
-    std::vector<uint8_t> carry;   // undecoded tail of previous reads (starts at a frame header)
-    std::vector<uint8_t> fed;     // bytes read since the last decode
+    std::vector<uint8_t> carry;   // undecoded tail of earlier reads (starts at a frame header), masked
+    std::vector<uint8_t> spill;   // bytes fed while they did not fit the staging being filled
     std::vector<uint8_t> cont;    // continueBuffer (unmasked fragments so far)
     std::deque<Event> pending;
     Event current;                // storage for the event last returned by next()
+    uint64_t fill_epoch = ~0ull;  // == session fill_epoch while placed in the staging being filled
+    uint32_t seg = 0;             // its segment there
+    uint64_t reserved = 0;        // bytes handed out by the last reserve (0 = none)
+    bool reserved_spill = false;
+    bool failed = false;          // its batch hit a device error (WSC_ERR_DEVICE)
 };
 
-uint32_t close_code_for(uint32_t err) {   // eventloop/epoll.go:106-129
-    return err == WSC_ERR_MUST_UTF8 ? 1007u : 1002u;
-}
-
-}  // namespace
-
-struct wsc_session {
+struct Stage {                    // one staging set: pinned host buffers, device buffers, context
     wsc_ctx* ctx = nullptr;
-    wsc_config cfg{};
-    uint32_t flags = 0;
-    std::vector<Conn> conns;
-    std::vector<uint32_t> free_ids;
-    // pinned staging
-    uint8_t* h_wire = nullptr;
-    uint8_t* h_arena = nullptr;
+    hipStream_t stream = nullptr;
+    uint8_t* h_wire = nullptr;    // masked bytes as read (input)
+    uint8_t* h_res = nullptr;     // results: unmasked wire (in place) or the arena (COMPACT)
     uint64_t* h_seg_off = nullptr;
     wsc_conn_state* h_state_in = nullptr;
     wsc_conn_state* h_state_out = nullptr;
     wsc_seg_result* h_seg_out = nullptr;
     wsc_frame* h_frames = nullptr;
     uint64_t* h_frame_dst = nullptr;
-    // WSC_SESSION_TIMING=1: seconds spent per phase of wsc_session_decode, printed at destroy
-    bool timing = false;
-    double t_pack = 0, t_device = 0, t_harvest = 0;
-    uint64_t n_decodes = 0, n_bytes = 0;
+    wsc_summary* h_summary = nullptr;
+    void* d_wire = nullptr;
+    void* d_arena = nullptr;
+    void* d_seg_off = nullptr;
+    void* d_state_in = nullptr;
+    void* d_state_out = nullptr;
+    void* d_seg_out = nullptr;
+    void* d_frames = nullptr;
+    void* d_frame_dst = nullptr;
+    void* d_summary = nullptr;
+    // the batch being filled / in flight
+    uint64_t bytes = 0;
+    std::vector<uint32_t> seg_conn;   // handle per segment (DEAD_SEG: a region nobody owns)
+    std::vector<uint64_t> seg_start;
+    std::vector<uint64_t> seg_len;
+    std::vector<uint8_t> done;        // segment harvested (complete)
+    bool in_flight = false;
+    int launch_rc = WSC_OK;
+    std::vector<uint32_t> view_conns; // slots holding zero-copy views into h_res
 };
 
-static double now_s() {
+uint32_t close_code_for(uint32_t err) {   // eventloop/epoll.go:106-129
+    return err == WSC_ERR_MUST_UTF8 ? 1007u : 1002u;
+}
+
+double now_s() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-extern "C" {
+}  // namespace
 
-int wsc_session_destroy(wsc_session* s);
+struct wsc_session {
+    wsc_config cfg{};
+    uint32_t flags = 0;
+    int device = 0;
+    std::vector<Conn> conns;
+    std::vector<uint32_t> free_slots;
+    std::atomic<uint32_t> n_slots{0};
+    Stage st[2];
+    int fill = 0;                 // staging set being filled
+    uint64_t fill_epoch = 1;
+    // removals queued by any thread, applied by the poller thread
+    std::mutex rm_mu;
+    std::vector<uint32_t> rm_q;
+    std::atomic<uint32_t> rm_pending{0};
+    // test knob: WSC_SESSION_FAULT=k fails the k-th device batch as a device error would
+    uint64_t fault_at = 0, n_submits = 0;
+    // WSC_SESSION_TIMING=1: seconds per phase, printed at destroy
+    bool timing = false;
+    double t_pack = 0, t_device = 0, t_harvest = 0;
+    uint64_t n_batches = 0, n_bytes = 0;
+};
 
-int wsc_session_create(int device, const wsc_config* cfg, uint32_t flags, wsc_session** out) {
-    if (!out) return WSC_E_INVAL;
-    *out = nullptr;
-    wsc_session* s = new wsc_session();
-    if (cfg) s->cfg = *cfg; else wsc_config_default(&s->cfg);
-    s->flags = flags & WSC_F_COMPACT;
-    int rc = wsc_create(device, &s->cfg, &s->ctx);
-    if (rc) { delete s; return rc; }
+namespace {
+
+Conn* lookup(wsc_session* s, uint32_t h) {
+    const uint32_t slot = h & SLOT_MASK;
+    if (slot >= s->conns.size()) return nullptr;
+    Conn& c = s->conns[slot];
+    if (!c.live || c.gen != (h >> SLOT_BITS)) return nullptr;
+    return &c;
+}
+
+void kill_conn(wsc_session* s, uint32_t slot) {
+    Conn& c = s->conns[slot];
+    const uint32_t gen = c.gen;
+    Stage& f = s->st[s->fill];
+    if (c.fill_epoch == s->fill_epoch && c.seg < f.seg_conn.size()) f.seg_conn[c.seg] = DEAD_SEG;
+    c = Conn();
+    c.gen = gen;   // the next open() of this slot bumps it
+    s->free_slots.push_back(slot);
+}
+
+// websocket_ctrl.go:73-96 remove(): applied on the poller thread
+void apply_removes(wsc_session* s) {
+    if (!s->rm_pending.load(std::memory_order_acquire)) return;
+    std::vector<uint32_t> q;
+    {
+        std::lock_guard<std::mutex> g(s->rm_mu);
+        q.swap(s->rm_q);
+        s->rm_pending.store(0, std::memory_order_relaxed);
+    }
+    for (uint32_t h : q)
+        if (lookup(s, h)) kill_conn(s, h & SLOT_MASK);
+}
+
+void materialize_views(wsc_session* s, int set) {
+    Stage& g = s->st[set];
+    for (uint32_t slot : g.view_conns) {
+        if (slot >= s->conns.size()) continue;
+        for (Event& e : s->conns[slot].pending)
+            if (e.view && e.set == set) {
+                e.data.assign(e.view, e.view + e.view_len);
+                e.view = nullptr;
+                e.set = -1;
+            }
+    }
+    g.view_conns.clear();
+}
+
+// place connection c (its carry first) in the staging being filled, with room for `extra` more
+// bytes; false if the staging cannot host it now
+bool place(wsc_session* s, Conn& c, uint32_t handle, uint64_t extra) {
+    Stage& f = s->st[s->fill];
     const wsc_config& g = s->cfg;
-    void* p = nullptr;
-    auto H = [&](uint64_t bytes) -> void* {
-        p = nullptr;
-        if (rc == WSC_OK) rc = wsc_host_alloc(bytes, &p);
-        return p;
-    };
-    s->h_wire = (uint8_t*)H(g.max_batch_bytes + 64);
-    s->h_arena = (uint8_t*)H(g.max_batch_bytes + 64);
-    s->h_seg_off = (uint64_t*)H((g.max_segs + 1) * sizeof(uint64_t));
-    s->h_state_in = (wsc_conn_state*)H(g.max_segs * sizeof(wsc_conn_state));
-    s->h_state_out = (wsc_conn_state*)H(g.max_segs * sizeof(wsc_conn_state));
-    s->h_seg_out = (wsc_seg_result*)H(g.max_segs * sizeof(wsc_seg_result));
-    s->h_frames = (wsc_frame*)H((uint64_t)g.max_frames * sizeof(wsc_frame));
-    s->h_frame_dst = (uint64_t*)H((uint64_t)g.max_frames * sizeof(uint64_t));
-    if (rc) { wsc_session_destroy(s); return rc; }
-    if (const char* e = std::getenv("WSC_SESSION_TIMING"); e && e[0] == '1') s->timing = true;
-    *out = s;
-    return WSC_OK;
-}
-
-int wsc_session_destroy(wsc_session* s) {
-    if (!s) return WSC_OK;
-    if (s->timing)
-        fprintf(stderr, "wsc_session: %llu decodes, %llu bytes: pack %.4f s, device (H2D+kernels+D2H) %.4f s, harvest %.4f s\n",
-                (unsigned long long)s->n_decodes, (unsigned long long)s->n_bytes, s->t_pack, s->t_device, s->t_harvest);
-    void* ps[] = {s->h_wire, s->h_arena, s->h_seg_off, s->h_state_in, s->h_state_out,
-                  s->h_seg_out, s->h_frames, s->h_frame_dst};
-    for (void* p : ps)
-        if (p) wsc_host_free(p);
-    if (s->ctx) wsc_destroy(s->ctx);
-    delete s;
-    return WSC_OK;
-}
-
-int wsc_session_open(wsc_session* s, uint32_t* conn_out) {   // newWebsocketProtocol, websocket.go:59-79
-    if (!s || !conn_out) return WSC_E_INVAL;
-    uint32_t id;
-    if (!s->free_ids.empty()) { id = s->free_ids.back(); s->free_ids.pop_back(); }
-    else { id = (uint32_t)s->conns.size(); s->conns.emplace_back(); }
-    s->conns[id] = Conn();
-    s->conns[id].live = true;
-    *conn_out = id;
-    return WSC_OK;
-}
-
-int wsc_session_remove(wsc_session* s, uint32_t conn) {     // remove(), websocket_ctrl.go:73-96
-    if (!s || conn >= s->conns.size() || !s->conns[conn].live) return WSC_E_STATE;
-    s->conns[conn] = Conn();
-    s->free_ids.push_back(conn);
-    return WSC_OK;
-}
-
-int wsc_session_feed(wsc_session* s, uint32_t conn, const uint8_t* bytes, uint64_t n) {
-    if (!s || conn >= s->conns.size() || !s->conns[conn].live) return WSC_E_STATE;
-    if (n && !bytes) return WSC_E_INVAL;
-    Conn& c = s->conns[conn];
-    if (c.st.status != WSC_SEG_OPEN) return WSC_OK;   // closed / stalled: bytes are ignored
-    c.fed.insert(c.fed.end(), bytes, bytes + n);
-    return WSC_OK;
+    if (c.fill_epoch == s->fill_epoch) return true;
+    const uint64_t need = c.carry.size() + c.spill.size() + extra;
+    if (f.bytes + need > g.max_batch_bytes && f.bytes > 0) return false;
+    if (f.seg_conn.size() + 2 > g.max_segs) return false;   // keep one slot for a dead region
+    if (need > g.max_batch_bytes) {
+        // only a batch's first connection may exceed it: it is decoded from a prefix (below)
+        if (f.bytes > 0) return false;
+    }
+    uint64_t n = c.carry.size() + c.spill.size();
+    if (n > g.max_batch_bytes) n = g.max_batch_bytes;   // prefix (carry first, at most one frame)
+    c.seg = (uint32_t)f.seg_conn.size();
+    f.seg_conn.push_back(handle);
+    f.seg_start.push_back(f.bytes);
+    uint64_t k = 0;
+    const uint64_t kc = c.carry.size() < n ? c.carry.size() : n;
+    if (kc) std::memcpy(f.h_wire + f.bytes, c.carry.data(), kc);
+    k = kc;
+    if (k < n) {
+        const uint64_t ks = n - k;
+        std::memcpy(f.h_wire + f.bytes + k, c.spill.data(), ks);
+        k += ks;
+    }
+    // what was copied leaves carry/spill (a prefix leaves the rest behind, in order)
+    if (kc) c.carry.erase(c.carry.begin(), c.carry.begin() + (long)kc);
+    if (k > kc) c.spill.erase(c.spill.begin(), c.spill.begin() + (long)(k - kc));
+    if (!c.carry.empty()) {   // prefix cut inside the carry: keep order carry -> spill
+        c.spill.insert(c.spill.begin(), c.carry.begin(), c.carry.end());
+        c.carry.clear();
+    }
+    f.seg_len.push_back(n);
+    f.bytes += n;
+    c.fill_epoch = s->fill_epoch;
+    return true;
 }
 
 // turn one segment's frame records into the DecodePacket results the reference would return
-// zero_copy: the staging stays untouched until the next wsc_session_decode (this is the decode's
-// last device batch), so complete single-frame messages and PING payloads are handed out as views
-// into it instead of copies; wsc_event.data's lifetime is exactly that (include/wscodec.h).
-static void harvest(wsc_session* s, Conn& c, const uint8_t* seg, const wsc_seg_result& r,
-                    const wsc_conn_state& so, uint64_t seg_base, bool zero_copy) {
+void harvest(wsc_session* s, int set, Conn& c, uint32_t slot, const uint8_t* in_seg, const uint8_t* res_base,
+             uint64_t seg_len, const wsc_seg_result& r, const wsc_conn_state& so,
+             const wsc_frame* frames, const uint64_t* frame_dst, uint64_t arena_base) {
     const bool compact = (s->flags & WSC_F_COMPACT) != 0;
+    bool views = false;
     for (uint32_t i = r.frame_begin; i < r.frame_begin + r.frame_count; ++i) {
-        const wsc_frame& f = s->h_frames[i];
-        const uint8_t* p = compact ? s->h_arena + s->h_frame_dst[i]
-                                   : seg + (f.hdr_off - seg_base) + f.hdr_len;
+        const wsc_frame& f = frames[i];
+        const uint8_t* p = compact ? res_base + arena_base + frame_dst[i] : res_base + f.hdr_off + f.hdr_len;
         Event e;
         std::memset(&e.ev, 0, sizeof(e.ev));
         switch (f.kind) {
@@ -171,23 +252,21 @@ static void harvest(wsc_session* s, Conn& c, const uint8_t* seg, const wsc_seg_r
             if (f.flags & WSC_FF_CONT_MSG) {
                 e.data.swap(c.cont);
                 e.data.insert(e.data.end(), p, p + f.payload_len);
-            } else if (zero_copy) {
+            } else {
                 e.view = p;
                 e.view_len = f.payload_len;
-            } else {
-                e.data.assign(p, p + f.payload_len);
+                e.set = set;
+                views = true;
             }
             e.ev.type = WSC_EV_MESSAGE;
             e.ev.msg_id = f.msg_id;
             e.ev.opcode = f.mode;
             break;
         case WSC_FK_PING:                                     // websocket_ctrl.go:128-153
-            if (zero_copy) {
-                e.view = p;
-                e.view_len = f.payload_len;
-            } else {
-                e.data.assign(p, p + f.payload_len);
-            }
+            e.view = p;
+            e.view_len = f.payload_len;
+            e.set = set;
+            views = true;
             e.ev.type = WSC_EV_PONG;
             break;
         case WSC_FK_PONG:
@@ -209,100 +288,503 @@ static void harvest(wsc_session* s, Conn& c, const uint8_t* seg, const wsc_seg_r
         }
         c.pending.push_back(std::move(e));
     }
+    if (views) s->st[set].view_conns.push_back(slot);
     c.st = so;
-    if (r.status == WSC_SEG_OPEN) {
-        const uint64_t seg_len = c.carry.size() + c.fed.size();
-        std::vector<uint8_t> rest(seg + r.consumed, seg + seg_len);
-        c.carry.swap(rest);
+    if (r.status == WSC_SEG_OPEN) {   // the undecoded tail (still masked) goes in front of the next bytes
+        c.carry.assign(in_seg + r.consumed, in_seg + seg_len);   // (placing a segment emptied the carry)
     } else {
         c.carry.clear();
+        c.spill.clear();
         c.cont.clear();
     }
-    c.fed.clear();
 }
 
-int wsc_session_decode(wsc_session* s) {
-    if (!s) return WSC_E_INVAL;
-    const wsc_config& g = s->cfg;
-    std::vector<uint32_t> ids;
-    for (uint32_t i = 0; i < s->conns.size(); ++i) {
-        Conn& c = s->conns[i];
-        for (Event& e : c.pending)   // undrained zero-copy views: the staging is about to be reused
-            if (e.view) {
-                e.data.assign(e.view, e.view + e.view_len);
-                e.view = nullptr;
-            }
-        if (c.live && c.st.status == WSC_SEG_OPEN && !c.fed.empty()) ids.push_back(i);
+void fail_conn(wsc_session* s, Conn& c) {
+    (void)s;
+    c.failed = true;
+    Event e;
+    std::memset(&e.ev, 0, sizeof(e.ev));
+    e.ev.type = WSC_EV_CLOSE;
+    e.ev.close_code = 1011;   // RFC 6455 §7.4.1 internal error
+    e.ev.err = WSC_ERR_DEVICE;
+    c.pending.push_back(std::move(e));
+    c.st.status = WSC_SEG_ERROR;
+}
+
+// Synchronous decode of segments [a, b) of a completed-with-overflow staging set, re-read from the
+// masked input into the result buffer; halves until every part's records fit.
+int decode_range(wsc_session* s, int set, uint32_t a, uint32_t b, uint64_t prefix_limit);
+
+int decode_sync_part(wsc_session* s, int set, uint32_t a, uint32_t b, uint64_t prefix_limit) {
+    Stage& g = s->st[set];
+    const bool compact = (s->flags & WSC_F_COMPACT) != 0;
+    const uint64_t base = g.seg_start[a];
+    const uint32_t n = b - a;
+    std::vector<uint64_t> off(n + 1);
+    std::vector<wsc_conn_state> sin(n);
+    for (uint32_t q = 0; q < n; ++q) {
+        off[q] = g.seg_start[a + q] - base;
+        sin[q] = g.h_state_in[a + q];
     }
-    size_t k = 0;
-    while (k < ids.size()) {
-        // pack as many connections as fit into one device batch
-        const double t0 = s->timing ? now_s() : 0;
-        uint64_t bytes = 0;
-        uint32_t n = 0;
-        size_t j = k;
-        while (j < ids.size() && n < g.max_segs) {
-            const Conn& c = s->conns[ids[j]];
-            const uint64_t sl = c.carry.size() + c.fed.size();
-            if (sl > g.max_batch_bytes) return WSC_E_CAPACITY;
-            if (bytes + sl > g.max_batch_bytes && n > 0) break;
-            s->h_seg_off[n] = bytes;
-            uint8_t* dst = s->h_wire + bytes;
-            if (!c.carry.empty()) std::memcpy(dst, c.carry.data(), c.carry.size());
-            std::memcpy(dst + c.carry.size(), c.fed.data(), c.fed.size());
-            s->h_state_in[n] = c.st;
-            bytes += sl;
-            ++n;
-            ++j;
+    uint64_t end = g.seg_start[b - 1] + g.seg_len[b - 1] - base;
+    if (prefix_limit && n == 1 && prefix_limit < end) end = prefix_limit;
+    off[n] = end;
+    uint8_t* res = g.h_res + base;
+    if (!compact) std::memcpy(res, g.h_wire + base, end);
+    std::vector<wsc_conn_state> sout(n);
+    std::vector<wsc_seg_result> sres(n);
+    std::vector<wsc_frame> fr(s->cfg.max_frames);
+    std::vector<uint64_t> fd(compact ? s->cfg.max_frames : 0);
+    wsc_summary sm{};
+    // COMPACT: this part's arena lands at the same offset of the result buffer (arena <= wire bytes)
+    std::vector<uint8_t> wire_copy;
+    uint8_t* wire = res;
+    if (compact) {
+        wire_copy.assign(g.h_wire + base, g.h_wire + base + end);
+        wire = wire_copy.data();
+    }
+    const int rc = wsc_decode_host(g.ctx, wire, end, off.data(), n, s->flags, sin.data(), sout.data(), sres.data(),
+                                   fr.data(), s->cfg.max_frames, compact ? res : nullptr,
+                                   compact ? fd.data() : nullptr, &sm);
+    if (rc == WSC_E_CAPACITY && (sm.overflow & 1u)) {
+        if (n > 1) {
+            const uint32_t mid = a + n / 2;
+            const int r1 = decode_range(s, set, a, mid, 0);
+            if (r1) return r1;
+            return decode_range(s, set, mid, b, 0);
         }
-        s->h_seg_off[n] = bytes;
-        const double t1 = s->timing ? now_s() : 0;
-        wsc_summary sm;
-        int rc = wsc_decode_host(s->ctx, s->h_wire, bytes, s->h_seg_off, n, s->flags, s->h_state_in,
-                                 s->h_state_out, s->h_seg_out, s->h_frames, g.max_frames, s->h_arena,
-                                 s->h_frame_dst, &sm);
+        // one connection: decode the prefix that ends where its last reported frame begins
+        const uint64_t cut = fr[s->cfg.max_frames - 1].hdr_off;
+        if (cut == 0 || (prefix_limit && cut >= prefix_limit)) return WSC_E_CAPACITY;
+        return decode_range(s, set, a, b, cut);
+    }
+    if (rc) return rc;
+    for (uint32_t q = 0; q < n; ++q) {
+        const uint32_t h = g.seg_conn[a + q];
+        if (h == DEAD_SEG) continue;
+        Conn* c = lookup(s, h);
+        if (!c) continue;
+        const uint64_t seg_len = (q + 1 < n ? off[q + 1] : end) - off[q];
+        harvest(s, set, *c, h & SLOT_MASK, g.h_wire + base + off[q], res, seg_len, sres[q], sout[q],
+                fr.data(), compact ? fd.data() : nullptr, 0);
+        g.done[a + q] = 1;
+        if (n == 1 && end < g.seg_len[a]) {   // a prefix: the rest is decoded by the caller's next batch
+            std::vector<uint8_t> tail(g.h_wire + base + end, g.h_wire + base + g.seg_len[a]);
+            if (c->st.status == WSC_SEG_OPEN) c->spill.insert(c->spill.begin(), tail.begin(), tail.end());
+        }
+    }
+    // views handed out above point into res (in place) / the arena copy region: both in h_res
+    return WSC_OK;
+}
+
+int decode_range(wsc_session* s, int set, uint32_t a, uint32_t b, uint64_t prefix_limit) {
+    return decode_sync_part(s, set, a, b, prefix_limit);
+}
+
+int launch_stage(wsc_session* s, Stage& g) {
+    const bool compact = (s->flags & WSC_F_COMPACT) != 0;
+    const uint32_t n = (uint32_t)g.seg_conn.size();
+    hipStream_t st = g.stream;
+#define HT(x) do { if ((x) != hipSuccess) return WSC_E_DEVICE; } while (0)
+    HT(hipMemcpyAsync(g.d_wire, g.h_wire, g.bytes, hipMemcpyHostToDevice, st));
+    HT(hipMemcpyAsync(g.d_seg_off, g.h_seg_off, (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+    HT(hipMemcpyAsync(g.d_state_in, g.h_state_in, n * sizeof(wsc_conn_state), hipMemcpyHostToDevice, st));
+    wsc_batch b{};
+    b.wire = (uint8_t*)g.d_wire;
+    b.n_bytes = g.bytes;
+    b.seg_off = (const uint64_t*)g.d_seg_off;
+    b.n_segs = n;
+    b.flags = s->flags;
+    b.state_in = (const wsc_conn_state*)g.d_state_in;
+    b.state_out = (wsc_conn_state*)g.d_state_out;
+    b.seg_out = (wsc_seg_result*)g.d_seg_out;
+    b.frames = (wsc_frame*)g.d_frames;
+    b.frames_cap = s->cfg.max_frames;
+    b.arena = compact ? (uint8_t*)g.d_arena : nullptr;
+    b.frame_dst = compact ? (uint64_t*)g.d_frame_dst : nullptr;
+    b.summary = (wsc_summary*)g.d_summary;
+    const int rc = wsc_decode(g.ctx, &b, st);
+    if (rc) return rc;
+    HT(hipMemcpyAsync(g.h_summary, g.d_summary, sizeof(wsc_summary), hipMemcpyDeviceToHost, st));
+    HT(hipMemcpyAsync(g.h_state_out, g.d_state_out, n * sizeof(wsc_conn_state), hipMemcpyDeviceToHost, st));
+    HT(hipMemcpyAsync(g.h_seg_out, g.d_seg_out, n * sizeof(wsc_seg_result), hipMemcpyDeviceToHost, st));
+#undef HT
+    return WSC_OK;
+}
+
+void reset_stage(Stage& g) {
+    g.bytes = 0;
+    g.seg_conn.clear();
+    g.seg_start.clear();
+    g.seg_len.clear();
+    g.in_flight = false;
+    g.launch_rc = WSC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int wsc_session_destroy(wsc_session* s);
+
+int wsc_session_create(int device, const wsc_config* cfg, uint32_t flags, wsc_session** out) {
+    if (!out) return WSC_E_INVAL;
+    *out = nullptr;
+    wsc_session* s = new wsc_session();
+    if (cfg) s->cfg = *cfg; else wsc_config_default(&s->cfg);
+    wsc_config& g = s->cfg;
+    if (g.max_frames < 2 || g.max_segs < 2 || g.max_batch_bytes < 64) { delete s; return WSC_E_INVAL; }
+    // a frame that can never fit one batch closes its connection (WSC_ERR_TOO_LARGE) instead of
+    // holding every other connection of the session back
+    if (g.max_frame_len > g.max_batch_bytes - 14) g.max_frame_len = g.max_batch_bytes - 14;
+    s->flags = flags & WSC_F_COMPACT;
+    s->device = device;
+    int rc = WSC_OK;
+    for (Stage& t : s->st) {
+        if (rc == WSC_OK) rc = wsc_create(device, &g, &t.ctx);
+        if (rc) break;
+        if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&t.stream, hipStreamNonBlocking) != hipSuccess) {
+            rc = WSC_E_DEVICE;
+            break;
+        }
+        auto H = [&](uint64_t bytes) -> void* {
+            void* p = nullptr;
+            if (rc == WSC_OK) rc = wsc_host_alloc(bytes, &p);
+            return p;
+        };
+        auto D = [&](uint64_t bytes) -> void* {
+            void* p = nullptr;
+            if (rc == WSC_OK) rc = wsc_dev_alloc(t.ctx, bytes, &p);
+            return p;
+        };
+        t.h_wire = (uint8_t*)H(g.max_batch_bytes + 64);
+        t.h_res = (uint8_t*)H(g.max_batch_bytes + 64);
+        t.h_seg_off = (uint64_t*)H((g.max_segs + 1) * sizeof(uint64_t));
+        t.h_state_in = (wsc_conn_state*)H(g.max_segs * sizeof(wsc_conn_state));
+        t.h_state_out = (wsc_conn_state*)H(g.max_segs * sizeof(wsc_conn_state));
+        t.h_seg_out = (wsc_seg_result*)H(g.max_segs * sizeof(wsc_seg_result));
+        t.h_frames = (wsc_frame*)H((uint64_t)g.max_frames * sizeof(wsc_frame));
+        t.h_frame_dst = (uint64_t*)H((uint64_t)g.max_frames * sizeof(uint64_t));
+        t.h_summary = (wsc_summary*)H(sizeof(wsc_summary));
+        t.d_wire = D(g.max_batch_bytes + 64);
+        t.d_arena = D(g.max_batch_bytes + 64);
+        t.d_seg_off = D((g.max_segs + 1) * sizeof(uint64_t));
+        t.d_state_in = D(g.max_segs * sizeof(wsc_conn_state));
+        t.d_state_out = D(g.max_segs * sizeof(wsc_conn_state));
+        t.d_seg_out = D(g.max_segs * sizeof(wsc_seg_result));
+        t.d_frames = D((uint64_t)g.max_frames * sizeof(wsc_frame));
+        t.d_frame_dst = D((uint64_t)g.max_frames * sizeof(uint64_t));
+        t.d_summary = D(sizeof(wsc_summary));
+    }
+    if (rc) { wsc_session_destroy(s); return rc; }
+    if (const char* e = std::getenv("WSC_SESSION_TIMING"); e && e[0] == '1') s->timing = true;
+    if (const char* e = std::getenv("WSC_SESSION_FAULT"); e && *e) s->fault_at = std::strtoull(e, nullptr, 10);
+    *out = s;
+    return WSC_OK;
+}
+
+int wsc_session_destroy(wsc_session* s) {
+    if (!s) return WSC_OK;
+    if (s->timing)
+        fprintf(stderr, "wsc_session: %llu batches, %llu bytes: pack %.4f s, device (H2D+kernels+D2H) %.4f s, harvest %.4f s\n",
+                (unsigned long long)s->n_batches, (unsigned long long)s->n_bytes, s->t_pack, s->t_device, s->t_harvest);
+    for (Stage& t : s->st) {
+        if (t.stream) (void)hipStreamSynchronize(t.stream);
+        void* hs[] = {t.h_wire, t.h_res, t.h_seg_off, t.h_state_in, t.h_state_out, t.h_seg_out, t.h_frames,
+                      t.h_frame_dst, t.h_summary};
+        for (void* p : hs)
+            if (p) wsc_host_free(p);
+        if (t.ctx) {
+            void* ds[] = {t.d_wire, t.d_arena, t.d_seg_off, t.d_state_in, t.d_state_out, t.d_seg_out, t.d_frames,
+                          t.d_frame_dst, t.d_summary};
+            for (void* p : ds)
+                if (p) wsc_dev_free(t.ctx, p);
+        }
+        if (t.stream) (void)hipStreamDestroy(t.stream);
+        if (t.ctx) wsc_destroy(t.ctx);
+    }
+    delete s;
+    return WSC_OK;
+}
+
+int wsc_session_open(wsc_session* s, uint32_t* conn_out) {   // newWebsocketProtocol, websocket.go:59-79
+    if (!s || !conn_out) return WSC_E_INVAL;
+    apply_removes(s);
+    uint32_t slot;
+    if (!s->free_slots.empty()) {
+        slot = s->free_slots.back();
+        s->free_slots.pop_back();
+    } else {
+        if (s->conns.size() > SLOT_MASK) return WSC_E_CAPACITY;
+        slot = (uint32_t)s->conns.size();
+        s->conns.emplace_back();
+        s->n_slots.store((uint32_t)s->conns.size(), std::memory_order_release);
+    }
+    Conn& c = s->conns[slot];
+    const uint32_t gen = (c.gen + 1) & GEN_MASK;
+    c = Conn();
+    c.gen = gen;
+    c.live = true;
+    *conn_out = slot | gen << SLOT_BITS;
+    return WSC_OK;
+}
+
+// remove() (websocket_ctrl.go:73-96): safe from any thread; applied by the poller thread
+int wsc_session_remove(wsc_session* s, uint32_t conn) {
+    if (!s) return WSC_E_INVAL;
+    if ((conn & SLOT_MASK) >= s->n_slots.load(std::memory_order_acquire)) return WSC_E_STATE;
+    std::lock_guard<std::mutex> g(s->rm_mu);
+    s->rm_q.push_back(conn);
+    s->rm_pending.store(1, std::memory_order_release);
+    return WSC_OK;
+}
+
+int wsc_session_reserve(wsc_session* s, uint32_t conn, uint64_t max_bytes, uint8_t** ptr, uint64_t* avail) {
+    if (!s || !ptr || !avail) return WSC_E_INVAL;
+    apply_removes(s);
+    Conn* c = lookup(s, conn);
+    if (!c) return WSC_E_STATE;
+    *ptr = nullptr;
+    *avail = 0;
+    c->reserved = 0;
+    if (c->st.status != WSC_SEG_OPEN || c->failed || max_bytes == 0) return WSC_OK;   // closed: nothing to read into
+    Stage& f = s->st[s->fill];
+    const uint64_t cap = s->cfg.max_batch_bytes;
+    // straight into the staging being filled, right behind the connection's segment there (its
+    // carried bytes first); bytes already waiting in its spill keep the order, so they go first
+    if (c->spill.empty()) {
+        if (c->fill_epoch == s->fill_epoch && c->seg + 1 != f.seg_conn.size()) {
+            // read twice in one round and no longer the last segment: the old region becomes a dead
+            // segment and the bytes move to the end
+            const uint64_t a = f.seg_start[c->seg], n = f.seg_len[c->seg];
+            c->carry.assign(f.h_wire + a, f.h_wire + a + n);
+            f.seg_conn[c->seg] = DEAD_SEG;
+            c->fill_epoch = ~0ull;
+        }
+        if (place(s, *c, conn, 0)) {
+            const uint64_t room = cap > f.bytes ? cap - f.bytes : 0;
+            const uint64_t k = room < max_bytes ? room : max_bytes;
+            if (k >= max_bytes || k >= MIN_RESERVE) {
+                *ptr = f.h_wire + f.bytes;
+                *avail = k;
+                c->reserved = k;
+                c->reserved_spill = false;
+                return WSC_OK;
+            }
+        }
+    }
+    // otherwise into the connection's spill (decoded in a later batch)
+    const uint64_t at = c->spill.size();
+    c->spill.resize(at + max_bytes);
+    *ptr = c->spill.data() + at;
+    *avail = max_bytes;
+    c->reserved = max_bytes;
+    c->reserved_spill = true;
+    return WSC_OK;
+}
+
+int wsc_session_commit(wsc_session* s, uint32_t conn, uint64_t n) {
+    if (!s) return WSC_E_INVAL;
+    Conn* c = lookup(s, conn);
+    if (!c) return WSC_E_STATE;
+    if (n > c->reserved) return WSC_E_INVAL;
+    if (c->reserved_spill) {
+        c->spill.resize(c->spill.size() - (c->reserved - n));
+    } else if (c->reserved) {
+        Stage& f = s->st[s->fill];
+        f.seg_len[c->seg] += n;
+        f.bytes += n;
+    }
+    c->reserved = 0;
+    return WSC_OK;
+}
+
+int wsc_session_feed(wsc_session* s, uint32_t conn, const uint8_t* bytes, uint64_t n) {
+    if (!s) return WSC_E_INVAL;
+    if (n && !bytes) return WSC_E_INVAL;
+    while (n) {
+        uint8_t* p = nullptr;
+        uint64_t k = 0;
+        int rc = wsc_session_reserve(s, conn, n, &p, &k);
         if (rc) return rc;
-        const double t2 = s->timing ? now_s() : 0;
-        for (uint32_t q = 0; q < n; ++q) {
-            Conn& c = s->conns[ids[k + q]];
-            harvest(s, c, s->h_wire + s->h_seg_off[q], s->h_seg_out[q], s->h_state_out[q], s->h_seg_off[q],
-                    j == ids.size());
+        if (!p) return WSC_OK;   // closed / stalled: bytes are ignored
+        if (k > n) k = n;
+        std::memcpy(p, bytes, k);
+        rc = wsc_session_commit(s, conn, k);
+        if (rc) return rc;
+        bytes += k;
+        n -= k;
+    }
+    Conn* c = lookup(s, conn);
+    return c ? WSC_OK : WSC_E_STATE;
+}
+
+// Launch the staging being filled (async: H2D, walk + unmask, small D2H on its stream) and switch
+// filling to the other set.  Connections whose bytes wait in their spill are packed first.
+int wsc_session_submit(wsc_session* s) {
+    if (!s) return WSC_E_INVAL;
+    apply_removes(s);
+    if (s->st[0].in_flight || s->st[1].in_flight) return WSC_E_STATE;   // complete() first
+    const double t0 = s->timing ? now_s() : 0;
+    Stage& f = s->st[s->fill];
+    for (uint32_t slot = 0; slot < s->conns.size(); ++slot) {   // spilled bytes ride in this batch if they fit
+        Conn& c = s->conns[slot];
+        if (!c.live || c.failed || c.st.status != WSC_SEG_OPEN || c.spill.empty()) continue;
+        if (c.fill_epoch == s->fill_epoch) {
+            if (c.seg + 1 != f.seg_conn.size()) continue;   // not last: next batch
+            const uint64_t room = s->cfg.max_batch_bytes - f.bytes;
+            const uint64_t k = c.spill.size() < room ? c.spill.size() : room;
+            std::memcpy(f.h_wire + f.bytes, c.spill.data(), k);
+            c.spill.erase(c.spill.begin(), c.spill.begin() + (long)k);
+            f.seg_len[c.seg] += k;
+            f.bytes += k;
+        } else {
+            place(s, c, slot | c.gen << SLOT_BITS, 0);
         }
-        if (s->timing) {
-            const double t3 = now_s();
-            s->t_pack += t1 - t0;
-            s->t_device += t2 - t1;
-            s->t_harvest += t3 - t2;
-            s->n_decodes += 1;
-            s->n_bytes += bytes;
-        }
-        k = j;
+    }
+    const uint32_t n = (uint32_t)f.seg_conn.size();
+    if (n == 0) return WSC_OK;
+    for (uint32_t q = 0; q < n; ++q) {
+        s->st[s->fill].h_seg_off[q] = f.seg_start[q];
+        Conn* c = f.seg_conn[q] == DEAD_SEG ? nullptr : lookup(s, f.seg_conn[q]);
+        wsc_conn_state st{};
+        if (c) st = c->st;
+        else st.status = WSC_SEG_CLOSED;   // a dead region: the walk decodes nothing there
+        f.h_state_in[q] = st;
+    }
+    f.h_seg_off[n] = f.bytes;
+    const double t1 = s->timing ? now_s() : 0;
+    s->n_submits += 1;
+    f.launch_rc = (s->fault_at && s->n_submits == s->fault_at) ? WSC_E_DEVICE : launch_stage(s, f);
+    f.in_flight = true;
+    s->fill ^= 1;
+    s->fill_epoch += 1;
+    Stage& nf = s->st[s->fill];
+    reset_stage(nf);
+    if (s->timing) {
+        s->t_pack += t1 - t0;
+        s->n_batches += 1;
+        s->n_bytes += f.bytes;
     }
     return WSC_OK;
 }
 
+// Wait for the batch in flight and turn its records into events.  Event data handed out by the
+// previous complete() is materialised (copied) or dropped here: it stays valid until this call.
+int wsc_session_complete(wsc_session* s) {
+    if (!s) return WSC_E_INVAL;
+    apply_removes(s);
+    const int set = s->st[0].in_flight ? 0 : (s->st[1].in_flight ? 1 : -1);
+    if (set < 0) return WSC_OK;
+    Stage& g = s->st[set];
+    const bool compact = (s->flags & WSC_F_COMPACT) != 0;
+    const double t0 = s->timing ? now_s() : 0;
+    int rc = g.launch_rc;
+    if (rc == WSC_OK && hipStreamSynchronize(g.stream) != hipSuccess) rc = WSC_E_DEVICE;
+    if (rc == WSC_OK && (g.h_summary->overflow & 2u)) rc = WSC_E_INTERNAL;
+    const uint32_t n = (uint32_t)g.seg_conn.size();
+    g.done.assign(n, 0);
+    bool split = false;
+    if (rc == WSC_OK && (g.h_summary->overflow & 1u)) split = true;
+    uint32_t nf = 0;
+    if (rc == WSC_OK && !split) {
+        nf = g.h_summary->n_frames;
+        hipStream_t st = g.stream;
+        bool ok = true;
+        if (nf) ok = ok && hipMemcpyAsync(g.h_frames, g.d_frames, (uint64_t)nf * sizeof(wsc_frame), hipMemcpyDeviceToHost, st) == hipSuccess;
+        if (compact) {
+            const uint64_t ab = g.h_summary->data_bytes + g.h_summary->ctrl_bytes;
+            if (ab) ok = ok && hipMemcpyAsync(g.h_res, g.d_arena, ab, hipMemcpyDeviceToHost, st) == hipSuccess;
+            if (nf) ok = ok && hipMemcpyAsync(g.h_frame_dst, g.d_frame_dst, (uint64_t)nf * sizeof(uint64_t), hipMemcpyDeviceToHost, st) == hipSuccess;
+        } else if (g.bytes) {
+            ok = ok && hipMemcpyAsync(g.h_res, g.d_wire, g.bytes, hipMemcpyDeviceToHost, st) == hipSuccess;
+        }
+        ok = ok && hipStreamSynchronize(st) == hipSuccess;
+        if (!ok) rc = WSC_E_DEVICE;
+    }
+    const double t1 = s->timing ? now_s() : 0;
+    materialize_views(s, set ^ 1);   // the other set is filled next: its views must not dangle
+    g.view_conns.clear();
+    if (rc == WSC_OK && split) {
+        rc = decode_range(s, set, 0, n, 0);   // records exceeded max_frames: halves, synchronously
+    } else if (rc == WSC_OK) {
+        for (uint32_t q = 0; q < n; ++q) {
+            const uint32_t h = g.seg_conn[q];
+            if (h == DEAD_SEG) continue;
+            Conn* c = lookup(s, h);
+            if (!c) continue;   // removed while in flight
+            harvest(s, set, *c, h & SLOT_MASK, g.h_wire + g.seg_start[q], g.h_res, g.seg_len[q],
+                    g.h_seg_out[q], g.h_state_out[q], g.h_frames, compact ? g.h_frame_dst : nullptr, 0);
+            g.done[q] = 1;
+        }
+    }
+    if (rc != WSC_OK && rc != WSC_E_CAPACITY) {
+        // device failure: the batch's connections are closed (1011), their carried bytes kept
+        for (uint32_t q = 0; q < n; ++q) {
+            Conn* c = g.seg_conn[q] == DEAD_SEG ? nullptr : lookup(s, g.seg_conn[q]);
+            if (!c || g.done[q]) continue;   // (a split decode may have finished some before failing)
+            std::vector<uint8_t> keep(g.h_wire + g.seg_start[q], g.h_wire + g.seg_start[q] + g.seg_len[q]);
+            keep.insert(keep.end(), c->spill.begin(), c->spill.end());
+            c->carry.swap(keep);
+            c->spill.clear();
+            fail_conn(s, *c);
+        }
+    }
+    g.in_flight = false;
+    if (s->timing) {
+        const double t2 = now_s();
+        s->t_device += t1 - t0;
+        s->t_harvest += t2 - t1;
+    }
+    return rc;
+}
+
+// one batched device pass over everything fed so far (submit + complete until nothing is left)
+int wsc_session_decode(wsc_session* s) {
+    if (!s) return WSC_E_INVAL;
+    int rc = wsc_session_complete(s);   // a batch submitted earlier is finished first
+    if (rc) return rc;
+    for (int guard = 0; guard < 1 << 20; ++guard) {
+        rc = wsc_session_submit(s);
+        if (rc) return rc;
+        if (!s->st[0].in_flight && !s->st[1].in_flight) return WSC_OK;   // nothing was pending
+        rc = wsc_session_complete(s);
+        if (rc) return rc;
+        bool more = false;   // bytes left over (prefixes, spills that did not fit)
+        for (const Conn& c : s->conns)
+            if (c.live && !c.failed && c.st.status == WSC_SEG_OPEN && !c.spill.empty()) { more = true; break; }
+        if (!more) return WSC_OK;
+    }
+    return WSC_E_CAPACITY;
+}
+
 int wsc_session_next(wsc_session* s, uint32_t conn, wsc_event* ev) {
-    if (!s || !ev || conn >= s->conns.size() || !s->conns[conn].live) return WSC_E_STATE;
-    Conn& c = s->conns[conn];
+    if (!s || !ev) return WSC_E_INVAL;
+    apply_removes(s);
+    Conn* c = lookup(s, conn);
+    if (!c) return WSC_E_STATE;
     std::memset(ev, 0, sizeof(*ev));
-    if (c.pending.empty()) { ev->type = WSC_EV_NONE; return WSC_OK; }   // (nil, EAGAIN)
-    c.current = std::move(c.pending.front());
-    c.pending.pop_front();
-    *ev = c.current.ev;
-    if (c.current.view) {
-        ev->data = c.current.view_len ? c.current.view : nullptr;
-        ev->len = c.current.view_len;
+    if (c->pending.empty()) { ev->type = WSC_EV_NONE; return WSC_OK; }   // (nil, EAGAIN)
+    c->current = std::move(c->pending.front());
+    c->pending.pop_front();
+    *ev = c->current.ev;
+    if (c->current.view) {
+        ev->data = c->current.view_len ? c->current.view : nullptr;
+        ev->len = c->current.view_len;
     } else {
-        ev->data = c.current.data.empty() ? nullptr : c.current.data.data();
-        ev->len = c.current.data.size();
+        ev->data = c->current.data.empty() ? nullptr : c->current.data.data();
+        ev->len = c->current.data.size();
     }
     return WSC_OK;
 }
 
 int wsc_session_state(wsc_session* s, uint32_t conn, wsc_conn_state* st, uint64_t* carry_bytes) {
-    if (!s || conn >= s->conns.size() || !s->conns[conn].live) return WSC_E_STATE;
-    if (st) *st = s->conns[conn].st;
-    if (carry_bytes) *carry_bytes = s->conns[conn].carry.size();
+    if (!s) return WSC_E_INVAL;
+    apply_removes(s);
+    Conn* c = lookup(s, conn);
+    if (!c) return WSC_E_STATE;
+    if (st) *st = c->st;
+    if (carry_bytes) *carry_bytes = c->carry.size() + c->spill.size();
     return WSC_OK;
 }
 

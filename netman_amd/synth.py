@@ -111,6 +111,44 @@ def uniform_batch(n_frames, size, frames_per_seg, seed, opcode=OP_BIN):
                 n_frames=n_frames, payload_bytes=int(plen.sum()))
 
 
+def _splitmix64(x):
+    """vectorised splitmix64 finaliser (counter-based: value = f(seed, index), order-free)"""
+    x = np.asarray(x, dtype=np.uint64).copy()
+    with np.errstate(over="ignore"):
+        x += np.uint64(0x9E3779B97F4A7C15)
+        x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return x ^ (x >> np.uint64(31))
+
+
+def dealt_uniform_batch(n_frames_total, size, frames_per_seg, seed, world, rank, opcode=OP_BIN):
+    """Rank `rank`'s shard of ONE global batch of n_frames_total masked frames (configs[3]: 8 M x
+    4 KiB over 8 GPUs): global connection segment g (frames_per_seg frames each) goes to rank
+    shard.assign_segments(G, world)[g] = g mod world.  Every segment is generated from (seed, g)
+    alone -- mask of global frame f = splitmix64(seed ^ f), payload bytes from
+    default_rng([seed, g]) -- so the shards of all ranks are exactly split_batch() of the global
+    batch (tests/test_shard.py) while each rank only materialises its own segments."""
+    from netman_amd.shard import assign_segments
+    G = (n_frames_total + frames_per_seg - 1) // frames_per_seg
+    mine = np.nonzero(assign_segments(G, world) == rank)[0]
+    segf = np.minimum(frames_per_seg, n_frames_total - mine * frames_per_seg).astype(np.int64)
+    gframe = np.concatenate([g * frames_per_seg + np.arange(k, dtype=np.int64) for g, k in zip(mine, segf)]) \
+        if len(mine) else np.zeros(0, np.int64)
+    n = len(gframe)
+    b0 = np.full(n, 0x80 | opcode, dtype=np.uint8)
+    plen = np.full(n, size, dtype=np.uint64)
+    mask = (_splitmix64(np.uint64(seed) ^ gframe.astype(np.uint64)) & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+    wire, seg_off, poff = build_frames(b0, plen, mask, None, seg_frames=segf, fill=False)
+    hl = int(header_len(size))
+    for j, g in enumerate(mine):   # payload bytes of segment g: a function of (seed, g) only
+        a, b = int(seg_off[j]), int(seg_off[j + 1])
+        k = int(segf[j])
+        pay = np.frombuffer(np.random.default_rng([seed, int(g)]).bytes(k * size), np.uint8).reshape(k, size)
+        wire[a:b].reshape(k, hl + size)[:, hl:] = pay
+    return dict(wire=wire, seg_off=seg_off, payload_off=poff, plen=plen, mask=mask, segments=mine,
+                n_frames=n, payload_bytes=int(plen.sum()))
+
+
 def utf8_units(rng, n_units):
     """n_units random 4-byte units, each valid UTF-8 on its own: 4 ASCII, 2 x 2-byte (Greek),
     3-byte (CJK) + ASCII, or one 4-byte character (emoji) -- uint8[4 * n_units]."""

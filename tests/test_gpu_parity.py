@@ -269,6 +269,32 @@ def _device_batch(c, cfg, torch, compact=False):
     return b, t
 
 
+def _device_result(t, cfg, compact=False):
+    """the device batch's outputs as a DecodeResult (host copies)"""
+    summ = t["summ"].cpu().numpy().copy().view(K.SUMMARY_DTYPE)[0]
+    assert K.Codec.summary_status(summ) == K.WSC_OK
+    nf = int(summ["n_frames"])
+    return K.DecodeResult(seg=t["seg_out"].cpu().numpy().copy().view(K.SEG_RESULT_DTYPE),
+                          state=t["st_out"].cpu().numpy().copy().view(K.CONN_STATE_DTYPE),
+                          frames=t["frames"].cpu().numpy().copy().view(K.FRAME_DTYPE)[:nf], summary=summ,
+                          frame_dst=t["frame_dst"].cpu().numpy().copy().view(np.uint64)[:nf] if compact else None,
+                          arena=t["arena"].cpu().numpy().copy() if compact else None)
+
+
+def _oracle_sample(cfg, res, after, compact=False, n=2000, must=(), seed=0):
+    """record-by-record and byte-by-byte comparison with the oracle (O.run on the segment's own
+    masked bytes) for n sampled segments + the segments in `must` + the first and last ones"""
+    n_segs = len(cfg["seg_off"]) - 1
+    rng = np.random.default_rng(seed)
+    pick = set(rng.choice(n_segs, size=min(n, n_segs), replace=False).tolist()) | set(int(x) for x in must)
+    pick |= {0, n_segs - 1}
+    for i in sorted(pick):
+        a, b = int(cfg["seg_off"][i]), int(cfg["seg_off"][i + 1])
+        stream = bytes(cfg["wire"][a:b])
+        compare_segment(i, stream, a, res, O.run(stream), wire_after=after, compact=compact)
+    return len(pick)
+
+
 @pytest.mark.parametrize("per_seg", [16, 1])   # SURVEY §8(d): 64 k connections x 16 frames, and 1 frame per segment
 def test_config1_1m_x_1k_frames(codec_lib, per_seg):
     torch = pytest.importorskip("torch")
@@ -277,9 +303,12 @@ def test_config1_1m_x_1k_frames(codec_lib, per_seg):
     b, t = _device_batch(c, cfg, torch)
     c.decode(b)
     c.sync()
-    assert np.array_equal(t["wire"].cpu().numpy().copy(), synth.unmask_uniform(cfg))
-    fr = t["frames"].cpu().numpy().copy().view(K.FRAME_DTYPE)[: 1 << 20]
-    assert (fr["kind"] == K.FK_MESSAGE).all() and (fr["hdr_len"] == 8).all()
+    after = t["wire"].cpu().numpy().copy()
+    assert np.array_equal(after, synth.unmask_uniform(cfg))
+    res = _device_result(t, cfg)
+    fr = res.frames
+    assert len(fr) == 1 << 20 and (fr["kind"] == K.FK_MESSAGE).all() and (fr["hdr_len"] == 8).all()
+    assert _oracle_sample(cfg, res, after, n=2000 // per_seg * per_seg) >= 2000
     c.close()
 
 
@@ -291,8 +320,13 @@ def test_config2_mixed_power_law(codec_lib, per_seg):
     b, t = _device_batch(c, cfg, torch)
     c.decode(b)
     c.sync()
+    after = t["wire"].cpu().numpy().copy()
     ref = synth.unmask_reference(cfg["wire"], cfg["payload_off"], cfg["plen"], cfg["mask"])
-    assert np.array_equal(t["wire"].cpu().numpy().copy(), ref)
+    assert np.array_equal(after, ref)
+    # every segment that holds a 1 MiB frame (6 / 8 / 14-byte headers side by side), + 2000 more
+    big = np.nonzero(cfg["plen"] == 1048576)[0] // per_seg
+    res = _device_result(t, cfg)
+    assert _oracle_sample(cfg, res, after, must=big, seed=2) >= 2000
     c.close()
 
 
@@ -352,6 +386,9 @@ def test_config4_fragmented_reassembly(codec_lib, ping_p):
         p, L = int(cfg["payload_off"][i]), int(cfg["plen"][i])
         assert np.array_equal(arena[int(dst[i]):int(dst[i]) + L], ref[p:p + L]), \
             (i, int(dst[i]), p, L, fr[i - 2:i + 3], dst[i - 2:i + 3], cfg["plen"][i - 2:i + 3])
+    # record by record against the oracle (MsgIDs across PINGs, Q5) on 2,000 sampled connections
+    res = _device_result(t, cfg, compact=True)
+    assert _oracle_sample(cfg, res, t["wire"].cpu().numpy().copy(), compact=True, seed=4) >= 2000
     c.close()
 
 
@@ -475,3 +512,39 @@ def test_decode_split_pipeline_matches_oracle(codec_lib, compact, layout, inline
             ctxs[0].stream_destroy(s)
         for c in ctxs:
             c.close()
+
+
+# ---- multi-GPU sharding: shards decoded independently == the unsharded decode ----
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_sharded_decode_equals_unsharded(codec, world):
+    """one global batch of fuzz connections split with shard.split_batch (connection c -> rank
+    c mod world), every shard decoded on its own (device 0 stands in for device r), the shards'
+    records and bytes merged back by connection: identical to decoding the whole batch at once,
+    and to the oracle -- no cross-shard state exists (no collective needed)"""
+    from netman_amd import shard
+    streams = [random_stream(13000 + i, n_units=int(3 + i % 25)) for i in range(240)]
+    wire, off = pack_streams(streams)
+    whole_wire = wire.copy()
+    whole = codec.decode_host(whole_wire, off)
+    assert K.Codec.summary_status(whole.summary) == K.WSC_OK
+    merged_wire = np.empty_like(wire)
+    for r in range(world):
+        w, so, mine = shard.split_batch(wire, off, world, r)
+        w = w.copy()
+        res = codec.decode_host(w, so)
+        for j, g in enumerate(mine):
+            a, b = int(off[g]), int(off[g + 1])
+            merged_wire[a:b] = w[int(so[j]):int(so[j + 1])]
+            # records: same fields as the unsharded decode's, offsets rebased to the global batch
+            sr, wr = res.seg[j], whole.seg[g]
+            for f in ("consumed", "frame_count", "status", "close_code", "err"):
+                assert int(sr[f]) == int(wr[f]), (g, f)
+            fs = res.frames[int(sr["frame_begin"]):int(sr["frame_begin"]) + int(sr["frame_count"])].copy()
+            fw = whole.frames[int(wr["frame_begin"]):int(wr["frame_begin"]) + int(wr["frame_count"])].copy()
+            fs["hdr_off"] += np.uint64(a) - so[j]
+            fs["seg"] = g
+            assert np.array_equal(fs, fw), g
+            assert np.array_equal(res.state[j], whole.state[g])
+    assert np.array_equal(merged_wire, whole_wire)
+    for i, s in enumerate(streams):
+        compare_segment(i, s, int(off[i]), whole, O.run(s), wire_after=whole_wire)

@@ -61,3 +61,17 @@ def test_gloo_two_ranks():
     assert [r[2] for r in res] == [2.0, 2.0]        # max over ranks
     assert res[0][3] != res[1][3]                   # independent shards
     assert abs(shard.aggregate_rate([2**30, 2**30], 1.0, 1) - 2.0) < 1e-9
+
+
+def test_dealt_shards_are_split_of_global_batch():
+    """configs[3] shards: each rank's dealt_uniform_batch == split_batch of the one global batch"""
+    glob = synth.dealt_uniform_batch(1000, 256, 7, seed=99, world=1, rank=0)
+    for world in (2, 3, 4):
+        for r in range(world):
+            part = synth.dealt_uniform_batch(1000, 256, 7, seed=99, world=world, rank=r)
+            w, off, mine = shard.split_batch(glob["wire"], glob["seg_off"], world, r)
+            assert np.array_equal(mine, part["segments"])
+            assert np.array_equal(off, part["seg_off"]) and np.array_equal(w, part["wire"])
+    # the headers/masks decode like any other batch: the numpy restatement unmasks the payload
+    ref = synth.unmask_reference(glob["wire"], glob["payload_off"], glob["plen"], glob["mask"])
+    assert np.array_equal(synth.unmask_uniform(glob), ref)
