@@ -521,25 +521,27 @@ def encode_configs(torch, K, synth):
 def echo_configs(with_cpu=True):
     """configs[0]: examples/websocket echo on loopback, rebuilt around a pluggable decoder
     (tools/echo_harness.hpp; the Go reference server cannot run here).  gpu = tools/ws_echo
-    (libwscodec wsc_session, one device decode per poller round); cpu = oracle/_build/ws_echo_cpu,
+    (libwscodec wsc_session: recv straight into pinned staging, round r+1 submitted to the device
+    while round r is echoed); gpu_sync = the same with one synchronous decode per round; cpu = oracle/_build/ws_echo_cpu,
     the reference's frame-at-a-time decode ported to C++ (cpu_baseline leg, kind "port").  Each
     run is a separate process; msgs/s and GiB/s of echoed payload, every byte checked."""
     import subprocess
     runs = [("1 conn x 4000 x 64 KiB (configs[0])", ["--conns", "1", "--frames", "4000", "--size", "65536"]),
             ("64 conns x 200 x 64 KiB", ["--conns", "64", "--frames", "200", "--size", "65536", "--client-threads", "4"]),
             ("64 conns x 2000 x 1 KiB", ["--conns", "64", "--frames", "2000", "--size", "1024", "--client-threads", "4"])]
-    bins = [("gpu", os.path.join(ROOT, "tools", "ws_echo"))]
+    bins = [("gpu", os.path.join(ROOT, "tools", "ws_echo"), []),
+            ("gpu_sync", os.path.join(ROOT, "tools", "ws_echo"), ["--sync"])]
     if with_cpu:
-        bins.append(("cpu_port", os.path.join(ROOT, "oracle", "_build", "ws_echo_cpu")))
+        bins.append(("cpu_port", os.path.join(ROOT, "oracle", "_build", "ws_echo_cpu"), []))
     res = {}
     for name, args in runs:
         row = {}
-        for kind, exe in bins:
+        for kind, exe, extra in bins:
             if not os.path.exists(exe):
                 row[kind] = None
                 continue
             try:
-                p = subprocess.run([exe] + args, capture_output=True, text=True, timeout=120)
+                p = subprocess.run([exe] + args + extra, capture_output=True, text=True, timeout=120)
                 line = [x for x in p.stdout.splitlines() if x.startswith("{")]
                 d = json.loads(line[-1]) if line else {"ok": False, "error": p.stderr[-300:]}
                 row[kind] = {k: d.get(k) for k in ("ok", "gib_s", "msgs_per_s", "seconds", "rounds", "error")}

@@ -1,0 +1,234 @@
+"""wsc_session (the per-connection DecodePacket mirror above the C ABI) on the GPU: per-connection
+capacity, cross-thread removal, device-failure policy, zero-copy reserve/commit and the
+double-buffered submit/complete cycle.  Every delivered event is compared with the oracle run on
+the connection's whole stream (the reference's DecodePacket + epoll.go:104-140)."""
+import threading
+
+import numpy as np
+import pytest
+
+import oracle_ref as O
+from fuzz_streams import random_stream, random_splits
+from gpu_helpers import events_of_session
+from netman_amd import codec as K
+from netman_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _oracle_keys(stream, max_frame_len=0x7FFFFFFF):
+    return [e.key() for e in O.run(stream, max_frame_len=max_frame_len).events]
+
+
+def _read(sess, c, chunk):
+    """one socket read into the pinned staging (reserve/commit may hand out less room than asked)"""
+    k = 0
+    while k < len(chunk):
+        took = sess.reserve_commit(c, chunk[k:])
+        if took == 0:     # closed / stalled connection: the bytes are ignored (no room handed out)
+            return
+        k += took
+
+
+def _drive(sess, streams, rng, zero_copy=False, max_chunks=5):
+    """feed each stream in random chunks over several rounds (one read per connection per
+    round), decode every round, collect each connection's events"""
+    conns = [sess.open() for _ in streams]
+    splits = [random_splits(rng, len(s), int(rng.integers(0, max_chunks + 1))) for s in streams]
+    got = {c: [] for c in conns}
+    prev = [0] * len(streams)
+    for r in range(max(len(sp) for sp in splits)):
+        for i, (c, s, sp) in enumerate(zip(conns, streams, splits)):
+            if r < len(sp):
+                chunk = s[prev[i]:sp[r]]
+                if zero_copy:
+                    _read(sess, c, chunk)
+                else:
+                    sess.feed(c, chunk)
+                prev[i] = sp[r]
+        sess.decode()
+        for c in conns:
+            got[c].extend(events_of_session(sess, c))
+    return conns, got
+
+
+@pytest.mark.parametrize("compact,zero_copy", [(False, True), (True, True), (False, False)])
+def test_reserve_commit_matches_oracle(codec_lib, compact, zero_copy):
+    rng = np.random.default_rng(21)
+    sess = K.Session(0, compact=compact, max_batch_bytes=16 << 20, max_segs=1024, max_frames=1 << 16)
+    streams = [random_stream(21000 + i, n_units=25) for i in range(150)]
+    conns, got = _drive(sess, streams, rng, zero_copy=zero_copy)
+    for i, (c, s) in enumerate(zip(conns, streams)):
+        assert got[c] == _oracle_keys(s), f"stream {i}"
+    sess.close()
+
+
+def test_oversized_connection_does_not_stall_others(codec_lib):
+    """one connection's huge frame must not stop the session.  max_batch_bytes
+    1 MiB: a 3 MiB frame can never fit a batch -> that connection closes with TOO_LARGE / 1002
+    (Q4 divergence, clamp at create); a 900 KiB frame fed in pieces fits and is delivered; a
+    connection sending 5 MiB of small frames in ONE read is decoded over several batches; the
+    ordinary connections decode every round throughout."""
+    sess = K.Session(0, max_batch_bytes=1 << 20, max_segs=64, max_frames=1 << 14)
+    rng = np.random.default_rng(5)
+    huge = synth.frame(2, rng.bytes(3 << 20), mask=0x01020304) + synth.frame(2, b"after", mask=5)
+    big = synth.frame(2, rng.bytes(900 << 10), mask=0x0A0B0C0D) + synth.frame(1, b"ok", mask=6)
+    many = b"".join(synth.frame(2, rng.bytes(int(rng.integers(0, 2000))), mask=int(rng.integers(0, 2**32)))
+                    for _ in range(5000))
+    normal = [random_stream(22000 + i, n_units=20) for i in range(20)]
+    streams = [huge, big, many] + normal
+    conns = [sess.open() for _ in streams]
+    got = {c: [] for c in conns}
+    pos = [0] * len(streams)
+    for r in range(12):
+        for i, (c, s) in enumerate(zip(conns, streams)):
+            step = len(s) if i == 2 else max(1, len(s) // 10)   # `many` arrives in one read
+            chunk = s[pos[i]:pos[i] + step]
+            if chunk:
+                sess.feed(c, chunk)
+                pos[i] += len(chunk)
+        sess.decode()
+        for c in conns:
+            got[c].extend(events_of_session(sess, c))
+    limit = (1 << 20) - 14
+    for i, (c, s) in enumerate(zip(conns, streams)):
+        assert got[c] == _oracle_keys(s, max_frame_len=limit), f"stream {i}"
+    ev0 = got[conns[0]]
+    assert len(ev0) == 1 and ev0[0][0] == K.EV_CLOSE and ev0[0][3] == 1002 and ev0[0][4] == K.ERR_TOO_LARGE
+    assert len(got[conns[2]]) == 5000 and len(got[conns[1]]) == 2
+    sess.close()
+
+
+def test_frame_records_overflow_splits_batch(codec_lib):
+    """more frame records in one batch than max_frames: the batch is re-decoded in halves (one
+    connection: a prefix ending at a frame boundary), nothing is lost or reordered"""
+    sess = K.Session(0, max_batch_bytes=8 << 20, max_segs=64, max_frames=1024)
+    rng = np.random.default_rng(9)
+    streams = [b"".join(synth.frame(2, rng.bytes(int(rng.integers(0, 40))), mask=int(rng.integers(0, 2**32)))
+                        for _ in range(n)) for n in (5000, 700, 700, 3000)]
+    streams += [random_stream(23000 + i, n_units=10) for i in range(8)]
+    conns = [sess.open() for _ in streams]
+    for c, s in zip(conns, streams):
+        sess.feed(c, s)
+    sess.decode()
+    for i, (c, s) in enumerate(zip(conns, streams)):
+        assert events_of_session(sess, c) == _oracle_keys(s), f"stream {i}"
+    sess.close()
+
+
+def test_remove_from_another_thread(codec_lib):
+    """remove() (websocket_ctrl.go:73-96) called from a handler thread while the poller thread
+    feeds and decodes: removed handles become invalid, nothing more is delivered for them, the
+    other connections decode exactly as the oracle says; a stale handle never touches the slot's
+    next connection"""
+    sess = K.Session(0, max_batch_bytes=8 << 20, max_segs=512, max_frames=1 << 15)
+    streams = [random_stream(24000 + i, n_units=30) for i in range(200)]
+    conns = [sess.open() for _ in streams]
+    doomed = set(conns[::3])
+    got = {c: [] for c in conns}
+    go = threading.Event()
+
+    def handler():
+        go.wait()
+        for c in list(doomed):
+            sess.remove(c)
+            sess.remove(c)          # Close() twice: harmless
+
+    t = threading.Thread(target=handler)
+    t.start()
+    rng = np.random.default_rng(3)
+    splits = [random_splits(rng, len(s), 4) for s in streams]
+    prev = [0] * len(streams)
+    for r in range(5):
+        if r == 2:
+            go.set()
+        for i, (c, s, sp) in enumerate(zip(conns, streams, splits)):
+            if r < len(sp):
+                try:
+                    sess.feed(c, s[prev[i]:sp[r]])
+                except K.WscError:
+                    assert c in doomed
+                prev[i] = sp[r]
+        sess.decode()
+        for c in conns:
+            try:
+                got[c].extend(events_of_session(sess, c))
+            except K.WscError:
+                assert c in doomed
+    t.join()
+    for i, (c, s) in enumerate(zip(conns, streams)):
+        ref = _oracle_keys(s)
+        if c in doomed:
+            assert got[c] == ref[:len(got[c])]          # a prefix, then nothing
+            with pytest.raises(K.WscError):
+                sess.next_event(c)
+        else:
+            assert got[c] == ref, f"stream {i}"
+    # stale handles: the slots are reused by new connections with a new generation
+    fresh = [sess.open() for _ in doomed]
+    for c in doomed:
+        sess.remove(c)             # stale: must not close the slot's new connection
+    sess.feed(fresh[0], synth.frame(2, b"still here", mask=7))
+    sess.decode()
+    assert [e.data for e in sess.events(fresh[0])] == [b"still here"]
+    sess.close()
+
+
+def test_device_failure_closes_only_that_batch(codec_lib, monkeypatch):
+    """WSC_SESSION_FAULT=2 fails the second device batch as a device error would: decode()
+    reports it, exactly that batch's connections get CLOSE 1011 / WSC_ERR_DEVICE with their
+    bytes kept, every later batch and every other connection decodes normally"""
+    monkeypatch.setenv("WSC_SESSION_FAULT", "2")
+    sess = K.Session(0, max_batch_bytes=4 << 20, max_segs=256, max_frames=1 << 14)
+    a = [sess.open() for _ in range(4)]
+    for c in a:
+        sess.feed(c, synth.frame(2, b"round1", mask=1))
+    sess.decode()                                   # batch 1: fine
+    for c in a:
+        assert [e.data for e in sess.events(c)] == [b"round1"]
+    for c in a[:2]:
+        sess.feed(c, synth.frame(2, b"round2", mask=2) + synth.frame(2, b"x")[:5])
+    with pytest.raises(K.WscError) as ei:
+        sess.decode()                               # batch 2: injected device failure
+    assert ei.value.rc == K.WSC_E_DEVICE
+    for c in a[:2]:
+        evs = sess.events(c)
+        assert [(e.type, e.close_code, e.err) for e in evs] == [(K.EV_CLOSE, 1011, K.ERR_DEVICE)]
+        st, carry = sess.state(c)
+        assert st.status == K.SEG_ERROR and carry > 0      # carried bytes kept
+        sess.feed(c, synth.frame(2, b"ignored"))            # a failed connection decodes nothing more
+    for c in a[2:]:
+        sess.feed(c, synth.frame(2, b"round3", mask=3))
+    sess.decode()                                   # batch 3: fine again
+    for c in a[2:]:
+        assert [e.data for e in sess.events(c)] == [b"round3"]
+    for c in a[:2]:
+        assert sess.events(c) == []
+    sess.close()
+
+
+def test_submit_complete_double_buffered(codec_lib):
+    """the echo poller's cycle: read round r+1, submit it, drain round r while the device works,
+    complete r+1.  Round r's message views stay valid until complete(r+1)."""
+    rng = np.random.default_rng(17)
+    sess = K.Session(0, max_batch_bytes=8 << 20, max_segs=256, max_frames=1 << 15)
+    streams = [random_stream(25000 + i, n_units=30) for i in range(64)]
+    conns = [sess.open() for _ in streams]
+    splits = [random_splits(rng, len(s), 6) for s in streams]
+    prev = [0] * len(streams)
+    got = {c: [] for c in conns}
+    rounds = max(len(sp) for sp in splits)
+    for r in range(rounds + 1):
+        for i, (c, s, sp) in enumerate(zip(conns, streams, splits)):
+            if r < len(sp):
+                _read(sess, c, s[prev[i]:sp[r]])
+                prev[i] = sp[r]
+        sess.submit()                                 # round r on the device
+        for c in conns:                               # round r-1's events, read after the submit
+            got[c].extend(events_of_session(sess, c))
+        sess.complete()
+    for c in conns:
+        got[c].extend(events_of_session(sess, c))
+    for i, (c, s) in enumerate(zip(conns, streams)):
+        assert got[c] == _oracle_keys(s), f"stream {i}"
+    sess.close()

@@ -41,6 +41,13 @@ struct Decoder {
     virtual void feed(int conn, const uint8_t* p, size_t n) = 0;          // one bulk read
     virtual void decode() = 0;                                            // once per poller round
     virtual bool next(int conn, const uint8_t** data, size_t* len) = 0;   // DecodePacket() -> message
+    // optional zero-copy read: room for the connection's next read (recv straight into it)
+    virtual bool reserve(int, size_t, uint8_t**, size_t*) { return false; }
+    virtual void commit(int, size_t) {}
+    // optional double buffering: submit(r+1), echo round r, complete(r+1)
+    virtual bool pipelined() const { return false; }
+    virtual void submit() { decode(); }
+    virtual void complete() {}
 };
 
 struct Result {
@@ -234,28 +241,12 @@ inline Result run(Decoder& dec, int conns, int frames, size_t frame_bytes, int c
     const auto t0 = std::chrono::steady_clock::now();
     go = true;
     const auto deadline = t0 + std::chrono::seconds(timeout_s);
-    while (res.error.empty() && served < want && client_fail.load() == 0) {
-        if (std::chrono::steady_clock::now() > deadline) {
-            res.error = "server timeout";
-            break;
-        }
-        const int n = epoll_wait(ep, evs, 1024, 100);
-        fed.clear();
-        for (int k = 0; k < n; ++k) {
-            ServerConn& c = sc[evs[k].data.u64];
-            if (evs[k].events & EPOLLIN) {
-                const ssize_t r = recv(c.fd, rb.data(), rb.size(), 0);   // ONE bulk read per event
-                if (r > 0) {
-                    dec.feed(c.id, rb.data(), (size_t)r);
-                    fed.push_back(evs[k].data.u64);
-                }
-            }
-        }
-        if (!fed.empty()) {
-            dec.decode();
-            res.rounds++;
-        }
-        for (size_t q : fed) {   // drain the round: every delivered message is echoed
+    // pipelined decoders: round r+1's reads are submitted to the device before round r's messages
+    // are echoed, so the device decodes while this thread builds and sends the replies
+    const bool pipe = dec.pipelined();
+    std::vector<size_t> drain;   // connections whose messages are ready to echo (previous round)
+    auto echo_round = [&](const std::vector<size_t>& conns_ready) {
+        for (size_t q : conns_ready) {   // every delivered message is echoed
             ServerConn& c = sc[q];
             const uint8_t* d;
             size_t len;
@@ -267,6 +258,47 @@ inline Result run(Decoder& dec, int conns, int frames, size_t frame_bytes, int c
                 served++;
                 res.payload_bytes += len;
             }
+        }
+    };
+    while (res.error.empty() && served < want && client_fail.load() == 0) {
+        if (std::chrono::steady_clock::now() > deadline) {
+            res.error = "server timeout";
+            break;
+        }
+        const int n = epoll_wait(ep, evs, 1024, pipe && !drain.empty() ? 0 : 100);
+        fed.clear();
+        for (int k = 0; k < n; ++k) {
+            ServerConn& c = sc[evs[k].data.u64];
+            if (evs[k].events & EPOLLIN) {
+                uint8_t* p = nullptr;
+                size_t avail = 0;
+                if (dec.reserve(c.id, rb.size(), &p, &avail)) {   // ONE bulk read per event, into pinned staging
+                    const ssize_t r = recv(c.fd, p, avail, 0);
+                    dec.commit(c.id, r > 0 ? (size_t)r : 0);
+                    if (r > 0) fed.push_back(evs[k].data.u64);
+                } else {
+                    const ssize_t r = recv(c.fd, rb.data(), rb.size(), 0);   // ONE bulk read per event
+                    if (r > 0) {
+                        dec.feed(c.id, rb.data(), (size_t)r);
+                        fed.push_back(evs[k].data.u64);
+                    }
+                }
+            }
+        }
+        if (pipe) {
+            if (!fed.empty()) {
+                dec.submit();          // round r+1 on the device ...
+                res.rounds++;
+            }
+            echo_round(drain);         // ... while round r is echoed
+            dec.complete();
+            drain = fed;
+        } else {
+            if (!fed.empty()) {
+                dec.decode();
+                res.rounds++;
+            }
+            echo_round(fed);
         }
         for (size_t i = 0; i < sc.size(); ++i) {
             ServerConn& c = sc[i];

@@ -2,7 +2,7 @@
 // (the DecodePacket mirror above the C ABI) decodes every round's bulk reads in ONE batched device
 // pass on the MI355X.  Harness: tools/echo_harness.hpp.  The CPU baseline twin is
 // oracle/ws_echo_cpu.cpp.  Prints one JSON line.
-//   ws_echo [--conns C] [--frames N] [--size BYTES] [--client-threads T]
+//   ws_echo [--conns C] [--frames N] [--size BYTES] [--client-threads T] [--sync]
 #include "../include/wscodec.h"
 #include "echo_harness.hpp"
 
@@ -29,12 +29,25 @@ struct GpuDecoder : echo::Decoder {
         return (int)id;
     }
     void feed(int conn, const uint8_t* p, size_t n) override { wsc_session_feed(s, (uint32_t)conn, p, n); }
-    void decode() override {
-        if (wsc_session_decode(s) != WSC_OK) {
-            fprintf(stderr, "wsc_session_decode: %s\n", wsc_last_error());
+    // recv() straight into the session's pinned staging (the only host copy of inbound bytes)
+    bool reserve(int conn, size_t max, uint8_t** p, size_t* avail) override {
+        uint64_t a = 0;
+        if (wsc_session_reserve(s, (uint32_t)conn, max, p, &a) != WSC_OK || !*p) return false;
+        *avail = (size_t)a;
+        return true;
+    }
+    void commit(int conn, size_t n) override { wsc_session_commit(s, (uint32_t)conn, n); }
+    bool pipelined() const override { return pipe; }
+    void submit() override { check(wsc_session_submit(s), "wsc_session_submit"); }
+    void complete() override { check(wsc_session_complete(s), "wsc_session_complete"); }
+    void decode() override { check(wsc_session_decode(s), "wsc_session_decode"); }
+    static void check(int rc, const char* what) {
+        if (rc != WSC_OK) {
+            fprintf(stderr, "%s: %s\n", what, wsc_last_error());
             exit(3);
         }
     }
+    bool pipe = true;
     bool next(int conn, const uint8_t** data, size_t* len) override {
         while (true) {
             wsc_session_next(s, (uint32_t)conn, &ev);
@@ -55,7 +68,11 @@ int main(int argc, char** argv) {
     size_t size = 65536;
     echo::parse_args(argc, argv, conns, frames, size, threads);
     GpuDecoder d(conns);
+    for (int i = 1; i < argc; ++i)
+        if (std::string(argv[i]) == "--sync") d.pipe = false;   // one synchronous decode per round
     const echo::Result r = echo::run(d, conns, frames, size, threads);
-    echo::print_json("gpu: libwscodec wsc_session (one device decode per poller round)", r, conns, frames, size);
+    echo::print_json(d.pipe ? "gpu: libwscodec wsc_session, recv into pinned staging, submit r+1 / echo r / complete"
+                            : "gpu: libwscodec wsc_session, one synchronous device decode per poller round",
+                     r, conns, frames, size);
     return r.ok ? 0 : 1;
 }
