@@ -67,7 +67,7 @@ struct wsc_ctx {
     U8Seg* u8seg = nullptr;
     uint32_t u8_inline_max = 256;
     uint32_t u8_grid = 0;               // WSC_U8_GRID: k_u8_check workgroups (A/B experiments; 0 = 5 per CU)
-    int walk_krec = 0;                  // WSC_WALK_KREC: 16 or 4 pins that walk instance (A/B, tests); 0 = auto
+    int walk_krec = 0;                  // WSC_WALK_KREC: 16, 8 or 2 pins that walk instance (A/B, tests); 0 = auto
     uint64_t tile_entries = 0;
     // host-staged path buffers (lazily allocated)
     uint8_t* d_wire = nullptr;
@@ -185,8 +185,10 @@ int wsc_create(int device, const wsc_config* cfg_in, wsc_ctx** out) {
     chk(hipMalloc(&c->u8maps, (uint64_t)c->u8items_cap * sizeof(uint64_t)), "hipMalloc u8maps");
     chk(hipMalloc(&c->u8seg, (uint64_t)cfg.max_segs * sizeof(U8Seg)), "hipMalloc u8seg");
     if (const char* e = std::getenv("WSC_U8_GRID"); e && *e) c->u8_grid = (uint32_t)std::strtoul(e, nullptr, 10);
-    if (const char* e = std::getenv("WSC_WALK_KREC"); e && *e)
-        c->walk_krec = std::atoi(e) == 4 ? 4 : 16;
+    if (const char* e = std::getenv("WSC_WALK_KREC"); e && *e) {   // pin an instance (tests, A/B)
+        const int k = std::atoi(e);
+        c->walk_krec = k <= 2 ? 2 : (k <= 8 ? 8 : 16);
+    }
     if (const char* e = std::getenv("WSC_U8_INLINE_MAX"); e && *e)   // test knob: 0 sends all text chip-wide
         c->u8_inline_max = (uint32_t)std::strtoul(e, nullptr, 10);
     c->enc_blocks = (cfg.max_frames + 255) / 256 + 1;
@@ -304,13 +306,18 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     // (an event never recorded is a no-op wait)
     const hipStream_t ws = split ? sw : st;
     if (split) HIP_TRY(hipStreamWaitEvent(ws, c->ev_done, 0));
-    // more walk blocks than 2 per CU (the KR = 16 instance's LDS residency): the KR = 4 instance
-    const bool short_segs = c->walk_krec ? c->walk_krec == 4 : wgrid.x > 2u * (uint32_t)c->n_cu;
+    // frame records kept in LDS per lane (KR): 16 (~138 KiB of LDS, one block per CU) while the
+    // blocks fit the CUs at once; 8 (two per CU) up to twice that; 2 for batches of many short
+    // segments (VGPR-bound residency).  Segments with more frames re-walk their headers to emit.
+    uint32_t kr = wgrid.x <= (uint32_t)c->n_cu ? 16u : (wgrid.x <= 2u * (uint32_t)c->n_cu ? 8u : 2u);
+    if (c->walk_krec) kr = (uint32_t)c->walk_krec;
     if (compact) {
-        if (short_segs) hipLaunchKernelGGL((k_walk_fused<true, 4>), wgrid, wblk, 0, ws, wa);
+        if (kr == 2) hipLaunchKernelGGL((k_walk_fused<true, 2>), wgrid, wblk, 0, ws, wa);
+        else if (kr == 8) hipLaunchKernelGGL((k_walk_fused<true, 8>), wgrid, wblk, 0, ws, wa);
         else hipLaunchKernelGGL((k_walk_fused<true, 16>), wgrid, wblk, 0, ws, wa);
     } else {
-        if (short_segs) hipLaunchKernelGGL((k_walk_fused<false, 4>), wgrid, wblk, 0, ws, wa);
+        if (kr == 2) hipLaunchKernelGGL((k_walk_fused<false, 2>), wgrid, wblk, 0, ws, wa);
+        else if (kr == 8) hipLaunchKernelGGL((k_walk_fused<false, 8>), wgrid, wblk, 0, ws, wa);
         else hipLaunchKernelGGL((k_walk_fused<false, 16>), wgrid, wblk, 0, ws, wa);
     }
     HIP_TRY(hipGetLastError());

@@ -72,36 +72,17 @@ __device__ __attribute__((noinline)) uint32_t u8_run_masked(uint32_t s, const ui
     return s;
 }
 
-// Header fetch: the longest masked header is 14 bytes.  Two aligned 16-byte loads cover
-// [pos, pos+16) -- one request per lane per load instead of 14 byte gathers.  Bytes past the
-// segment end are never used (every use is guarded by `avail`).
-__device__ __forceinline__ void hdr_issue(const uint8_t* __restrict__ w, uint64_t n, uint64_t pos,
-                                          uint4& c0, uint4& c1) {
-    const uint64_t a0 = pos & ~15ull;
-    if (a0 + 32 <= n) {
-        c0 = *reinterpret_cast<const uint4*>(w + a0);
-        c1 = *reinterpret_cast<const uint4*>(w + a0 + 16);
-    } else {   // the last 32 bytes of the buffer: byte loads, nothing read past n
-        uint32_t t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        for (uint32_t k = 0; k < 32 && a0 + k < n; ++k) t[k >> 2] |= (uint32_t)w[a0 + k] << (8 * (k & 3));
-        c0 = make_uint4(t[0], t[1], t[2], t[3]);
-        c1 = make_uint4(t[4], t[5], t[6], t[7]);
-    }
+// Header fetch: the longest masked header is 14 bytes, so ONE byte-aligned 16-byte load at the
+// frame's first byte covers it (gfx950 takes unaligned dwordx4 addresses); the last 16 bytes of the
+// buffer are read byte by byte (nothing past n).  Bytes past the segment end are never used
+// (every use is guarded by `avail`).
+__device__ __forceinline__ uint4 hdr_load(const uint8_t* __restrict__ w, uint64_t n, uint64_t pos) {
+    return load16_unaligned(w, (int64_t)pos, n);
 }
-__device__ __forceinline__ void hdr_extract(const uint4& c0, const uint4& c1, uint64_t pos, uint32_t (&h)[14]) {
-    const uint32_t d[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-    const uint32_t sh = (uint32_t)(pos & 15), q = sh >> 2, rb = sh & 3;
-    uint32_t hd[4];
+__device__ __forceinline__ void hdr_bytes(const uint4& hd, uint32_t (&h)[14]) {
+    const uint32_t d[4] = {hd.x, hd.y, hd.z, hd.w};
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        uint32_t lo = d[j], hi = d[j + 1];
-        if (q == 1) { lo = d[j + 1]; hi = d[j + 2]; }
-        else if (q == 2) { lo = d[j + 2]; hi = d[j + 3]; }
-        else if (q == 3) { lo = d[j + 3]; hi = d[j + 4]; }
-        hd[j] = __builtin_amdgcn_alignbyte(hi, lo, rb);
-    }
-#pragma unroll
-    for (int k = 0; k < 14; ++k) h[k] = (hd[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+    for (int k = 0; k < 14; ++k) h[k] = (d[k >> 2] >> (8 * (k & 3))) & 0xFFu;
 }
 
 // Output side of the walk: everything a frame writes (record, arena offset, span, window index)
@@ -191,6 +172,7 @@ __device__ __forceinline__ void emit_frame(const WalkArgs& a, EmitCtx& e, const 
 // the walk's final per-connection state (from the counting pass)
 struct WalkEnd {
     uint64_t pos, cont;
+    uint64_t last_dend;      // wire end of the segment's last payload span (seg_start if none)
     uint32_t msg, mode, status, close_code, err, u8dfa;
 };
 
@@ -231,34 +213,6 @@ __device__ __forceinline__ uint4 rec_pack(const wsc_frame& fr, uint64_t seg_star
     return make_uint4((uint32_t)(fr.hdr_off - seg_start), fr.payload_len, fr.mask, bits);
 }
 
-template <bool COMPACT>
-__device__ __forceinline__ void emit_replay(const WalkArgs& a, uint32_t s, uint64_t seg_start, uint64_t seg_end,
-                                            const SegCount& base, const SegCount& own, const uint4* lrec,
-                                            uint32_t msg0, const WalkEnd& end) {
-    EmitCtx e = emit_begin<COMPACT>(a, s, seg_start, seg_end, base, own);
-    uint32_t msg = msg0;
-    for (uint32_t i = 0; i < own.frames; ++i) {
-        const uint4 r = lrec[i * 256];
-        wsc_frame fr;
-        fr.hdr_off = seg_start + r.x;
-        fr.payload_len = r.y;
-        fr.mask = r.z;
-        fr.seg = s;
-        fr.msg_id = msg;
-        fr.opcode = (uint8_t)(r.w & 0xF);
-        fr.fin = (uint8_t)((r.w >> 4) & 1);
-        fr.kind = (uint8_t)((r.w >> 5) & 7);
-        fr.mode = (uint8_t)((r.w >> 8) & 3);
-        fr.err = (uint8_t)((r.w >> 10) & 7);
-        fr.hdr_len = (uint8_t)((r.w >> 13) & 15);
-        fr.flags = (uint8_t)((r.w >> 17) & 0x7F);
-        fr.pad = 0;
-        if ((r.w >> 26) & 1) msg += 1;
-        emit_frame<COMPACT>(a, e, fr, r.y, (r.w >> 25) & 1, (r.w >> 24) & 1);
-    }
-    emit_end<COMPACT>(a, e, end);
-}
-
 // Walk one segment's frames (one lane).  Pass 1 (EMIT=false) counts, decides utf8 verdicts and
 // keeps up to KREC frame records in LDS; pass 2 (EMIT=true, only for segments with more frames)
 // re-walks and writes every output at the offsets `base` (exclusive prefix over segments).
@@ -272,7 +226,8 @@ constexpr int SPEC_D = 4;
 
 template <bool EMIT, bool COMPACT, uint32_t KR = KREC>
 __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, const SegCount& base,
-                                                 const SegCount& own, uint4* lrec, WalkEnd* wend) {
+                                                 const SegCount& own, uint4* lrec, WalkEnd* wend,
+                                                 uint4* lrec2 = nullptr) {
     const uint8_t* __restrict__ w = a.wire;
     const uint64_t seg_start = a.seg_off[s];
     const uint64_t seg_end = a.seg_off[s + 1];
@@ -302,14 +257,27 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
     }
 
     uint64_t pos = seg_start;
+    uint64_t pend = seg_start;   // wire end of the last payload span so far (window index, emit)
+
+    // LDS records of the counting pass for the emit: rec_pack + the frame's position among the
+    // segment's outputs (MsgID, span ordinal, arena offset in its region, previous span end)
+    auto record = [&](const wsc_frame& fr, bool have_span, uint32_t region, bool inc, uint64_t plen) {
+        if (lrec && nf < KR) {
+            lrec[nf * 256] = rec_pack(fr, seg_start, have_span, region, inc);
+            if (lrec2)
+                lrec2[nf * 256] = make_uint4(fr.msg_id, ns0 + ns1, (uint32_t)(COMPACT && region ? nb1 : nb0),
+                                             (uint32_t)(pend - seg_start));
+        }
+        if (have_span) pend = fr.hdr_off + fr.hdr_len + plen;
+    };
 
     // One frame at `pos` from its 32-byte header window; returns false when the walk stops
     // (terminal status, or the frame is incomplete and is carried to the next batch).
-    auto step = [&](const uint4& hc0, const uint4& hc1) -> bool {
+    auto step = [&](const uint4& hd) -> bool {
         const uint64_t avail = seg_end - pos;
         if (avail < 2) return false;
         uint32_t h[14];
-        hdr_extract(hc0, hc1, pos, h);
+        hdr_bytes(hd, h);
         const uint32_t fin = h[0] >> 7;
         const uint32_t rsv = (h[0] >> 4) & 7;
         const uint32_t op = h[0] & 0xF;
@@ -507,9 +475,9 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
 
         if constexpr (EMIT) {
             emit_frame<COMPACT>(a, e, fr, (uint32_t)plen, have_span, region);
-        } else if (lrec && nf < KR) {
-            const bool inc = fr.kind == WSC_FK_MESSAGE || fr.kind == WSC_FK_PING || fr.kind == WSC_FK_PONG;
-            lrec[nf * 256] = rec_pack(fr, seg_start, have_span, region, inc);
+        } else {
+            record(fr, have_span, region,
+                   fr.kind == WSC_FK_MESSAGE || fr.kind == WSC_FK_PING || fr.kind == WSC_FK_PONG, plen);
         }
         nf += 1;
         if (have_span) {
@@ -520,18 +488,68 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
         return status == WSC_SEG_OPEN;
     };
 
+    // Fast path (counting pass): a complete, masked FIN BIN frame (0x82) while no fragmented
+    // message is open (cont == 0) is always Message{MsgID: msg, Opcode: 2} (websocket.go:142-146,
+    // websocket_frame.go:52-91; messageMode 2 -> 0, msgID + 1): its record is written without the
+    // general state machine.  Everything else goes through `step`.
+    auto fast = [&](const uint4& hd) -> bool {
+        if constexpr (EMIT) return false;
+        const uint32_t b0 = hd.x & 0xFFu, b1 = (hd.x >> 8) & 0xFFu;
+        if (b0 != 0x82u || !(b1 & 0x80u) || cont != 0) return false;
+        const uint32_t len7 = b1 & 0x7Fu;
+        uint64_t plen;
+        uint32_t mask, hl;
+        if (len7 < 126) {
+            plen = len7;
+            mask = __builtin_amdgcn_alignbyte(hd.y, hd.x, 2);
+            hl = 6;
+        } else if (len7 == 126) {
+            plen = ((hd.x >> 8) & 0xFF00u) | (hd.x >> 24);
+            mask = hd.y;
+            hl = 8;
+        } else {
+            const uint64_t x = (uint64_t)__builtin_amdgcn_alignbyte(hd.y, hd.x, 2) |
+                               (uint64_t)__builtin_amdgcn_alignbyte(hd.z, hd.y, 2) << 32;
+            plen = __builtin_bswap64(x);
+            mask = __builtin_amdgcn_alignbyte(hd.w, hd.z, 2);
+            hl = 14;
+        }
+        if (plen > a.max_frame_len || seg_end - pos < hl + plen) return false;
+        wsc_frame fr;
+        fr.hdr_off = pos;
+        fr.payload_len = (uint32_t)plen;
+        fr.mask = mask;
+        fr.seg = s;
+        fr.msg_id = msg;
+        fr.opcode = 2;
+        fr.fin = 1;
+        fr.kind = WSC_FK_MESSAGE;
+        fr.mode = 2;
+        fr.err = 0;
+        fr.hdr_len = (uint8_t)hl;
+        fr.flags = WSC_FF_UNMASKED;
+        fr.pad = 0;
+        const bool have_span = plen > 0;
+        record(fr, have_span, 0, true, plen);
+        msg += 1;
+        mode = 0;
+        nf += 1;
+        if (have_span) { ns0 += 1; nb0 += plen; }
+        pos += hl + plen;
+        return true;
+    };
+
     uint64_t stride = 0;
     bool go = status == WSC_SEG_OPEN;
     while (go) {
         // one memory round trip: the next header + SPEC_D-1 speculative ones
-        uint4 hc0[SPEC_D], hc1[SPEC_D];
+        uint4 hc[SPEC_D];
         uint64_t hp[SPEC_D];
 #pragma unroll
         for (int k = 0; k < SPEC_D; ++k) {
             hp[k] = pos + (uint64_t)k * stride;
-            hc0[k] = make_uint4(0, 0, 0, 0);
-            hc1[k] = hc0[k];
-            if (k == 0 || (stride != 0 && hp[k] + 2 <= seg_end)) hdr_issue(w, a.n_bytes, hp[k], hc0[k], hc1[k]);
+            hc[k] = make_uint4(0, 0, 0, 0);
+            if (k == 0 || (stride != 0 && hp[k] + 2 <= seg_end)) hc[k] = hdr_load(w, a.n_bytes, hp[k]);
             else hp[k] = ~0ull;
         }
         // consume the round's headers in order from the front of the queue; one copy of `step`
@@ -540,12 +558,11 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
         for (int k = 0; k < SPEC_D; ++k) {
             if (!go || hp[0] != pos) break;   // speculation ran out or missed: next round trip
             const uint64_t p0 = pos;
-            go = step(hc0[0], hc1[0]);
+            if (!fast(hc[0])) go = step(hc[0]);
             stride = pos - p0;
 #pragma unroll
             for (int q = 0; q + 1 < SPEC_D; ++q) {
-                hc0[q] = hc0[q + 1];
-                hc1[q] = hc1[q + 1];
+                hc[q] = hc[q + 1];
                 hp[q] = hp[q + 1];
             }
             hp[SPEC_D - 1] = ~0ull;
@@ -556,8 +573,10 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
     c.frames = nf; c.spans0 = ns0; c.spans1 = ns1; c.flags = sflags;
     c.bytes0 = nb0; c.bytes1 = nb1;
     if constexpr (!EMIT) {
-        a.u8info[2 * s] = u8fail;
-        a.u8info[2 * s + 1] = u8dfa;
+        if (nf > KR || !lrec) {   // only a re-walking emit pass reads them back
+            a.u8info[2 * s] = u8fail;
+            a.u8info[2 * s + 1] = u8dfa;
+        }
         if (u8_n) {
             U8Seg g{};
             g.head = u8_head;
@@ -571,6 +590,7 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
     WalkEnd we;
     we.pos = pos; we.cont = cont; we.msg = msg; we.mode = mode; we.status = status;
     we.close_code = close_code; we.err = err_out; we.u8dfa = u8dfa;
+    we.last_dend = pend;
     if (wend) *wend = we;
     if constexpr (EMIT) emit_end<COMPACT>(a, e, we);
     return c;
@@ -628,6 +648,17 @@ __global__ __launch_bounds__(256) void k_walk_fused(WalkArgs a) {
     __shared__ SegCount sh_wave[4];
     __shared__ SegCount sh_prefix;
     __shared__ uint4 sh_rec[KR * 256];   // [frame ordinal][lane]: conflict-free 16 B per lane
+    __shared__ uint4 sh_rec2[KR * 256];  // the frame's MsgID / span ordinal / arena offset / previous span end
+    // per lane, for the block's cooperative emit: block-local first frame (flat index), segment
+    // start, global frame / span / arena bases, data-region bytes, and whether it replays from LDS
+    __shared__ uint32_t sh_rpre[256], sh_wtot[4];
+    __shared__ uint64_t sh_sstart[256];
+    __shared__ uint32_t sh_fbase[256], sh_sbase[256];
+    __shared__ uint64_t sh_abase[COMPACT ? 256 : 1], sh_ob0[COMPACT ? 256 : 1];
+    __shared__ uint8_t sh_replay[256];
+    __shared__ uint8_t sh_owner[KR * 256];   // flat replayed frame -> its lane
+    __shared__ uint32_t sh_nbig;             // long spans whose window index a whole wave writes
+    __shared__ uint4 sh_big[64];
     if (threadIdx.x == 0)
         sh_bid = __hip_atomic_fetch_add(a.lb_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
@@ -641,11 +672,8 @@ __global__ __launch_bounds__(256) void k_walk_fused(WalkArgs a) {
     if (a.dbg && threadIdx.x == 0) t0 = __builtin_amdgcn_s_memrealtime();
     SegCount own = zero;
     WalkEnd wend = {};
-    uint32_t msg0 = 0;
     if (s < a.n_segs) {
-        own = walk_segment<false, COMPACT, KR>(a, s, zero, zero, sh_rec + threadIdx.x, &wend);
-        a.counts[s] = own;
-        msg0 = a.state_in ? a.state_in[s].msg_id : 0u;
+        own = walk_segment<false, COMPACT, KR>(a, s, zero, zero, sh_rec + threadIdx.x, &wend, sh_rec2 + threadIdx.x);
     }
     // block-wide scan (64-lane shuffles, then across the 4 waves)
     SegCount inc = own;
@@ -728,11 +756,112 @@ __global__ __launch_bounds__(256) void k_walk_fused(WalkArgs a) {
         a.u8seg[s].nspans = own.spans0 + own.spans1;
         a.u8seg[s].fbase = base.frames;
     }
+    // Emit.  Segments whose frames all sit in LDS are emitted by the whole block cooperatively:
+    // their frames in flat order (lane-major) are consecutive records / spans / arena offsets in
+    // memory, so thread t writes flat frames t, t + 256, ... and every store instruction covers
+    // contiguous memory; then the window index of the block's byte range is written window by
+    // window.  Longer segments re-walk their (cache-warm) headers and emit serially.
+    const uint64_t seg_start = s < a.n_segs ? a.seg_off[s] : 0;
+    const uint64_t seg_end = s < a.n_segs ? a.seg_off[s + 1] : 0;
+    const bool replay = s < a.n_segs && own.frames <= KR && seg_end - seg_start <= 0xFFFFFFFFull;
+    const uint32_t rc = replay ? own.frames : 0u;
+    uint32_t rv = rc;   // block scan of the replayed frame counts
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(rv, d);
+        if (lane >= (uint32_t)d) rv += o;
+    }
+    if (lane == 63) sh_wtot[wave] = rv;
+    sh_sstart[threadIdx.x] = seg_start;
+    sh_fbase[threadIdx.x] = base.frames;
+    sh_sbase[threadIdx.x] = base.spans0 + base.spans1;
+    if constexpr (COMPACT) {
+        sh_abase[threadIdx.x] = base.bytes0 + base.bytes1;
+        sh_ob0[threadIdx.x] = own.bytes0;
+    }
+    sh_replay[threadIdx.x] = replay ? 1 : 0;
+    __syncthreads();
+    uint32_t rpre = rv - rc, F = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        if ((uint32_t)q < wave) rpre += sh_wtot[q];
+        F += sh_wtot[q];
+    }
+    sh_rpre[threadIdx.x] = rpre;
+    for (uint32_t k = 0; k < rc; ++k) sh_owner[rpre + k] = (uint8_t)threadIdx.x;
+    if (threadIdx.x == 0) sh_nbig = 0;
+    __syncthreads();
+    const uint32_t W = 1u << a.win_shift;
+    for (uint32_t f = threadIdx.x; f < F; f += 256) {
+        const uint32_t o = sh_owner[f];
+        const uint32_t k = f - sh_rpre[o];
+        const uint4 r = sh_rec[k * 256 + o];
+        const uint4 q = sh_rec2[k * 256 + o];
+        const uint64_t ss = sh_sstart[o];
+        const uint32_t fi = sh_fbase[o] + k;
+        const uint32_t hl = (r.w >> 13) & 15, fl = (r.w >> 17) & 0x7F, region = (r.w >> 24) & 1;
+        const bool have_span = (r.w >> 25) & 1;
+        const uint64_t hdr_off = ss + r.x;
+        uint64_t dst = ~0ull;
+        if constexpr (COMPACT)
+            if (fl & WSC_FF_UNMASKED) dst = sh_abase[o] + (region ? sh_ob0[o] : 0ull) + q.z;
+        if (fi < a.frames_cap) {
+            const uint4 r0 = make_uint4((uint32_t)hdr_off, (uint32_t)(hdr_off >> 32), r.y, r.z);
+            const uint4 r1 = make_uint4(bid * 256 + o, q.x,
+                                        (r.w & 0xF) | ((r.w >> 4) & 1) << 8 | ((r.w >> 5) & 7) << 16 |
+                                            ((r.w >> 8) & 3) << 24,
+                                        ((r.w >> 10) & 7) | hl << 8 | fl << 16);
+            reinterpret_cast<uint4*>(a.frames + fi)[0] = r0;
+            reinterpret_cast<uint4*>(a.frames + fi)[1] = r1;
+            if constexpr (COMPACT) a.frame_dst[fi] = dst;
+        }
+        if (have_span) {
+            const uint32_t idx = sh_sbase[o] + q.y;
+            Span sp;
+            sp.src = hdr_off + hl;
+            sp.len = r.y;
+            sp.dst = COMPACT ? dst : sp.src;
+            sp.key = rotr32(r.z, 8u * ((uint32_t)(0u - (uint32_t)sp.src) & 3u));
+            if (idx < a.spans_cap) a.spans[idx] = sp;
+            // windows starting in [previous span end, this span end) look this span up first
+            uint64_t t = (ss + q.w + W - 1) >> a.win_shift;
+            const uint64_t t_end = ((sp.src + r.y - 1) >> a.win_shift) + 1;
+            if (t_end > t + 64) {   // a long span: its windows are written by a whole wave below
+                const uint32_t j = atomicAdd(&sh_nbig, 1u);
+                if (j < 64) {
+                    sh_big[j] = make_uint4((uint32_t)t, (uint32_t)(t >> 32), (uint32_t)(t_end - t), idx);
+                    t = t_end;
+                }
+            }
+            for (; t < t_end && (t & 3); ++t) a.tile_first[t] = idx;
+            const uint4 q4 = make_uint4(idx, idx, idx, idx);
+            for (; t + 4 <= t_end; t += 4) *reinterpret_cast<uint4*>(a.tile_first + t) = q4;
+            for (; t < t_end; ++t) a.tile_first[t] = idx;
+        }
+    }
+    // window index of long spans (more than 64 windows: 256 KiB+ payloads), one wave per span
+    __syncthreads();
+    {
+        const uint32_t nbig = sh_nbig < 64 ? sh_nbig : 64;
+        for (uint32_t j = wave; j < nbig; j += 4) {
+            const uint64_t tb = sh_big[j].x | (uint64_t)sh_big[j].y << 32;
+            const uint32_t nw = sh_big[j].z, idx = sh_big[j].w;
+            for (uint32_t i = lane; i < nw; i += 64) a.tile_first[tb + i] = idx;
+        }
+    }
     if (s < a.n_segs) {
-        if (own.frames <= KR)   // replay from LDS: no second dependent walk, no loads at all
-            emit_replay<COMPACT>(a, s, a.seg_off[s], a.seg_off[s + 1], base, own, sh_rec + threadIdx.x, msg0, wend);
-        else                      // long segment: re-walk the (cache-warm) headers
+        if (replay) {             // the segment's own outputs (its frames and windows were written above)
+            EmitCtx e = emit_begin<COMPACT>(a, s, seg_start, seg_end, base, own);
+            e.nf = own.frames;
+            e.ns0 = own.spans0;
+            e.ns1 = own.spans1;
+            const uint64_t Wd = 1ull << a.win_shift;   // windows after the last span: emit_end
+            const uint64_t lo = wend.last_dend > seg_start ? wend.last_dend : seg_start;
+            e.nx0 = (lo + Wd - 1) & ~(Wd - 1);
+            emit_end<COMPACT>(a, e, wend);
+        } else {                  // long segment: re-walk the (cache-warm) headers
             walk_segment<true, COMPACT>(a, s, base, own, nullptr, nullptr);
+        }
     }
     if (a.dbg) {   // diagnostic timestamps (100 MHz s_memrealtime), written only to the dbg buffer
         __syncthreads();
@@ -1040,7 +1169,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
 // explicit instantiations used by the host code
 template __global__ void k_walk_fused<false, KREC>(WalkArgs);
 template __global__ void k_walk_fused<true, KREC>(WalkArgs);
-template __global__ void k_walk_fused<false, 4>(WalkArgs);
-template __global__ void k_walk_fused<true, 4>(WalkArgs);
+template __global__ void k_walk_fused<false, 8>(WalkArgs);
+template __global__ void k_walk_fused<true, 8>(WalkArgs);
+template __global__ void k_walk_fused<false, 2>(WalkArgs);
+template __global__ void k_walk_fused<true, 2>(WalkArgs);
 
 }  // namespace wsc

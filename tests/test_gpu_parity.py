@@ -61,11 +61,12 @@ def test_fuzz_single_batch(codec, compact):
     _check_batch(codec, streams, compact=compact)
 
 
-@pytest.mark.parametrize("compact", [False, True])
-def test_fuzz_walk_4_records(codec_lib, monkeypatch, compact):
-    """The walk instance batches of many short segments launch (4 LDS frame records per lane, the
-    rest re-walked by the emit pass), forced on fuzz streams of 5..44 units with text and errors."""
-    monkeypatch.setenv("WSC_WALK_KREC", "4")
+@pytest.mark.parametrize("compact,krec", [(False, 2), (True, 2), (False, 8), (True, 8)])
+def test_fuzz_walk_few_records(codec_lib, monkeypatch, compact, krec):
+    """The walk instances for many segments (2 or 8 LDS frame records per lane; segments with
+    more frames re-walked by the emit pass, the rest emitted cooperatively by the block), forced
+    on fuzz streams of 5..44 units with text and errors, and of 1..6 units."""
+    monkeypatch.setenv("WSC_WALK_KREC", str(krec))
     c = K.Codec(0, max_batch_bytes=64 << 20, max_segs=1 << 14, max_frames=1 << 18)
     try:
         streams = [random_stream(7000 + i, n_units=int(5 + i % 40), text_p=0.5) for i in range(400)]
