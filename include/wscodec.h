@@ -317,6 +317,9 @@ int wsc_session_feed(wsc_session* s, uint32_t conn, const uint8_t* bytes, uint64
 int wsc_session_submit(wsc_session* s);    /* async device pass over everything fed (one batch)  */
 int wsc_session_complete(wsc_session* s);  /* wait for it, queue each connection's events        */
 int wsc_session_decode(wsc_session* s);    /* submit + complete until everything fed is decoded  */
+/* Bytes fed but not yet submitted (a batch takes what fits; the rest waits in per-connection
+ * spills): a double-buffered poller submits again while this is non-zero, new reads or not.   */
+int wsc_session_pending(wsc_session* s, uint64_t* bytes);
 int wsc_session_next(wsc_session* s, uint32_t conn, wsc_event* ev);  /* DecodePacket() */
 int wsc_session_state(wsc_session* s, uint32_t conn, wsc_conn_state* st, uint64_t* carry_bytes);
 

@@ -116,6 +116,7 @@ SIGNATURES = {
     "wsc_session_submit": (_I, [_P]),
     "wsc_session_complete": (_I, [_P]),
     "wsc_session_decode": (_I, [_P]),
+    "wsc_session_pending": (_I, [_P, C.POINTER(_U64)]),
     "wsc_session_next": (_I, [_P, _U32, C.POINTER(WscEvent)]),
     "wsc_session_state": (_I, [_P, _U32, C.POINTER(WscConnState), C.POINTER(_U64)]),
 }
@@ -473,6 +474,12 @@ class Session:
 
     def decode(self):
         _check(self.lib.wsc_session_decode(self.h), "wsc_session_decode")
+
+    def pending(self) -> int:
+        """bytes fed but not yet submitted (submit again while non-zero)"""
+        n = C.c_uint64()
+        _check(self.lib.wsc_session_pending(self.h, C.byref(n)), "wsc_session_pending")
+        return n.value
 
     def next_event(self, conn: int) -> Event:
         ev = WscEvent()

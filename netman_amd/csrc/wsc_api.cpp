@@ -11,7 +11,10 @@
 #include "wsc_kernels.hpp"
 
 namespace wsc {
-template <bool COMPACT, uint32_t KR> __global__ void k_walk_fused(WalkArgs);
+template <bool COMPACT, uint32_t KR, uint32_t NT, uint32_t G> __global__ void k_walk_fused(WalkArgs);
+template <bool COMPACT> __global__ void k_walk_count(WalkArgs);
+__global__ void k_walk_scan(WalkArgs, uint32_t);
+template <bool COMPACT> __global__ void k_walk_emit(WalkArgs);
 __global__ void k_u8_check(U8Args);
 template <bool COMPACT, int P, int NT, int MINW>
 __global__ void k_unmask(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*,
@@ -51,7 +54,6 @@ struct wsc_ctx {
     hipEvent_t ev_done = nullptr;     // wsc_decode_split: unmask done (the next walk on this ctx waits)
     wsc_config cfg{};
     uint32_t pieces = 8;          // 16 B pieces per lane -> window = pieces KiB
-    SegCount* counts = nullptr;
     uint32_t* sticky = nullptr;      // error bits of every decode/encode (wsc_error_flags), never re-armed
     uint32_t* lb_state = nullptr;    // [0] ticket, [1] spin-timeout flag, [2] UTF-8 item count, [3..] per-block flags
     uint32_t* u8info = nullptr;      // per segment {utf8-failing frame ordinal, DFA state}
@@ -67,7 +69,8 @@ struct wsc_ctx {
     U8Seg* u8seg = nullptr;
     uint32_t u8_inline_max = 256;
     uint32_t u8_grid = 0;               // WSC_U8_GRID: k_u8_check workgroups (A/B experiments; 0 = 5 per CU)
-    int walk_krec = 0;                  // WSC_WALK_KREC: 16, 8 or 2 pins that walk instance (A/B, tests); 0 = auto
+    int walk_mode = 0;                  // WSC_WALK_MODE: 64, 256 or 3 pins the walk geometry (A/B, tests); 0 = auto
+    SegCount* counts = nullptr;         // three-launch walk: per-segment counts
     uint64_t tile_entries = 0;
     // host-staged path buffers (lazily allocated)
     uint8_t* d_wire = nullptr;
@@ -95,6 +98,15 @@ struct wsc_ctx {
 };
 
 extern "C" {
+
+// walk geometry (see launch): 64 = fused walk with 64-lane blocks, 256 = fused with 256-lane
+// blocks, 3 = the three-launch walk (count / scan / emit)
+static uint32_t walk_mode(const wsc_ctx* c, uint32_t n_segs) {
+    if (c->walk_mode) return (uint32_t)c->walk_mode;
+    if (n_segs <= 64u * (uint32_t)c->n_cu) return 64;
+    if (n_segs <= 256u * (uint32_t)c->n_cu) return 256;
+    return 3;
+}
 
 int wsc_abi_version(void) { return WSC_ABI_VERSION; }
 const char* wsc_last_error(void) { return g_err.c_str(); }
@@ -162,10 +174,10 @@ int wsc_create(int device, const wsc_config* cfg_in, wsc_ctx** out) {
     chk(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate");
     chk(hipEventCreateWithFlags(&c->ev_walked, hipEventDisableTiming), "hipEventCreate");
     chk(hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming), "hipEventCreate");
-    chk(hipMalloc(&c->counts, cfg.max_segs * sizeof(SegCount)), "hipMalloc counts");
     chk(hipMalloc(&c->sticky, sizeof(uint32_t)), "hipMalloc sticky");
+    chk(hipMalloc(&c->counts, (uint64_t)cfg.max_segs * sizeof(SegCount)), "hipMalloc counts");
     if (rc == WSC_OK) chk(hipMemsetAsync(c->sticky, 0, sizeof(uint32_t), c->stream), "hipMemset sticky");
-    const uint64_t max_blocks = (cfg.max_segs + 255) / 256 + 1;
+    const uint64_t max_blocks = (cfg.max_segs + 63) / 64 + 1;   // the most walk blocks (64-lane blocks)
     chk(hipMalloc(&c->lb_state, (max_blocks + 3) * sizeof(uint32_t)), "hipMalloc lb_state");
     chk(hipMalloc(&c->u8info, (uint64_t)cfg.max_segs * 2 * sizeof(uint32_t)), "hipMalloc u8info");
     chk(hipMalloc(&c->lb_agg, max_blocks * 4 * sizeof(uint64_t)), "hipMalloc lb_agg");
@@ -185,9 +197,9 @@ int wsc_create(int device, const wsc_config* cfg_in, wsc_ctx** out) {
     chk(hipMalloc(&c->u8maps, (uint64_t)c->u8items_cap * sizeof(uint64_t)), "hipMalloc u8maps");
     chk(hipMalloc(&c->u8seg, (uint64_t)cfg.max_segs * sizeof(U8Seg)), "hipMalloc u8seg");
     if (const char* e = std::getenv("WSC_U8_GRID"); e && *e) c->u8_grid = (uint32_t)std::strtoul(e, nullptr, 10);
-    if (const char* e = std::getenv("WSC_WALK_KREC"); e && *e) {   // pin an instance (tests, A/B)
-        const int k = std::atoi(e);
-        c->walk_krec = k <= 2 ? 2 : (k <= 8 ? 8 : 16);
+    if (const char* e = std::getenv("WSC_WALK_MODE"); e && *e) {   // pin a walk geometry (tests, A/B): 64, 256 or 3
+        const int m = std::atoi(e);
+        c->walk_mode = (m == 64 || m == 256 || m == 3) ? m : 0;
     }
     if (const char* e = std::getenv("WSC_U8_INLINE_MAX"); e && *e)   // test knob: 0 sends all text chip-wide
         c->u8_inline_max = (uint32_t)std::strtoul(e, nullptr, 10);
@@ -297,7 +309,12 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     wa.u8_inline_max = c->u8_inline_max;
     wa.sticky = c->sticky;
 
-    const dim3 wblk(256), wgrid((n + 255) / 256);
+    // walk geometry: the fused walk with blocks that fill the CUs once (64 lanes for up to 64
+    // segments per CU, else 256), or -- for more segments than the chip holds lanes at once -- the
+    // three-launch walk, which never waits on another block
+    const uint32_t mode = walk_mode(c, n);
+    const uint32_t wnt = mode == 64 ? 64u : 256u;
+    const dim3 wblk(wnt), wgrid((n + wnt - 1) / wnt);
     auto rec = [&](int i) {
         if (ev) (void)hipEventRecord(ev[i], st);
     };
@@ -306,19 +323,21 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     // (an event never recorded is a no-op wait)
     const hipStream_t ws = split ? sw : st;
     if (split) HIP_TRY(hipStreamWaitEvent(ws, c->ev_done, 0));
-    // frame records kept in LDS per lane (KR): 16 (~138 KiB of LDS, one block per CU) while the
-    // blocks fit the CUs at once; 8 (two per CU) up to twice that; 2 for batches of many short
-    // segments (VGPR-bound residency).  Segments with more frames re-walk their headers to emit.
-    uint32_t kr = wgrid.x <= (uint32_t)c->n_cu ? 16u : (wgrid.x <= 2u * (uint32_t)c->n_cu ? 8u : 2u);
-    if (c->walk_krec) kr = (uint32_t)c->walk_krec;
-    if (compact) {
-        if (kr == 2) hipLaunchKernelGGL((k_walk_fused<true, 2>), wgrid, wblk, 0, ws, wa);
-        else if (kr == 8) hipLaunchKernelGGL((k_walk_fused<true, 8>), wgrid, wblk, 0, ws, wa);
-        else hipLaunchKernelGGL((k_walk_fused<true, 16>), wgrid, wblk, 0, ws, wa);
+    // fused: 16 frame records per lane in LDS (segments with more frames re-walk their headers)
+    if (mode == 3) {
+        if (compact) hipLaunchKernelGGL((k_walk_count<true>), wgrid, wblk, 0, ws, wa);
+        else hipLaunchKernelGGL((k_walk_count<false>), wgrid, wblk, 0, ws, wa);
+        HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(k_walk_scan, dim3(1), dim3(256), 0, ws, wa, wgrid.x);
+        HIP_TRY(hipGetLastError());
+        if (compact) hipLaunchKernelGGL((k_walk_emit<true>), wgrid, wblk, 0, ws, wa);
+        else hipLaunchKernelGGL((k_walk_emit<false>), wgrid, wblk, 0, ws, wa);
+    } else if (compact) {
+        if (wnt == 64) hipLaunchKernelGGL((k_walk_fused<true, 16, 64, 1>), wgrid, wblk, 0, ws, wa);
+        else hipLaunchKernelGGL((k_walk_fused<true, 16, 256, 1>), wgrid, wblk, 0, ws, wa);
     } else {
-        if (kr == 2) hipLaunchKernelGGL((k_walk_fused<false, 2>), wgrid, wblk, 0, ws, wa);
-        else if (kr == 8) hipLaunchKernelGGL((k_walk_fused<false, 8>), wgrid, wblk, 0, ws, wa);
-        else hipLaunchKernelGGL((k_walk_fused<false, 16>), wgrid, wblk, 0, ws, wa);
+        if (wnt == 64) hipLaunchKernelGGL((k_walk_fused<false, 16, 64, 1>), wgrid, wblk, 0, ws, wa);
+        else hipLaunchKernelGGL((k_walk_fused<false, 16, 256, 1>), wgrid, wblk, 0, ws, wa);
     }
     HIP_TRY(hipGetLastError());
     if (split) {
@@ -365,7 +384,7 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     UK kern = table[compact ? 1 : 0][pi][compact ? (c->cfg.unmask_nt >> 2) & 3 : c->cfg.unmask_nt & 3];
     hipLaunchKernelGGL(kern, ugrid, ublk, 0, st, udst, (const uint8_t*)b->wire, b->n_bytes, b->n_bytes,
                        (const Span*)c->spans, (const uint32_t*)c->tile, (const wsc_summary*)b->summary,
-                       c->lb_state, (n + 255) / 256 + 1);   // re-arms ticket, timeout, item count, flags
+                       c->lb_state, mode == 3 ? 1u : wgrid.x + 1);   // re-arms ticket, timeout, item count, flags
     HIP_TRY(hipGetLastError());
     rec(4);
 

@@ -1,6 +1,6 @@
 // wsc_kernels.hip -- gfx950 kernels of the WebSocket frame decoder.
 //
-//   k_walk_fused<COMPACT> header walk + per-frame decode state machine, one lane per segment
+//   k_walk_fused<COMPACT,KR,G> header walk + per-frame decode state machine, one lane per G segments
 //                         (server/websocket.go:82-302, server/websocket_frame.go:13-103 minus the
 //                         byte loops).  Count, block scan + decoupled look-back, then emit frame
 //                         records, payload spans and the window->span index, in one launch.
@@ -200,9 +200,6 @@ __device__ __forceinline__ void emit_end(const WalkArgs& a, EmitCtx& e, const Wa
     a.state_out[e.s] = o;
 }
 
-// Frames a lane keeps in LDS between its counting walk and its emission (16 B each); segments
-// with more frames are re-walked from the (cache-warm) wire instead.
-constexpr uint32_t KREC = 16;
 
 __device__ __forceinline__ uint4 rec_pack(const wsc_frame& fr, uint64_t seg_start, bool have_span,
                                           uint32_t region, bool msg_inc) {
@@ -214,8 +211,9 @@ __device__ __forceinline__ uint4 rec_pack(const wsc_frame& fr, uint64_t seg_star
 }
 
 // Walk one segment's frames (one lane).  Pass 1 (EMIT=false) counts, decides utf8 verdicts and
-// keeps up to KREC frame records in LDS; pass 2 (EMIT=true, only for segments with more frames)
-// re-walks and writes every output at the offsets `base` (exclusive prefix over segments).
+// keeps up to `cap` frame records in LDS (lrec / lrec2, stride LS); pass 2 (EMIT=true, only for
+// segments with more frames) re-walks and writes every output at the offsets `base` (exclusive
+// prefix over segments).
 //
 // The header chain is serial, so the walk fetches SPEC_D headers per memory round trip: the
 // next header and the ones at +stride, +2*stride, ... (stride = the last frame's size).  A
@@ -224,10 +222,10 @@ __device__ __forceinline__ uint4 rec_pack(const wsc_frame& fr, uint64_t seg_star
 // one round trip per SPEC_D frames.  All loads of a round are waited together.
 constexpr int SPEC_D = 4;
 
-template <bool EMIT, bool COMPACT, uint32_t KR = KREC>
+template <bool EMIT, bool COMPACT, uint32_t LS = 64>
 __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, const SegCount& base,
                                                  const SegCount& own, uint4* lrec, WalkEnd* wend,
-                                                 uint4* lrec2 = nullptr) {
+                                                 uint4* lrec2 = nullptr, uint32_t cap = 0, uint32_t tag = 0) {
     const uint8_t* __restrict__ w = a.wire;
     const uint64_t seg_start = a.seg_off[s];
     const uint64_t seg_end = a.seg_off[s + 1];
@@ -262,11 +260,12 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
     // LDS records of the counting pass for the emit: rec_pack + the frame's position among the
     // segment's outputs (MsgID, span ordinal, arena offset in its region, previous span end)
     auto record = [&](const wsc_frame& fr, bool have_span, uint32_t region, bool inc, uint64_t plen) {
-        if (lrec && nf < KR) {
-            lrec[nf * 256] = rec_pack(fr, seg_start, have_span, region, inc);
-            if (lrec2)
-                lrec2[nf * 256] = make_uint4(fr.msg_id, ns0 + ns1, (uint32_t)(COMPACT && region ? nb1 : nb0),
-                                             (uint32_t)(pend - seg_start));
+        if (lrec && nf < cap) {
+            uint4 r = rec_pack(fr, seg_start, have_span, region, inc);
+            r.w |= tag << 27;   // the lane's segment the frame belongs to
+            lrec[nf * LS] = r;
+            lrec2[nf * LS] = make_uint4(fr.msg_id, ns0 + ns1, (uint32_t)(COMPACT && region ? nb1 : nb0),
+                                        (uint32_t)(pend - seg_start));
         }
         if (have_span) pend = fr.hdr_off + fr.hdr_len + plen;
     };
@@ -573,7 +572,7 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
     c.frames = nf; c.spans0 = ns0; c.spans1 = ns1; c.flags = sflags;
     c.bytes0 = nb0; c.bytes1 = nb1;
     if constexpr (!EMIT) {
-        if (nf > KR || !lrec) {   // only a re-walking emit pass reads them back
+        if (nf > cap || !lrec) {   // only a re-walking emit pass reads them back
             a.u8info[2 * s] = u8fail;
             a.u8info[2 * s + 1] = u8dfa;
         }
@@ -638,67 +637,233 @@ __device__ __forceinline__ SegCount lb_load(uint64_t* p) {
     return v;
 }
 
-// KR: frame records kept in LDS per lane for the emit replay (segments with more frames walk
-// their chain a second time).  KR = 16 is 64 KiB of LDS per block = 2 resident blocks per CU;
-// batches of many short segments launch the KR = 4 instance (4 blocks per CU, VGPR-bound) so that
-// twice as many blocks of the ticketed look-back run at once.
-template <bool COMPACT, uint32_t KR>
-__global__ __launch_bounds__(256) void k_walk_fused(WalkArgs a) {
-    __shared__ uint32_t sh_bid;
-    __shared__ SegCount sh_wave[4];
-    __shared__ SegCount sh_prefix;
-    __shared__ uint4 sh_rec[KR * 256];   // [frame ordinal][lane]: conflict-free 16 B per lane
-    __shared__ uint4 sh_rec2[KR * 256];  // the frame's MsgID / span ordinal / arena offset / previous span end
-    // per lane, for the block's cooperative emit: block-local first frame (flat index), segment
-    // start, global frame / span / arena bases, data-region bytes, and whether it replays from LDS
-    __shared__ uint32_t sh_rpre[256], sh_wtot[4];
-    __shared__ uint64_t sh_sstart[256];
-    __shared__ uint32_t sh_fbase[256], sh_sbase[256];
-    __shared__ uint64_t sh_abase[COMPACT ? 256 : 1], sh_ob0[COMPACT ? 256 : 1];
-    __shared__ uint8_t sh_replay[256];
-    __shared__ uint8_t sh_owner[KR * 256];   // flat replayed frame -> its lane
-    __shared__ uint32_t sh_nbig;             // long spans whose window index a whole wave writes
-    __shared__ uint4 sh_big[64];
-    if (threadIdx.x == 0)
-        sh_bid = __hip_atomic_fetch_add(a.lb_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    const uint32_t bid = sh_bid;
-    const uint32_t n_blocks = (a.n_segs + 255) / 256;
-    const uint32_t s = bid * 256 + threadIdx.x;
-    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+// ---------------------------------------------------------------------------------------------
+// Three-launch walk for batches of many (short) segments -- more lanes than the chip holds at once,
+// where the fused walk's look-back would wait on blocks that have not started:
+//   k_walk_count  one lane per segment: the counting pass (no LDS records), the segment's counts
+//                 and each block's total
+//   k_walk_scan   one block: exclusive scan of the block totals, batch summary
+//   k_walk_emit   one lane per segment: block prefix + in-block scan of the counts = the segment's
+//                 output offsets; re-walks its (cache-warm) headers and emits
+// No inter-block waiting anywhere; the kernel boundaries order the phases.
+// ---------------------------------------------------------------------------------------------
+template <uint32_t NT>
+__device__ __forceinline__ SegCount block_excl_scan(const SegCount& v, SegCount& total, SegCount* sh_wave) {
+    const uint32_t wl = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const SegCount zero = {};
-
-    uint64_t t0 = 0, t1 = 0, t2 = 0;
-    if (a.dbg && threadIdx.x == 0) t0 = __builtin_amdgcn_s_memrealtime();
-    SegCount own = zero;
-    WalkEnd wend = {};
-    if (s < a.n_segs) {
-        own = walk_segment<false, COMPACT, KR>(a, s, zero, zero, sh_rec + threadIdx.x, &wend, sh_rec2 + threadIdx.x);
-    }
-    // block-wide scan (64-lane shuffles, then across the 4 waves)
-    SegCount inc = own;
+    SegCount inc = v;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
         const SegCount o = sc_shfl_up(inc, d);
-        if (lane >= (uint32_t)d) inc = sc_add(o, inc);
+        if (wl >= (uint32_t)d) inc = sc_add(o, inc);
     }
     SegCount excl = sc_shfl_up(inc, 1);
-    if (lane == 0) excl = zero;
-    if (lane == 63) sh_wave[wave] = inc;
+    if (wl == 0) excl = zero;
+    if (wl == 63) sh_wave[wave] = inc;
     __syncthreads();
-    SegCount wpre = zero, btot = zero;
+    total = zero;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        if ((uint32_t)q < wave) wpre = sc_add(wpre, sh_wave[q]);
-        btot = sc_add(btot, sh_wave[q]);
+    for (uint32_t w = 0; w < NT / 64; ++w) {
+        if (w < wave) excl = sc_add(excl, sh_wave[w]);
+        total = sc_add(total, sh_wave[w]);
     }
+    return excl;
+}
+
+template <bool COMPACT>
+__global__ __launch_bounds__(256) void k_walk_count(WalkArgs a) {
+    __shared__ SegCount sh_wave[4];
+    const uint32_t s = blockIdx.x * 256 + threadIdx.x;
+    const SegCount zero = {};
+    SegCount own = zero;
+    if (s < a.n_segs) {
+        WalkEnd we;
+        own = walk_segment<false, COMPACT, 256>(a, s, zero, zero, nullptr, &we);
+        a.counts[s] = own;
+    }
+    SegCount tot;
+    (void)block_excl_scan<256>(own, tot, sh_wave);
+    if (threadIdx.x == 0) {   // the next launch reads it (kernel boundary: visible)
+        uint64_t* p = a.lb_agg + 4ull * blockIdx.x;
+        p[0] = (uint64_t)tot.frames | ((uint64_t)tot.spans0 << 32);
+        p[1] = (uint64_t)tot.spans1 | ((uint64_t)tot.flags << 32);
+        p[2] = tot.bytes0;
+        p[3] = tot.bytes1;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_walk_scan(WalkArgs a, uint32_t n_blocks) {
+    __shared__ SegCount sh_wave[4];
+    __shared__ SegCount sh_carry;
+    const SegCount zero = {};
+    if (threadIdx.x == 0) sh_carry = zero;
+    __syncthreads();
+    for (uint32_t b0 = 0; b0 < n_blocks; b0 += 256) {
+        const uint32_t b = b0 + threadIdx.x;
+        SegCount v = zero;
+        if (b < n_blocks) {
+            const uint64_t* p = a.lb_agg + 4ull * b;
+            v.frames = (uint32_t)p[0];
+            v.spans0 = (uint32_t)(p[0] >> 32);
+            v.spans1 = (uint32_t)p[1];
+            v.flags = (uint32_t)(p[1] >> 32);
+            v.bytes0 = p[2];
+            v.bytes1 = p[3];
+        }
+        SegCount tot;
+        const SegCount ex = sc_add(sh_carry, block_excl_scan<256>(v, tot, sh_wave));
+        if (b < n_blocks) {
+            uint64_t* q = a.lb_incl + 4ull * b;   // exclusive prefix of block b
+            q[0] = (uint64_t)ex.frames | ((uint64_t)ex.spans0 << 32);
+            q[1] = (uint64_t)ex.spans1 | ((uint64_t)ex.flags << 32);
+            q[2] = ex.bytes0;
+            q[3] = ex.bytes1;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) sh_carry = sc_add(sh_carry, tot);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const SegCount tt = sh_carry;
+        wsc_summary sm;
+        sm.data_bytes = tt.bytes0;
+        sm.ctrl_bytes = tt.bytes1;
+        sm.n_frames = tt.frames;
+        sm.n_spans = tt.spans0 + tt.spans1;
+        sm.overflow = (tt.frames > a.frames_cap || tt.spans0 + tt.spans1 > a.spans_cap) ? 1u : 0u;
+        sm.pad = 0;
+        *a.summary = sm;
+        if (sm.overflow) __hip_atomic_fetch_or(a.sticky, sm.overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+template <bool COMPACT>
+__global__ __launch_bounds__(256) void k_walk_emit(WalkArgs a) {
+    __shared__ SegCount sh_wave[4];
+    const uint32_t s = blockIdx.x * 256 + threadIdx.x;
+    const SegCount zero = {};
+    const SegCount own = s < a.n_segs ? a.counts[s] : zero;
+    SegCount tot;
+    const SegCount ex = block_excl_scan<256>(own, tot, sh_wave);
+    if (s >= a.n_segs) return;
+    const uint64_t* q = a.lb_incl + 4ull * blockIdx.x;
+    SegCount bp;
+    bp.frames = (uint32_t)q[0];
+    bp.spans0 = (uint32_t)(q[0] >> 32);
+    bp.spans1 = (uint32_t)q[1];
+    bp.flags = (uint32_t)(q[1] >> 32);
+    bp.bytes0 = q[2];
+    bp.bytes1 = q[3];
+    const SegCount base = sc_add(bp, ex);
+    if (own.flags & SEGF_U8DEFER) {
+        a.u8seg[s].sbase = base.spans0 + base.spans1;
+        a.u8seg[s].nspans = own.spans0 + own.spans1;
+        a.u8seg[s].fbase = base.frames;
+    }
+    walk_segment<true, COMPACT, 256>(a, s, base, own, nullptr, nullptr);
+}
+
+// The fused walk kernel: NT lanes (64 or 256) per block, G consecutive segments per lane, KR frame
+// records per lane in LDS.  The host picks NT so that the blocks fill the CUs once (the count
+// phase wants every CU; the look-back wants few blocks).  Phases: count (each lane walks its segments; records in LDS) -> block scan -> decoupled
+// look-back -> cooperative emit of every frame held in LDS (flat order = memory order) -> per
+// segment results; segments whose frames did not fit re-walk their headers to emit.
+template <bool COMPACT, uint32_t KR, uint32_t NT, uint32_t G>
+__global__ __launch_bounds__(NT) void k_walk_fused(WalkArgs a) {
+    constexpr uint32_t NW = NT / 64;
+    __shared__ uint32_t sh_bid;
+    __shared__ SegCount sh_prefix;
+    __shared__ SegCount sh_wave[NW];
+    __shared__ uint32_t sh_wtot[NW];
+    __shared__ uint4 sh_rec[KR * NT];    // [record][lane]: conflict-free 16 B per lane
+    __shared__ uint4 sh_rec2[KR * NT];   // the frame's MsgID / span ordinal / arena offset / previous span end
+    __shared__ uint8_t sh_owner[KR * NT];   // flat replayed frame -> its lane
+    __shared__ uint32_t sh_rpre[NT];        // lane's first flat replayed frame
+    __shared__ uint32_t sh_nbig;            // long spans whose window index the wave writes
+    __shared__ uint4 sh_big[64];
+    // per segment, [segment of the lane][lane]: start, global frame / span (/ arena) bases, counts,
+    // consumed bytes + terminal status, wire end of its last span, replayed from LDS or not
+    __shared__ uint64_t sh_sstart[G * NT], sh_ldend[G * NT];
+    __shared__ uint32_t sh_fbase[G * NT], sh_sbase[G * NT], sh_nf[G * NT], sh_ns[G * NT];
+    __shared__ uint32_t sh_cons[G * NT], sh_endst[G * NT];
+    __shared__ uint64_t sh_abase[COMPACT ? G * NT : 1], sh_ob0[COMPACT ? G * NT : 1];
+    __shared__ uint8_t sh_rep[G * NT], sh_r0[G * NT];   // (sh_r0: the segment's first record in the lane's list)
+    const uint32_t lane = threadIdx.x, wl = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) sh_bid = __hip_atomic_fetch_add(a.lb_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const uint32_t bid = sh_bid;
+    const uint32_t n_blocks = (a.n_segs + NT * G - 1) / (NT * G);
+    const uint32_t s0 = (bid * NT + lane) * G;
+    const SegCount zero = {};
+
+    uint64_t t0 = 0, t1 = 0, t2 = 0;
+    if (a.dbg && lane == 0) t0 = __builtin_amdgcn_s_memrealtime();
+    // ---- count ----
+    SegCount tot = zero;
+    uint32_t nrec = 0;
+    for (uint32_t j = 0; j < G; ++j) {
+        const uint32_t s = s0 + j;
+        const uint32_t q = j * NT + lane;
+        if (s >= a.n_segs) {
+            sh_nf[q] = sh_ns[q] = 0;
+            sh_rep[q] = 0;
+            sh_sstart[q] = ~0ull;
+            continue;
+        }
+        WalkEnd we;
+        const uint32_t cap = KR - nrec;
+        const SegCount c = walk_segment<false, COMPACT, NT>(a, s, zero, zero, sh_rec + nrec * NT + lane, &we,
+                                                            sh_rec2 + nrec * NT + lane, cap, j);
+        const uint64_t ss = a.seg_off[s];
+        const bool rep = c.frames <= cap && a.seg_off[s + 1] - ss <= 0xFFFFFFFFull;
+        sh_r0[q] = (uint8_t)nrec;
+        if (rep) nrec += c.frames;
+        sh_rep[q] = rep ? 1 : 0;
+        sh_sstart[q] = ss;
+        sh_ldend[q] = we.last_dend;
+        sh_nf[q] = c.frames;
+        sh_ns[q] = c.spans0 + c.spans1;
+        sh_cons[q] = (uint32_t)(we.pos - ss);
+        sh_endst[q] = we.status | we.err << 4 | we.close_code << 8;
+        sh_fbase[q] = c.flags;   // (the flags until the bases are known)
+        if constexpr (COMPACT) {
+            sh_abase[q] = c.bytes0 + c.bytes1;
+            sh_ob0[q] = c.bytes0;
+        }
+        wsc_conn_state o;   // the connection's carried state (websocket.go:38-56 subset)
+        o.cont_len = we.cont;
+        o.msg_id = we.msg;
+        o.message_mode = (uint8_t)we.mode;
+        o.cont_utf8 = we.cont ? (uint8_t)we.u8dfa : 0;
+        o.status = (uint8_t)we.status;
+        o.pad = 0;
+        a.state_out[s] = o;
+        tot = sc_add(tot, c);
+    }
+    // ---- block scan of the lanes' totals (64-lane shuffles, then across the waves) ----
+    SegCount inc = tot;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const SegCount o = sc_shfl_up(inc, d);
+        if (wl >= (uint32_t)d) inc = sc_add(o, inc);
+    }
+    SegCount excl = sc_shfl_up(inc, 1);
+    if (wl == 0) excl = zero;
+    if (wl == 63) sh_wave[wave] = inc;
+    __syncthreads();
+    SegCount btot = zero;
+#pragma unroll
+    for (uint32_t w = 0; w < NW; ++w) {
+        if (w < wave) excl = sc_add(excl, sh_wave[w]);
+        btot = sc_add(btot, sh_wave[w]);
+    }
+    // ---- decoupled look-back by the first wave: 64 predecessors are examined per round ----
     if (wave == 0) {
-        // decoupled look-back by one wave: 64 predecessors are examined per round
-        if (a.dbg && lane == 0) t1 = __builtin_amdgcn_s_memrealtime();
+        if (a.dbg && wl == 0) t1 = __builtin_amdgcn_s_memrealtime();
         uint32_t* flag = a.lb_flag;
         uint64_t* agg = a.lb_agg;      // [block][4]
         uint64_t* incl = a.lb_incl;    // [block][4]
-        if (lane == 0) {
+        if (wl == 0) {
             lb_store(bid == 0 ? incl : agg + 4ull * bid, btot);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __hip_atomic_store(flag + bid, bid == 0 ? 2u : 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -707,23 +872,23 @@ __global__ __launch_bounds__(256) void k_walk_fused(WalkArgs a) {
         int64_t j0 = (int64_t)bid - 1;
         uint32_t spins = 0;
         while (j0 >= 0) {
-            const int64_t j = j0 - (int64_t)lane;
+            const int64_t j = j0 - (int64_t)wl;
             const uint32_t f = j >= 0 ? __hip_atomic_fetch_add(flag + j, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                                       : 2u;   // before block 0: an inclusive prefix of zero
             const uint64_t m2 = __ballot(f == 2);
             const uint64_t m0 = __ballot(f == 0);
             const uint32_t first2 = m2 ? (uint32_t)__builtin_ctzll(m2) : 64u;
-            const uint64_t need = first2 >= 63 ? ~0ull : ((2ull << first2) - 1);   // lanes 0..first2
+            const uint64_t need = first2 >= 63 ? ~0ull : ((2ull << first2) - 1);   // wls 0..first2
             if (m0 & need) {   // a predecessor in range has not published yet: poll again
                 if (++spins > (1u << 22)) {   // bounded: never hang the device
-                    if (lane == 0) __hip_atomic_fetch_or(a.lb_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (wl == 0) __hip_atomic_fetch_or(a.lb_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     break;
                 }
                 __builtin_amdgcn_s_sleep(1);
                 continue;
             }
             SegCount v = zero;
-            if (lane <= first2 && j >= 0) v = lb_load((lane == first2 ? incl : agg) + 4ull * j);
+            if (wl <= first2 && j >= 0) v = lb_load((wl == first2 ? incl : agg) + 4ull * j);
 #pragma unroll
             for (int d = 32; d >= 1; d >>= 1) {
                 SegCount o;
@@ -739,7 +904,7 @@ __global__ __launch_bounds__(256) void k_walk_fused(WalkArgs a) {
             if (first2 < 64) break;
             j0 -= 64;
         }
-        if (lane == 0) {
+        if (wl == 0) {
             if (bid != 0) {
                 lb_store(incl + 4ull * bid, sc_add(prefix, btot));
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -749,74 +914,81 @@ __global__ __launch_bounds__(256) void k_walk_fused(WalkArgs a) {
         }
     }
     __syncthreads();
-    if (a.dbg && threadIdx.x == 0) t2 = __builtin_amdgcn_s_memrealtime();
-    const SegCount base = sc_add(sh_prefix, sc_add(wpre, excl));
-    if (s < a.n_segs && (own.flags & SEGF_U8DEFER)) {
-        a.u8seg[s].sbase = base.spans0 + base.spans1;
-        a.u8seg[s].nspans = own.spans0 + own.spans1;
-        a.u8seg[s].fbase = base.frames;
+    if (a.dbg && lane == 0) t2 = __builtin_amdgcn_s_memrealtime();
+    // ---- per segment bases ----
+    {
+        const SegCount lb = sc_add(sh_prefix, excl);   // the lane's first frame / span / arena byte
+        uint32_t fb = lb.frames, sb = lb.spans0 + lb.spans1;
+        uint64_t ab = lb.bytes0 + lb.bytes1;
+        for (uint32_t j = 0; j < G; ++j) {
+            const uint32_t q = j * NT + lane;
+            const uint32_t s = s0 + j;
+            const uint32_t fl = sh_fbase[q];
+            if (s < a.n_segs && (fl & SEGF_U8DEFER)) {
+                a.u8seg[s].sbase = sb;
+                a.u8seg[s].nspans = sh_ns[q];
+                a.u8seg[s].fbase = fb;
+            }
+            sh_fbase[q] = fb;
+            sh_sbase[q] = sb;
+            fb += sh_nf[q];
+            sb += sh_ns[q];
+            if constexpr (COMPACT) {
+                const uint64_t n = sh_abase[q];
+                sh_abase[q] = ab;
+                ab += n;
+            }
+        }
     }
-    // Emit.  Segments whose frames all sit in LDS are emitted by the whole block cooperatively:
-    // their frames in flat order (lane-major) are consecutive records / spans / arena offsets in
-    // memory, so thread t writes flat frames t, t + 256, ... and every store instruction covers
-    // contiguous memory; then the window index of the block's byte range is written window by
-    // window.  Longer segments re-walk their (cache-warm) headers and emit serially.
-    const uint64_t seg_start = s < a.n_segs ? a.seg_off[s] : 0;
-    const uint64_t seg_end = s < a.n_segs ? a.seg_off[s + 1] : 0;
-    const bool replay = s < a.n_segs && own.frames <= KR && seg_end - seg_start <= 0xFFFFFFFFull;
-    const uint32_t rc = replay ? own.frames : 0u;
-    uint32_t rv = rc;   // block scan of the replayed frame counts
+    // ---- flat order of the frames held in LDS ----
+    uint32_t rv = nrec;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
         const uint32_t o = __shfl_up(rv, d);
-        if (lane >= (uint32_t)d) rv += o;
+        if (wl >= (uint32_t)d) rv += o;
     }
-    if (lane == 63) sh_wtot[wave] = rv;
-    sh_sstart[threadIdx.x] = seg_start;
-    sh_fbase[threadIdx.x] = base.frames;
-    sh_sbase[threadIdx.x] = base.spans0 + base.spans1;
-    if constexpr (COMPACT) {
-        sh_abase[threadIdx.x] = base.bytes0 + base.bytes1;
-        sh_ob0[threadIdx.x] = own.bytes0;
-    }
-    sh_replay[threadIdx.x] = replay ? 1 : 0;
+    if (wl == 63) sh_wtot[wave] = rv;
+    if (lane == 0) sh_nbig = 0;
     __syncthreads();
-    uint32_t rpre = rv - rc, F = 0;
+    uint32_t rpre = rv - nrec, F = 0;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        if ((uint32_t)q < wave) rpre += sh_wtot[q];
-        F += sh_wtot[q];
+    for (uint32_t w = 0; w < NW; ++w) {
+        if (w < wave) rpre += sh_wtot[w];
+        F += sh_wtot[w];
     }
-    sh_rpre[threadIdx.x] = rpre;
-    for (uint32_t k = 0; k < rc; ++k) sh_owner[rpre + k] = (uint8_t)threadIdx.x;
-    if (threadIdx.x == 0) sh_nbig = 0;
+    sh_rpre[lane] = rpre;
+    for (uint32_t k = 0; k < nrec; ++k) sh_owner[rpre + k] = (uint8_t)lane;
     __syncthreads();
+    // ---- cooperative emit: the block's replayed frames in flat order are consecutive records,
+    //      spans and arena offsets in memory, so each store instruction covers contiguous bytes ----
     const uint32_t W = 1u << a.win_shift;
-    for (uint32_t f = threadIdx.x; f < F; f += 256) {
+    for (uint32_t f = lane; f < F; f += NT) {
         const uint32_t o = sh_owner[f];
         const uint32_t k = f - sh_rpre[o];
-        const uint4 r = sh_rec[k * 256 + o];
-        const uint4 q = sh_rec2[k * 256 + o];
-        const uint64_t ss = sh_sstart[o];
-        const uint32_t fi = sh_fbase[o] + k;
+        const uint4 r = sh_rec[k * NT + o];
+        const uint4 q = sh_rec2[k * NT + o];
+        const uint32_t j = r.w >> 27;
+        const uint32_t qi = j * NT + o;
+        const uint64_t ss = sh_sstart[qi];
         const uint32_t hl = (r.w >> 13) & 15, fl = (r.w >> 17) & 0x7F, region = (r.w >> 24) & 1;
         const bool have_span = (r.w >> 25) & 1;
         const uint64_t hdr_off = ss + r.x;
         uint64_t dst = ~0ull;
         if constexpr (COMPACT)
-            if (fl & WSC_FF_UNMASKED) dst = sh_abase[o] + (region ? sh_ob0[o] : 0ull) + q.z;
-        if (fi < a.frames_cap) {
+            if (fl & WSC_FF_UNMASKED) dst = sh_abase[qi] + (region ? sh_ob0[qi] : 0ull) + q.z;
+        const uint32_t fidx = sh_fbase[qi] + (k - sh_r0[qi]);   // the segment's first frame + ordinal
+        if (fidx < a.frames_cap) {
             const uint4 r0 = make_uint4((uint32_t)hdr_off, (uint32_t)(hdr_off >> 32), r.y, r.z);
-            const uint4 r1 = make_uint4(bid * 256 + o, q.x,
+            const uint4 r1 = make_uint4((bid * NT + o) * G + j, q.x,
                                         (r.w & 0xF) | ((r.w >> 4) & 1) << 8 | ((r.w >> 5) & 7) << 16 |
                                             ((r.w >> 8) & 3) << 24,
                                         ((r.w >> 10) & 7) | hl << 8 | fl << 16);
-            reinterpret_cast<uint4*>(a.frames + fi)[0] = r0;
-            reinterpret_cast<uint4*>(a.frames + fi)[1] = r1;
-            if constexpr (COMPACT) a.frame_dst[fi] = dst;
+            reinterpret_cast<uint4*>(a.frames + fidx)[0] = r0;
+            reinterpret_cast<uint4*>(a.frames + fidx)[1] = r1;
+            if constexpr (COMPACT) a.frame_dst[fidx] = dst;
         }
         if (have_span) {
-            const uint32_t idx = sh_sbase[o] + q.y;
+            const uint32_t idx = sh_sbase[qi] + q.y;
             Span sp;
             sp.src = hdr_off + hl;
             sp.len = r.y;
@@ -826,10 +998,10 @@ __global__ __launch_bounds__(256) void k_walk_fused(WalkArgs a) {
             // windows starting in [previous span end, this span end) look this span up first
             uint64_t t = (ss + q.w + W - 1) >> a.win_shift;
             const uint64_t t_end = ((sp.src + r.y - 1) >> a.win_shift) + 1;
-            if (t_end > t + 64) {   // a long span: its windows are written by a whole wave below
-                const uint32_t j = atomicAdd(&sh_nbig, 1u);
-                if (j < 64) {
-                    sh_big[j] = make_uint4((uint32_t)t, (uint32_t)(t >> 32), (uint32_t)(t_end - t), idx);
+            if (t_end > t + 64) {   // a long span: its windows are written by the whole wave below
+                const uint32_t jb = atomicAdd(&sh_nbig, 1u);
+                if (jb < 64) {
+                    sh_big[jb] = make_uint4((uint32_t)t, (uint32_t)(t >> 32), (uint32_t)(t_end - t), idx);
                     t = t_end;
                 }
             }
@@ -839,47 +1011,63 @@ __global__ __launch_bounds__(256) void k_walk_fused(WalkArgs a) {
             for (; t < t_end; ++t) a.tile_first[t] = idx;
         }
     }
-    // window index of long spans (more than 64 windows: 256 KiB+ payloads), one wave per span
     __syncthreads();
     {
         const uint32_t nbig = sh_nbig < 64 ? sh_nbig : 64;
-        for (uint32_t j = wave; j < nbig; j += 4) {
-            const uint64_t tb = sh_big[j].x | (uint64_t)sh_big[j].y << 32;
-            const uint32_t nw = sh_big[j].z, idx = sh_big[j].w;
-            for (uint32_t i = lane; i < nw; i += 64) a.tile_first[tb + i] = idx;
+        for (uint32_t jb = wave; jb < nbig; jb += NW) {   // one wave per long span
+            const uint64_t tb = sh_big[jb].x | (uint64_t)sh_big[jb].y << 32;
+            const uint32_t nw = sh_big[jb].z, idx = sh_big[jb].w;
+            for (uint32_t i = wl; i < nw; i += 64) a.tile_first[tb + i] = idx;
         }
     }
-    if (s < a.n_segs) {
-        if (replay) {             // the segment's own outputs (its frames and windows were written above)
-            EmitCtx e = emit_begin<COMPACT>(a, s, seg_start, seg_end, base, own);
-            e.nf = own.frames;
-            e.ns0 = own.spans0;
-            e.ns1 = own.spans1;
-            const uint64_t Wd = 1ull << a.win_shift;   // windows after the last span: emit_end
-            const uint64_t lo = wend.last_dend > seg_start ? wend.last_dend : seg_start;
-            e.nx0 = (lo + Wd - 1) & ~(Wd - 1);
-            emit_end<COMPACT>(a, e, wend);
-        } else {                  // long segment: re-walk the (cache-warm) headers
-            walk_segment<true, COMPACT>(a, s, base, own, nullptr, nullptr);
+    // ---- per segment results; segments not held in LDS re-walk their (cache-warm) headers ----
+    for (uint32_t j = 0; j < G; ++j) {
+        const uint32_t s = s0 + j;
+        if (s >= a.n_segs) break;
+        const uint32_t q = j * NT + lane;
+        const uint64_t se = a.seg_off[s + 1];
+        if (sh_rep[q]) {
+            const uint64_t Wd = W;   // windows that start after the last span, up to the segment end
+            const uint32_t nx = sh_sbase[q] + sh_ns[q];
+            for (uint64_t x = (sh_ldend[q] + Wd - 1) & ~(Wd - 1); x < se; x += Wd) a.tile_first[x >> a.win_shift] = nx;
+            wsc_seg_result r;
+            r.consumed = sh_cons[q];
+            r.frame_begin = sh_fbase[q];
+            r.frame_count = sh_nf[q];
+            r.status = sh_endst[q] & 0xF;
+            r.close_code = sh_endst[q] >> 8;
+            r.err = (sh_endst[q] >> 4) & 0xF;
+            r.pad = 0;
+            a.seg_out[s] = r;
+        } else {
+            SegCount base = zero, own = zero;
+            base.frames = sh_fbase[q];
+            base.spans0 = sh_sbase[q];
+            own.frames = sh_nf[q];
+            if constexpr (COMPACT) {
+                base.bytes0 = sh_abase[q];
+                own.bytes0 = sh_ob0[q];
+            }
+            walk_segment<true, COMPACT, NT>(a, s, base, own, nullptr, nullptr);
         }
     }
     if (a.dbg) {   // diagnostic timestamps (100 MHz s_memrealtime), written only to the dbg buffer
         __syncthreads();
-        if (threadIdx.x == 0) {
+        if (lane == 0) {
             a.dbg[4 * bid + 0] = t0;
             a.dbg[4 * bid + 1] = t1;
             a.dbg[4 * bid + 2] = t2;
             a.dbg[4 * bid + 3] = __builtin_amdgcn_s_memrealtime();
         }
     }
-    if (bid == n_blocks - 1 && threadIdx.x == 0) {
-        const SegCount tot = sc_add(sh_prefix, btot);
+    if (bid == n_blocks - 1 && lane == 0) {
+        const SegCount tt = sc_add(sh_prefix, btot);
         wsc_summary sm;
-        sm.data_bytes = COMPACT ? tot.bytes0 : 0;
-        sm.ctrl_bytes = COMPACT ? tot.bytes1 : 0;
-        sm.n_frames = tot.frames;
-        sm.n_spans = tot.spans0 + tot.spans1;
-        sm.overflow = (tot.frames > a.frames_cap || tot.spans0 + tot.spans1 > a.spans_cap) ? 1u : 0u;
+        sm.data_bytes = COMPACT ? tt.bytes0 : 0;
+        sm.ctrl_bytes = COMPACT ? tt.bytes1 : 0;
+        sm.n_frames = tt.frames;
+        sm.n_spans = tt.spans0 + tt.spans1;
+        sm.overflow = (tt.frames > a.frames_cap || tt.spans0 + tt.spans1 > a.spans_cap) ? 1u : 0u;
         if (__hip_atomic_load(a.lb_err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) sm.overflow |= 2u;
         sm.pad = 0;
         *a.summary = sm;
@@ -1166,12 +1354,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
     }
 }
 
-// explicit instantiations used by the host code
-template __global__ void k_walk_fused<false, KREC>(WalkArgs);
-template __global__ void k_walk_fused<true, KREC>(WalkArgs);
-template __global__ void k_walk_fused<false, 8>(WalkArgs);
-template __global__ void k_walk_fused<true, 8>(WalkArgs);
-template __global__ void k_walk_fused<false, 2>(WalkArgs);
-template __global__ void k_walk_fused<true, 2>(WalkArgs);
+// explicit instantiations used by the host code: 16 frame records per lane, one segment per
+// lane, blocks of 64 or 256 lanes; batches of more segments use the three-launch walk below
+template __global__ void k_walk_fused<false, 16, 64, 1>(WalkArgs);
+template __global__ void k_walk_fused<true, 16, 64, 1>(WalkArgs);
+template __global__ void k_walk_fused<false, 16, 256, 1>(WalkArgs);
+template __global__ void k_walk_fused<true, 16, 256, 1>(WalkArgs);
+template __global__ void k_walk_count<false>(WalkArgs);
+template __global__ void k_walk_count<true>(WalkArgs);
+template __global__ void k_walk_emit<false>(WalkArgs);
+template __global__ void k_walk_emit<true>(WalkArgs);
 
 }  // namespace wsc

@@ -74,7 +74,7 @@ struct WalkArgs {
     uint32_t frames_cap;
     const wsc_conn_state* state_in;
     uint64_t max_frame_len;
-    SegCount* counts;
+    SegCount* counts;            // three-launch walk: per segment counts
     wsc_frame* frames;
     Span* spans;
     uint32_t spans_cap;

@@ -36,7 +36,7 @@
 // heartbeat goroutines call Close() -> remove(), websocket_ctrl.go:73-96); it only queues the
 // handle, and the poller thread applies queued removals at its next session call.  Every other
 // function belongs to the one poller thread that owns the session.
-#include <hip/hip_runtime.h>
+#include <hip/hip_runtime_api.h>
 
 #include <atomic>
 #include <chrono>
@@ -756,6 +756,18 @@ int wsc_session_decode(wsc_session* s) {
         if (!more) return WSC_OK;
     }
     return WSC_E_CAPACITY;
+}
+
+// bytes fed but not yet submitted (the staging being filled + connections' spills): a poller calls
+// submit again while this is non-zero, even in a round without new reads
+int wsc_session_pending(wsc_session* s, uint64_t* bytes) {
+    if (!s || !bytes) return WSC_E_INVAL;
+    apply_removes(s);
+    uint64_t n = s->st[s->fill].bytes;
+    for (const Conn& c : s->conns)
+        if (c.live && !c.failed && c.st.status == WSC_SEG_OPEN) n += c.spill.size();
+    *bytes = n;
+    return WSC_OK;
 }
 
 int wsc_session_next(wsc_session* s, uint32_t conn, wsc_event* ev) {

@@ -61,12 +61,12 @@ def test_fuzz_single_batch(codec, compact):
     _check_batch(codec, streams, compact=compact)
 
 
-@pytest.mark.parametrize("compact,krec", [(False, 2), (True, 2), (False, 8), (True, 8)])
-def test_fuzz_walk_few_records(codec_lib, monkeypatch, compact, krec):
-    """The walk instances for many segments (2 or 8 LDS frame records per lane; segments with
-    more frames re-walked by the emit pass, the rest emitted cooperatively by the block), forced
-    on fuzz streams of 5..44 units with text and errors, and of 1..6 units."""
-    monkeypatch.setenv("WSC_WALK_KREC", str(krec))
+@pytest.mark.parametrize("compact,mode", [(False, 3), (True, 3), (False, 256), (True, 256), (False, 64), (True, 64)])
+def test_fuzz_walk_geometries(codec_lib, monkeypatch, compact, mode):
+    """Every walk geometry forced on the same fuzz batches (5..44 units with text and errors, and
+    1..6 units): the fused walk with 64- and 256-lane blocks (16 LDS records per lane, longer
+    segments re-walked, the rest emitted cooperatively) and the three-launch walk."""
+    monkeypatch.setenv("WSC_WALK_MODE", str(mode))
     c = K.Codec(0, max_batch_bytes=64 << 20, max_segs=1 << 14, max_frames=1 << 18)
     try:
         streams = [random_stream(7000 + i, n_units=int(5 + i % 40), text_p=0.5) for i in range(400)]

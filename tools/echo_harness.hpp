@@ -48,6 +48,7 @@ struct Decoder {
     virtual bool pipelined() const { return false; }
     virtual void submit() { decode(); }
     virtual void complete() {}
+    virtual bool pending() { return false; }   // fed bytes a batch could not take yet
 };
 
 struct Result {
@@ -286,7 +287,7 @@ inline Result run(Decoder& dec, int conns, int frames, size_t frame_bytes, int c
             }
         }
         if (pipe) {
-            if (!fed.empty()) {
+            if (!fed.empty() || dec.pending()) {
                 dec.submit();          // round r+1 on the device ...
                 res.rounds++;
             }

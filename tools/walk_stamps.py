@@ -25,7 +25,12 @@ t = [torch.from_numpy(cfg["wire"]).to(dev), torch.from_numpy(cfg["seg_off"].view
 arena = torch.zeros(len(cfg["wire"]) + 64, dtype=torch.uint8, device=dev) if compact else None
 fdst = torch.zeros(cfg["n_frames"] + 16, dtype=torch.int64, device=dev) if compact else None
 b = c.make_batch(t[0], t[1], None, t[2], t[3], t[4], t[5], compact=compact, arena=arena, frame_dst=fdst)
-nb = (n + 255) // 256
+n_cu = torch.cuda.get_device_properties(0).multi_processor_count
+if n > 256 * n_cu:   # the library's walk geometry (wsc_api.cpp walk_mode): three-launch walk, no stamps
+    print(f"{wl}: {n} segments -> three-launch walk (no per-block stamps)")
+    print(c.profile(b, 5) if False else "")
+    raise SystemExit(0)
+nb = (n + 63) // 64 if n <= 64 * n_cu else (n + 255) // 256
 for it in range(3):
     c.decode(b)
     c.sync()

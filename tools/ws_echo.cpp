@@ -40,6 +40,10 @@ struct GpuDecoder : echo::Decoder {
     bool pipelined() const override { return pipe; }
     void submit() override { check(wsc_session_submit(s), "wsc_session_submit"); }
     void complete() override { check(wsc_session_complete(s), "wsc_session_complete"); }
+    bool pending() override {
+        uint64_t n = 0;
+        return wsc_session_pending(s, &n) == WSC_OK && n > 0;
+    }
     void decode() override { check(wsc_session_decode(s), "wsc_session_decode"); }
     static void check(int rc, const char* what) {
         if (rc != WSC_OK) {
