@@ -220,9 +220,7 @@ __device__ __forceinline__ uint4 rec_pack(const wsc_frame& fr, uint64_t seg_star
 // speculative header is used only when its address is the real next position, so results never
 // depend on the guess; frames that repeat their size (the common case on one connection) cost
 // one round trip per SPEC_D frames.  All loads of a round are waited together.
-constexpr int SPEC_D = 4;
-
-template <bool EMIT, bool COMPACT, uint32_t LS = 64>
+template <bool EMIT, bool COMPACT, uint32_t LS = 64, int SPEC_D = 4>
 __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, const SegCount& base,
                                                  const SegCount& own, uint4* lrec, WalkEnd* wend,
                                                  uint4* lrec2 = nullptr, uint32_t cap = 0, uint32_t tag = 0) {
@@ -487,12 +485,11 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
         return status == WSC_SEG_OPEN;
     };
 
-    // Fast path (counting pass): a complete, masked FIN BIN frame (0x82) while no fragmented
+    // Fast path (both passes): a complete, masked FIN BIN frame (0x82) while no fragmented
     // message is open (cont == 0) is always Message{MsgID: msg, Opcode: 2} (websocket.go:142-146,
     // websocket_frame.go:52-91; messageMode 2 -> 0, msgID + 1): its record is written without the
     // general state machine.  Everything else goes through `step`.
     auto fast = [&](const uint4& hd) -> bool {
-        if constexpr (EMIT) return false;
         const uint32_t b0 = hd.x & 0xFFu, b1 = (hd.x >> 8) & 0xFFu;
         if (b0 != 0x82u || !(b1 & 0x80u) || cont != 0) return false;
         const uint32_t len7 = b1 & 0x7Fu;
@@ -529,7 +526,8 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
         fr.flags = WSC_FF_UNMASKED;
         fr.pad = 0;
         const bool have_span = plen > 0;
-        record(fr, have_span, 0, true, plen);
+        if constexpr (EMIT) emit_frame<COMPACT>(a, e, fr, (uint32_t)plen, have_span, 0);
+        else record(fr, have_span, 0, true, plen);
         msg += 1;
         mode = 0;
         nf += 1;
@@ -670,6 +668,22 @@ __device__ __forceinline__ SegCount block_excl_scan(const SegCount& v, SegCount&
     return excl;
 }
 
+__device__ __forceinline__ SegCount agg_load(const uint64_t* p) {
+    SegCount v;
+    v.frames = (uint32_t)p[0];
+    v.spans0 = (uint32_t)(p[0] >> 32);
+    v.spans1 = (uint32_t)p[1];
+    v.flags = (uint32_t)(p[1] >> 32);
+    v.bytes0 = p[2];
+    v.bytes1 = p[3];
+    return v;
+}
+__device__ __forceinline__ void agg_store(uint64_t* q, const SegCount& v) {
+    q[0] = (uint64_t)v.frames | ((uint64_t)v.spans0 << 32);
+    q[1] = (uint64_t)v.spans1 | ((uint64_t)v.flags << 32);
+    q[2] = v.bytes0;
+    q[3] = v.bytes1;
+}
 template <bool COMPACT>
 __global__ __launch_bounds__(256) void k_walk_count(WalkArgs a) {
     __shared__ SegCount sh_wave[4];
@@ -683,41 +697,32 @@ __global__ __launch_bounds__(256) void k_walk_count(WalkArgs a) {
     }
     SegCount tot;
     (void)block_excl_scan<256>(own, tot, sh_wave);
-    if (threadIdx.x == 0) {   // the next launch reads it (kernel boundary: visible)
-        uint64_t* p = a.lb_agg + 4ull * blockIdx.x;
-        p[0] = (uint64_t)tot.frames | ((uint64_t)tot.spans0 << 32);
-        p[1] = (uint64_t)tot.spans1 | ((uint64_t)tot.flags << 32);
-        p[2] = tot.bytes0;
-        p[3] = tot.bytes1;
-    }
+    if (threadIdx.x == 0) agg_store(a.lb_agg + 4ull * blockIdx.x, tot);   // read by the next launch
 }
 
+// one block: thread t owns the SCAN_PER consecutive block totals starting at t * SCAN_PER (all its
+// loads in flight at once), scans them in registers, then one block-wide scan of the threads' sums
+constexpr uint32_t SCAN_PER = 8;
 __global__ __launch_bounds__(256) void k_walk_scan(WalkArgs a, uint32_t n_blocks) {
     __shared__ SegCount sh_wave[4];
     __shared__ SegCount sh_carry;
     const SegCount zero = {};
     if (threadIdx.x == 0) sh_carry = zero;
     __syncthreads();
-    for (uint32_t b0 = 0; b0 < n_blocks; b0 += 256) {
-        const uint32_t b = b0 + threadIdx.x;
-        SegCount v = zero;
-        if (b < n_blocks) {
-            const uint64_t* p = a.lb_agg + 4ull * b;
-            v.frames = (uint32_t)p[0];
-            v.spans0 = (uint32_t)(p[0] >> 32);
-            v.spans1 = (uint32_t)p[1];
-            v.flags = (uint32_t)(p[1] >> 32);
-            v.bytes0 = p[2];
-            v.bytes1 = p[3];
-        }
+    for (uint32_t b0 = 0; b0 < n_blocks; b0 += 256 * SCAN_PER) {
+        const uint32_t first = b0 + threadIdx.x * SCAN_PER;
+        SegCount v[SCAN_PER];
+#pragma unroll
+        for (uint32_t i = 0; i < SCAN_PER; ++i) v[i] = first + i < n_blocks ? agg_load(a.lb_agg + 4ull * (first + i)) : zero;
+        SegCount sum = zero;
+#pragma unroll
+        for (uint32_t i = 0; i < SCAN_PER; ++i) sum = sc_add(sum, v[i]);
         SegCount tot;
-        const SegCount ex = sc_add(sh_carry, block_excl_scan<256>(v, tot, sh_wave));
-        if (b < n_blocks) {
-            uint64_t* q = a.lb_incl + 4ull * b;   // exclusive prefix of block b
-            q[0] = (uint64_t)ex.frames | ((uint64_t)ex.spans0 << 32);
-            q[1] = (uint64_t)ex.spans1 | ((uint64_t)ex.flags << 32);
-            q[2] = ex.bytes0;
-            q[3] = ex.bytes1;
+        SegCount ex = sc_add(sh_carry, block_excl_scan<256>(sum, tot, sh_wave));
+#pragma unroll
+        for (uint32_t i = 0; i < SCAN_PER; ++i) {
+            if (first + i < n_blocks) agg_store(a.lb_incl + 4ull * (first + i), ex);   // exclusive prefix
+            ex = sc_add(ex, v[i]);
         }
         __syncthreads();
         if (threadIdx.x == 0) sh_carry = sc_add(sh_carry, tot);
@@ -746,15 +751,7 @@ __global__ __launch_bounds__(256) void k_walk_emit(WalkArgs a) {
     SegCount tot;
     const SegCount ex = block_excl_scan<256>(own, tot, sh_wave);
     if (s >= a.n_segs) return;
-    const uint64_t* q = a.lb_incl + 4ull * blockIdx.x;
-    SegCount bp;
-    bp.frames = (uint32_t)q[0];
-    bp.spans0 = (uint32_t)(q[0] >> 32);
-    bp.spans1 = (uint32_t)q[1];
-    bp.flags = (uint32_t)(q[1] >> 32);
-    bp.bytes0 = q[2];
-    bp.bytes1 = q[3];
-    const SegCount base = sc_add(bp, ex);
+    const SegCount base = sc_add(agg_load(a.lb_incl + 4ull * blockIdx.x), ex);
     if (own.flags & SEGF_U8DEFER) {
         a.u8seg[s].sbase = base.spans0 + base.spans1;
         a.u8seg[s].nspans = own.spans0 + own.spans1;
