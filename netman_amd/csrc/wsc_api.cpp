@@ -172,8 +172,17 @@ int wsc_create(int device, const wsc_config* cfg_in, wsc_ctx** out) {
         if (e != hipSuccess && rc == WSC_OK) rc = fail(WSC_E_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
     };
     chk(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate");
-    chk(hipEventCreateWithFlags(&c->ev_walked, hipEventDisableTiming), "hipEventCreate");
-    chk(hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming), "hipEventCreate");
+    // the split pipeline's events join streams of this device only: no system-scope fence at the
+    // record (which writes back and invalidates caches; measured ~13 us between one batch's unmask
+    // and the next -- as long as the walk the split was meant to hide).  Kernel ends still release
+    // at device scope, which is what the other stream's kernels need.
+    unsigned ev_flags = hipEventDisableTiming | hipEventDisableSystemFence;
+    if (const char* e = std::getenv("WSC_EVENT_FENCE"); e && *e) {   // A/B: 0 system, 1 device, 2 no system fence
+        const int f = std::atoi(e);
+        ev_flags = hipEventDisableTiming | (f == 1 ? hipEventReleaseToDevice : (f == 2 ? hipEventDisableSystemFence : 0u));
+    }
+    chk(hipEventCreateWithFlags(&c->ev_walked, ev_flags), "hipEventCreate");
+    chk(hipEventCreateWithFlags(&c->ev_done, ev_flags), "hipEventCreate");
     chk(hipMalloc(&c->sticky, sizeof(uint32_t)), "hipMalloc sticky");
     chk(hipMalloc(&c->counts, (uint64_t)cfg.max_segs * sizeof(SegCount)), "hipMalloc counts");
     if (rc == WSC_OK) chk(hipMemsetAsync(c->sticky, 0, sizeof(uint32_t), c->stream), "hipMemset sticky");
