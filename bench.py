@@ -32,7 +32,7 @@ PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--frames", type=int, default=FRAMES)
     ap.add_argument("--frame-bytes", type=int, default=FRAME_BYTES)
@@ -50,6 +50,10 @@ def parse():
                          "many CUs, the UTF-8 check + unmask on --unmask-streams streams over every CU "
                          "(0 = every stage of a batch in order on its own stream)")
     ap.add_argument("--unmask-streams", type=int, default=1)
+    ap.add_argument("--staged", type=int, default=1,
+                    help="split pipeline staged by the host: walk, wait for it, then the unmask, so "
+                         "consecutive unmasks follow each other on the unmask stream with no dependency "
+                         "packet, event or empty check kernel between them; 0 = wsc_decode_split")
     ap.add_argument("--unmask-rest", action="store_true", help="mask the unmask streams to the CUs the walk does not use")
     ap.add_argument("--no-echo", action="store_true", help="skip the configs[0] loopback echo lines")
     ap.add_argument("--no-config3", action="store_true",
@@ -177,6 +181,17 @@ def main():
     def run(steps, depth):
         # batch i goes to context i % depth: independent batches (chaining the unmasks with
         # events measured slower: 0.361 vs 0.352 ms per step)
+        if split and depth == P and a.staged:
+            # staged: batch i+1's walk is enqueued, the host waits for it (it runs beside batch
+            # i's unmask), then batch i+1's unmask follows batch i's on the unmask stream with no
+            # dependency packet between them
+            for i in range(steps):
+                j = i % depth
+                codecs[j].decode_walk(batches[j], walk_st)
+                codecs[j].walk_wait()
+                codecs[j].decode_finish(batches[j], unmask_st[j % len(unmask_st)])
+                n_dec[j] += 1
+            return
         for i in range(steps):
             j = i % depth
             if split and depth == P:

@@ -204,6 +204,20 @@ int wsc_error_flags(wsc_ctx* ctx, uint32_t* flags, int clear);
  * decode at a time: order a split decode and any other call on the same context yourself.     */
 int wsc_decode_split(wsc_ctx* ctx, const wsc_batch* batch, void* walk_stream, void* unmask_stream);
 
+/* The split decode in two calls, for a host that pipelines batches: wsc_decode_walk enqueues
+ * the header walk on `walk_stream`; wsc_decode_finish enqueues the rest (UTF-8 check, unmask) on
+ * `unmask_stream`, joined to the walk by a stream wait only if it has not completed yet, and
+ * without the check's launch when the completed walk deferred no text.  The staged unmask records
+ * no event: its last workgroup signals the host through a pinned word, and the context's next
+ * decode waits for that on the host before it reuses the walk's scratch (so a host that pipelines
+ * keeps two or more contexts).  wsc_walk_wait blocks the host until the context's last walk has
+ * completed: calling it between the two (while the device still unmasks the previous batch) makes
+ * the unmasks of consecutive batches follow each other on their stream with nothing in between.
+ * Results of a finished decode are read after synchronising `unmask_stream` as usual.        */
+int wsc_decode_walk(wsc_ctx* ctx, const wsc_batch* batch, void* walk_stream);
+int wsc_decode_finish(wsc_ctx* ctx, const wsc_batch* batch, void* unmask_stream);
+int wsc_walk_wait(wsc_ctx* ctx);
+
 /* A non-blocking stream on the context's device, restricted to the CUs whose bits are set in
  * cu_mask[0..mask_words) (hipExtStreamCreateWithCUMask); cu_mask NULL = all CUs.             */
 int wsc_stream_create(wsc_ctx* ctx, const uint32_t* cu_mask, uint32_t mask_words, void** out);

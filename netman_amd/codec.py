@@ -99,6 +99,9 @@ SIGNATURES = {
     "wsc_summary_status": (_I, [_P]),
     "wsc_error_flags": (_I, [_P, C.POINTER(_U32), _I]),
     "wsc_decode_split": (_I, [_P, C.POINTER(WscBatch), _P, _P]),
+    "wsc_decode_walk": (_I, [_P, C.POINTER(WscBatch), _P]),
+    "wsc_decode_finish": (_I, [_P, C.POINTER(WscBatch), _P]),
+    "wsc_walk_wait": (_I, [_P]),
     "wsc_stream_create": (_I, [_P, _P, _U32, C.POINTER(_P)]),
     "wsc_stream_destroy": (_I, [_P, _P]),
     "wsc_decode_host": (_I, [_P, _P, _U64, _P, _U32, _U32, _P, _P, _P, _P, _U32, _P, _P, _P]),
@@ -272,6 +275,16 @@ class Codec:
             a = a.reshape(1)          # a record scalar (e.g. summary[0]) -> 1-element array
         a = np.ascontiguousarray(np.ascontiguousarray(a).view(np.uint8).reshape(-1)[:32])
         return load_library().wsc_summary_status(a.ctypes.data)
+
+    def decode_walk(self, batch: WscBatch, walk_stream: int):
+        """staged split decode, part 1: the walk (waits on the host for this context's last staged unmask)"""
+        _check(self.lib.wsc_decode_walk(self.h, C.byref(batch), walk_stream), "wsc_decode_walk")
+
+    def decode_finish(self, batch: WscBatch, unmask_stream: int):
+        _check(self.lib.wsc_decode_finish(self.h, C.byref(batch), unmask_stream), "wsc_decode_finish")
+
+    def walk_wait(self):
+        _check(self.lib.wsc_walk_wait(self.h), "wsc_walk_wait")
 
     def stream_create(self, cu_mask=None) -> int:
         """a raw hipStream_t (int), restricted to the CUs set in cu_mask (list of u32 words)"""

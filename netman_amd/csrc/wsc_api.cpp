@@ -3,6 +3,7 @@
 // missing device is an error, WSC_E_NODEVICE).
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -18,7 +19,7 @@ template <bool COMPACT> __global__ void k_walk_emit(WalkArgs);
 __global__ void k_u8_check(U8Args);
 template <bool COMPACT, int P, int NT, int MINW>
 __global__ void k_unmask(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*,
-                         const wsc_summary*, uint32_t*, uint32_t);
+                         const wsc_summary*, uint32_t*, uint32_t, uint32_t*, uint32_t*, uint32_t);
 __global__ void k_encode_scan(EncArgs);
 template <int NT> __global__ void k_encode_copy(EncCopyArgs);
 }  // namespace wsc
@@ -52,6 +53,19 @@ struct wsc_ctx {
     hipStream_t stream = nullptr;
     hipEvent_t ev_walked = nullptr;   // wsc_decode_split: walk done (unmask stream waits on it)
     hipEvent_t ev_done = nullptr;     // wsc_decode_split: unmask done (the next walk on this ctx waits)
+    // host-visible words (pinned, coherent): [0] the walk deferred UTF-8 items, [1] sequence number
+    // of the last staged unmask that has finished (written by its last workgroup)
+    uint32_t* hflag = nullptr;
+    uint32_t* fin_ctr = nullptr;      // staged unmask: finished-workgroup counters (two-level, self re-arming)
+    uint32_t fin_seq = 0;             // sequence number of the last staged unmask enqueued
+    bool fin_pending = false;         // a staged unmask was enqueued without ev_done
+    hipStream_t fin_stream = nullptr; // ... on this stream
+    bool walk_waited = false;         // wsc_walk_wait saw the last walk complete
+    int walk_delay_us = 0;            // WSC_WALK_DELAY_US (A/B experiment)
+    int unmask_buf = 3;               // WSC_UNMASK_BUF: in-place windows through buffer ops (1 nt, 2 nt sc1, 3 sc0 nt sc1
+                                      // stores; 0 = 64-bit global addresses).  3: headline 2,890-2,898 -> 2,911-2,918
+                                      // GiB/s (A/B on one box, profiles/r02_unmask_policy.log)
+    int stage_variant = 0;            // WSC_STAGE_VARIANT (A/B): bit 0 = wsc_walk_wait polls hipEventQuery
     wsc_config cfg{};
     uint32_t pieces = 8;          // 16 B pieces per lane -> window = pieces KiB
     uint32_t* sticky = nullptr;      // error bits of every decode/encode (wsc_error_flags), never re-armed
@@ -106,6 +120,33 @@ static uint32_t walk_mode(const wsc_ctx* c, uint32_t n_segs) {
     if (n_segs <= 64u * (uint32_t)c->n_cu) return 64;
     if (n_segs <= 256u * (uint32_t)c->n_cu) return 256;
     return 3;
+}
+
+// The staged pipeline's unmask records no event (a marker between two unmasks costs ~6 us of
+// idle chip): its last workgroup writes the sequence number to hflag[1] instead, and the next
+// walk on this context waits for it here, on the host.  A stream that drains without the word
+// arriving means the unmask failed.
+static int fin_wait(wsc_ctx* c) {
+    if (!c->fin_pending) return WSC_OK;
+    // no HIP call while the unmask is expected to finish: hipStreamQuery puts a marker packet on
+    // the stream (measured: a 5.6 us gap between consecutive unmasks); only a wait that has lasted
+    // 100 ms asks the stream whether it is still busy
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    for (uint32_t spin = 1;; ++spin) {
+        if (__atomic_load_n(&c->hflag[1], __ATOMIC_ACQUIRE) == c->fin_seq) break;
+        if ((spin & 4095) == 0 && clk::now() - t0 > std::chrono::milliseconds(100)) {
+            const hipError_t q = hipStreamQuery(c->fin_stream);
+            if (q == hipErrorNotReady) continue;
+            if (__atomic_load_n(&c->hflag[1], __ATOMIC_ACQUIRE) == c->fin_seq) break;
+            c->fin_pending = false;
+            return fail(WSC_E_DEVICE, std::string("staged unmask did not finish: ") +
+                                          (q == hipSuccess ? "stream drained" : hipGetErrorString(q)));
+        }
+        __builtin_ia32_pause();
+    }
+    c->fin_pending = false;
+    return WSC_OK;
 }
 
 int wsc_abi_version(void) { return WSC_ABI_VERSION; }
@@ -183,6 +224,12 @@ int wsc_create(int device, const wsc_config* cfg_in, wsc_ctx** out) {
     }
     chk(hipEventCreateWithFlags(&c->ev_walked, ev_flags), "hipEventCreate");
     chk(hipEventCreateWithFlags(&c->ev_done, ev_flags), "hipEventCreate");
+    chk(hipHostMalloc(&c->hflag, 64, hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc hflag");
+    chk(hipMalloc(&c->fin_ctr, 257 * 32 * sizeof(uint32_t)), "hipMalloc fin_ctr");   // k_unmask FIN_GROUPS/STRIDE
+    if (rc == WSC_OK) {
+        std::memset(c->hflag, 0, 64);
+        chk(hipMemsetAsync(c->fin_ctr, 0, 257 * 32 * sizeof(uint32_t), c->stream), "hipMemset fin_ctr");
+    }
     chk(hipMalloc(&c->sticky, sizeof(uint32_t)), "hipMalloc sticky");
     chk(hipMalloc(&c->counts, (uint64_t)cfg.max_segs * sizeof(SegCount)), "hipMalloc counts");
     if (rc == WSC_OK) chk(hipMemsetAsync(c->sticky, 0, sizeof(uint32_t), c->stream), "hipMemset sticky");
@@ -205,6 +252,9 @@ int wsc_create(int device, const wsc_config* cfg_in, wsc_ctx** out) {
     chk(hipMalloc(&c->u8items, (uint64_t)c->u8items_cap * sizeof(U8Item)), "hipMalloc u8items");
     chk(hipMalloc(&c->u8maps, (uint64_t)c->u8items_cap * sizeof(uint64_t)), "hipMalloc u8maps");
     chk(hipMalloc(&c->u8seg, (uint64_t)cfg.max_segs * sizeof(U8Seg)), "hipMalloc u8seg");
+    if (const char* e = std::getenv("WSC_STAGE_VARIANT"); e && *e) c->stage_variant = std::atoi(e);
+    if (const char* e = std::getenv("WSC_WALK_DELAY_US"); e && *e) c->walk_delay_us = std::atoi(e);
+    if (const char* e = std::getenv("WSC_UNMASK_BUF"); e && *e) c->unmask_buf = std::atoi(e);
     if (const char* e = std::getenv("WSC_U8_GRID"); e && *e) c->u8_grid = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("WSC_WALK_MODE"); e && *e) {   // pin a walk geometry (tests, A/B): 64, 256 or 3
         const int m = std::atoi(e);
@@ -235,7 +285,8 @@ int wsc_destroy(wsc_ctx* c) {
     if (!c) return WSC_OK;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    void* ptrs[] = {c->dbg, c->sticky, c->counts, c->lb_state, c->u8info, c->lb_agg, c->lb_incl, c->spans, c->tile, c->d_wire, c->d_arena,
+    (void)fin_wait(c);
+    void* ptrs[] = {c->fin_ctr, c->dbg, c->sticky, c->counts, c->lb_state, c->u8info, c->lb_agg, c->lb_incl, c->spans, c->tile, c->d_wire, c->d_arena,
                     c->d_seg_off, c->d_state_in, c->d_state_out, c->d_seg_out, c->d_frames,
                     c->d_frame_dst, c->d_summary, c->enc_lb_state, c->enc_lb_agg, c->enc_lb_incl, c->enc_tile,
                     c->d_enc_msgs, c->d_enc_src, c->d_enc_out, c->d_enc_off, c->u8items, c->u8maps, c->u8seg};
@@ -244,6 +295,7 @@ int wsc_destroy(wsc_ctx* c) {
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->ev_walked) (void)hipEventDestroy(c->ev_walked);
     if (c->ev_done) (void)hipEventDestroy(c->ev_done);
+    if (c->hflag) (void)hipHostFree(c->hflag);
     delete c;
     return WSC_OK;
 }
@@ -273,8 +325,10 @@ int wsc_host_free(void* p) {
 // The launch sequence.  `ev` (optional, 6 pairs) brackets each stage for wsc_profile.  With
 // sw != st (wsc_decode_split) the walk runs on sw and the UTF-8 check + unmask on st, joined by
 // the context's events; otherwise everything runs in order on st.
+// phase: 0 = the whole decode; 1 = only the walk (split: on sw, recording ev_walked); 2 = only the
+// UTF-8 check + unmask (split: on st, joined to the walk only if it has not completed yet).
 static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev, hipStream_t sw = nullptr,
-                  bool split = false) {
+                  bool split = false, int phase = 0) {
     const bool compact = (b->flags & WSC_F_COMPACT) != 0;
     const uint32_t n = b->n_segs;
     if (n == 0) return fail(WSC_E_INVAL, "n_segs == 0");
@@ -317,6 +371,7 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     wa.u8seg = c->u8seg;
     wa.u8_inline_max = c->u8_inline_max;
     wa.sticky = c->sticky;
+    wa.u8host = c->hflag;
 
     // walk geometry: the fused walk with blocks that fill the CUs once (64 lanes for up to 64
     // segments per CU, else 256), or -- for more segments than the chip holds lanes at once -- the
@@ -331,6 +386,14 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     // split: the walk reuses this context's scratch, so it waits for the context's previous unmask
     // (an event never recorded is a no-op wait)
     const hipStream_t ws = split ? sw : st;
+    if (phase != 2) {
+    if (const int r = fin_wait(c)) return r;
+    if (c->walk_delay_us) {   // A/B experiment: start the walk later than the unmask boundary
+        const auto t0 = std::chrono::steady_clock::now();
+        while (std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(c->walk_delay_us)) __builtin_ia32_pause();
+    }
+    __atomic_store_n(&c->hflag[0], 0u, __ATOMIC_RELEASE);
+    c->walk_waited = false;
     if (split) HIP_TRY(hipStreamWaitEvent(ws, c->ev_done, 0));
     // fused: 16 frame records per lane in LDS (segments with more frames re-walk their headers)
     if (mode == 3) {
@@ -349,27 +412,35 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
         else hipLaunchKernelGGL((k_walk_fused<false, 16, 256, 1>), wgrid, wblk, 0, ws, wa);
     }
     HIP_TRY(hipGetLastError());
-    if (split) {
-        HIP_TRY(hipEventRecord(c->ev_walked, ws));
-        HIP_TRY(hipStreamWaitEvent(st, c->ev_walked, 0));
-    }
+    if (split) HIP_TRY(hipEventRecord(c->ev_walked, ws));
+    }   // phase != 2
+    if (phase == 1) return WSC_OK;
+    // a stream wait is a barrier packet between this unmask and the previous one on st: skipped
+    // when the host already knows the walk has finished (the staged pipeline waits for it)
+    const bool walked = split && (c->walk_waited || hipEventQuery(c->ev_walked) == hipSuccess);
+    c->walk_waited = false;
+    if (split && !walked) HIP_TRY(hipStreamWaitEvent(st, c->ev_walked, 0));
     rec(1);
-    // deferred UTF-8 (large text): verdicts applied before the unmask; exits at once without text
-    U8Args ua{};
-    ua.wire = b->wire;
-    ua.n_bytes = b->n_bytes;
-    ua.seg_off = b->seg_off;
-    ua.items = c->u8items;
-    ua.count = c->lb_state + 2;
-    ua.maps = c->u8maps;
-    ua.seg = c->u8seg;
-    ua.frames = b->frames;
-    ua.spans = c->spans;
-    ua.seg_out = b->seg_out;
-    ua.state_out = b->state_out;
-    ua.summary = b->summary;
-    hipLaunchKernelGGL(k_u8_check, dim3(c->u8_grid ? c->u8_grid : (uint32_t)c->n_cu * 5), dim3(256), 0, st, ua);   // resident: 5 waves/SIMD (96 VGPRs)
-    HIP_TRY(hipGetLastError());
+    // deferred UTF-8 (large text): verdicts applied before the unmask.  The kernel exits at once
+    // without deferred text, but it is still a launch between two unmasks: skipped when the walk
+    // has completed and its host-visible flag says it deferred nothing.
+    if (!(walked && __atomic_load_n(&c->hflag[0], __ATOMIC_ACQUIRE) == 0)) {
+        U8Args ua{};
+        ua.wire = b->wire;
+        ua.n_bytes = b->n_bytes;
+        ua.seg_off = b->seg_off;
+        ua.items = c->u8items;
+        ua.count = c->lb_state + 2;
+        ua.maps = c->u8maps;
+        ua.seg = c->u8seg;
+        ua.frames = b->frames;
+        ua.spans = c->spans;
+        ua.seg_out = b->seg_out;
+        ua.state_out = b->state_out;
+        ua.summary = b->summary;
+        hipLaunchKernelGGL(k_u8_check, dim3(c->u8_grid ? c->u8_grid : (uint32_t)c->n_cu * 5), dim3(256), 0, st, ua);   // resident: 5 waves/SIMD (96 VGPRs)
+        HIP_TRY(hipGetLastError());
+    }
     rec(2);
     rec(3);
 
@@ -382,7 +453,7 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     if (waves == 0) waves = 1;
     const dim3 ublk(256), ugrid((uint32_t)((waves + 3) / 4));
     using UK = void (*)(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*,
-                        const wsc_summary*, uint32_t*, uint32_t);
+                        const wsc_summary*, uint32_t*, uint32_t, uint32_t*, uint32_t*, uint32_t);
     // [compact][pieces 4/8][nt 0..3]
     static const UK table[2][2][4] = {
         {{k_unmask<false, 4, 0, 1>, k_unmask<false, 4, 1, 1>, k_unmask<false, 4, 2, 1>, k_unmask<false, 4, 3, 1>},
@@ -390,15 +461,26 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
         {{k_unmask<true, 4, 0, 1>, k_unmask<true, 4, 1, 1>, k_unmask<true, 4, 2, 1>, k_unmask<true, 4, 3, 1>},
          {k_unmask<true, 8, 0, 1>, k_unmask<true, 8, 1, 1>, k_unmask<true, 8, 2, 1>, k_unmask<true, 8, 3, 1>}}};
     const int pi = c->pieces == 4 ? 0 : 1;
+    static const UK table_buf[2][3] = {
+        {k_unmask<false, 4, 35, 1>, k_unmask<false, 4, 291, 1>, k_unmask<false, 4, 307, 1>},
+        {k_unmask<false, 8, 35, 1>, k_unmask<false, 8, 291, 1>, k_unmask<false, 8, 307, 1>}};
     UK kern = table[compact ? 1 : 0][pi][compact ? (c->cfg.unmask_nt >> 2) & 3 : c->cfg.unmask_nt & 3];
+    if (!compact && (c->cfg.unmask_nt & 3) == 3 && c->unmask_buf > 0 && c->unmask_buf <= 3)
+        kern = table_buf[pi][c->unmask_buf - 1];
+    const bool signal = phase == 2;   // staged: the last workgroup signals the host, no ev_done
     hipLaunchKernelGGL(kern, ugrid, ublk, 0, st, udst, (const uint8_t*)b->wire, b->n_bytes, b->n_bytes,
                        (const Span*)c->spans, (const uint32_t*)c->tile, (const wsc_summary*)b->summary,
-                       c->lb_state, mode == 3 ? 1u : wgrid.x + 1);   // re-arms ticket, timeout, item count, flags
+                       c->lb_state, mode == 3 ? 1u : wgrid.x + 1,   // re-arms ticket, timeout, item count, flags
+                       signal ? c->fin_ctr : nullptr, signal ? c->hflag + 1 : nullptr, c->fin_seq + 1);
     HIP_TRY(hipGetLastError());
     rec(4);
-
-    HIP_TRY(hipGetLastError());
-    if (split) HIP_TRY(hipEventRecord(c->ev_done, st));
+    if (signal) {
+        ++c->fin_seq;
+        c->fin_pending = true;
+        c->fin_stream = st;
+    } else if (split) {
+        HIP_TRY(hipEventRecord(c->ev_done, st));
+    }
     rec(5);
     return WSC_OK;
 }
@@ -415,6 +497,32 @@ int wsc_decode_split(wsc_ctx* c, const wsc_batch* b, void* walk_stream, void* un
     if (walk_stream == unmask_stream) return fail(WSC_E_INVAL, "walk_stream == unmask_stream: use wsc_decode");
     HIP_TRY(hipSetDevice(c->device));
     return launch(c, b, static_cast<hipStream_t>(unmask_stream), nullptr, static_cast<hipStream_t>(walk_stream), true);
+}
+
+int wsc_decode_walk(wsc_ctx* c, const wsc_batch* b, void* walk_stream) {
+    if (!c || !b) return fail(WSC_E_INVAL, "NULL argument");
+    HIP_TRY(hipSetDevice(c->device));
+    return launch(c, b, nullptr, nullptr, static_cast<hipStream_t>(walk_stream), true, 1);
+}
+
+int wsc_decode_finish(wsc_ctx* c, const wsc_batch* b, void* unmask_stream) {
+    if (!c || !b) return fail(WSC_E_INVAL, "NULL argument");
+    HIP_TRY(hipSetDevice(c->device));
+    return launch(c, b, static_cast<hipStream_t>(unmask_stream), nullptr, nullptr, true, 2);
+}
+
+int wsc_walk_wait(wsc_ctx* c) {
+    if (!c) return fail(WSC_E_INVAL, "NULL ctx");
+    HIP_TRY(hipSetDevice(c->device));
+    if (c->stage_variant & 1) {
+        hipError_t q;
+        while ((q = hipEventQuery(c->ev_walked)) == hipErrorNotReady) __builtin_ia32_pause();
+        HIP_TRY(q);
+    } else {
+        HIP_TRY(hipEventSynchronize(c->ev_walked));
+    }
+    c->walk_waited = true;
+    return WSC_OK;
 }
 
 int wsc_stream_create(wsc_ctx* c, const uint32_t* cu_mask, uint32_t mask_words, void** out) {

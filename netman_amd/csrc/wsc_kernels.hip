@@ -429,6 +429,10 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
                     const uint8_t s_in = (part || chain) ? (u8_pending ? 0xFF : (uint8_t)u8dfa) : 0;
                     const uint32_t pieces = n ? (uint32_t)((n + U8_PIECE - 1) / U8_PIECE) : 1u;
                     const uint32_t b0 = __hip_atomic_fetch_add(a.u8count, pieces, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (b0 == 0 && a.u8host) {   // the first deferral tells the host the check has work
+                        __hip_atomic_store(a.u8host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        __threadfence_system();
+                    }
                     for (uint32_t p = 0; p < pieces; ++p) {   // capacity covers every frame + bytes / U8_PIECE
                         const uint32_t idx = b0 + p;
                         U8Item it;

@@ -97,6 +97,7 @@ struct WalkArgs {
     U8Seg* u8seg;
     uint32_t u8_inline_max;      // text payloads up to this many bytes are validated in the walk
     uint32_t* sticky;            // context error bits, never re-armed by a kernel (wsc_error_flags)
+    uint32_t* u8host;            // host-visible word set when any UTF-8 item is deferred (cleared by the host)
 };
 
 struct U8Args {

@@ -241,8 +241,14 @@ __device__ __forceinline__ bool unmask_window_lanes(uint8_t* __restrict__ dst, c
                 }
             }
         }
+        if constexpr (NT >= 16) {
+            const __amdgpu_buffer_rsrc_t rs = win_rsrc(dst + wbase, 1024u * P);
 #pragma unroll
-        for (int k = 0; k < P; ++k) st16v<NT>(dst + wbase + k * 1024u + lane * 16u, acc[k]);
+            for (int k = 0; k < P; ++k) st16b<(NT >> 4)>(rs, k * 1024u + lane * 16u, acc[k]);
+        } else {
+#pragma unroll
+            for (int k = 0; k < P; ++k) st16v<NT>(dst + wbase + k * 1024u + lane * 16u, acc[k]);
+        }
         return true;
     }
     if (__ballot(more)) {
@@ -274,14 +280,15 @@ __device__ __forceinline__ bool unmask_window_lanes(uint8_t* __restrict__ dst, c
 // NT bit 0: non-temporal loads, bit 1: non-temporal stores.  In place `src` is unused (dst is
 // both source and destination) so the two restrict pointers never alias in an access; COMPACT
 // reads `src` (the wire) and writes `dst` (the arena).  `total` = wire bytes.
-template <bool COMPACT, int P, int NT, int MINW = 1>
-__global__ __launch_bounds__(256, MINW) void k_unmask(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src,
-                                                uint64_t src_bytes, uint64_t total,
-                                                const Span* __restrict__ spans,
-                                                const uint32_t* __restrict__ tile_first,
-                                                const wsc_summary* __restrict__ summary,
-                                                uint32_t* __restrict__ lb_state, uint32_t n_walk_blocks) {
+template <bool COMPACT, int P, int NT>
+__device__ __forceinline__ void unmask_all(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src,
+                                           uint64_t src_bytes, uint64_t total,
+                                           const Span* __restrict__ spans,
+                                           const uint32_t* __restrict__ tile_first,
+                                           const wsc_summary* __restrict__ summary,
+                                           uint32_t* __restrict__ lb_state, uint32_t n_walk_blocks) {
     constexpr uint32_t WB = 1024u * P;
+    static_assert(NT < 16 || !COMPACT, "buffer-instruction windows are the in-place path");
     // re-arm the walk's look-back state for the next decode (this launch is ordered after it):
     // lb_state[0] = ticket, [1] = timeout flag, [2 ...] = per-block flags
     for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n_walk_blocks + 2; t += gridDim.x * blockDim.x)
@@ -305,8 +312,15 @@ __global__ __launch_bounds__(256, MINW) void k_unmask(uint8_t* __restrict__ dst,
         }
         u32x4 v[P];
         // the loads do not depend on the span lookup: issue them first
+        [[maybe_unused]] __amdgpu_buffer_rsrc_t rs;
+        if constexpr (NT >= 16) {
+            rs = win_rsrc(dst + wbase, WB);
 #pragma unroll
-        for (int k = 0; k < P; ++k) v[k] = ld16v<NT>(rd + wbase + k * 1024u + lofs);
+            for (int k = 0; k < P; ++k) v[k] = ld16b<(NT & 1) ? 2 : 0>(rs, k * 1024u + lofs);
+        } else {
+#pragma unroll
+            for (int k = 0; k < P; ++k) v[k] = ld16v<NT>(rd + wbase + k * 1024u + lofs);
+        }
         // the fast-path test uses scalar loads (lgkmcnt), so it never waits behind the data loads
         const uint32_t r = tile_first[win];
         Span s0 = spans[r < n_spans ? r : n_spans - 1];
@@ -317,6 +331,9 @@ __global__ __launch_bounds__(256, MINW) void k_unmask(uint8_t* __restrict__ dst,
                 uint8_t* d = dst + (s0.dst - s0.src) + wbase + lofs;
 #pragma unroll
                 for (int k = 0; k < P; ++k) st16u<NT>(d + k * 1024u, v[k] ^ s0.key);
+            } else if constexpr (NT >= 16) {
+#pragma unroll
+                for (int k = 0; k < P; ++k) st16b<(NT >> 4)>(rs, k * 1024u + lofs, v[k] ^ s0.key);
             } else {
 #pragma unroll
                 for (int k = 0; k < P; ++k) st16v<NT>(dst + wbase + k * 1024u + lofs, v[k] ^ s0.key);
@@ -329,6 +346,44 @@ __global__ __launch_bounds__(256, MINW) void k_unmask(uint8_t* __restrict__ dst,
         const bool valid = load_span_lane(spans, n_spans, r, lane, sp);
         if (!unmask_window_lanes<COMPACT, P, NT>(dst, sp, valid, n_spans, r, wbase, lane, v))
             unmask_window_general<COMPACT, P, NT>(dst, src, src_bytes, total, spans, n_spans, r, wbase, lofs);
+    }
+}
+
+// fin_host (staged pipeline): the last workgroup to finish writes fin_seq to the host-visible
+// word, after every workgroup has done all its reads of the walk's spans / window index -- the
+// host then lets the next walk reuse them (wsc_api.cpp fin_wait).  A grid is up to 2^16+
+// workgroups: one device-scope counter would serialise them (measured 5.9 ms for 64 Ki), so the
+// count is two-level -- FIN_GROUPS counters a cache line apart, each finished by its last
+// workgroup, which bumps the top counter.  The workgroups that re-armed lb_state release it
+// before counting (the next walk may run while this grid's tail drains).  Every level re-arms
+// itself for the next launch.  Vector atomics and stores only.
+constexpr uint32_t FIN_GROUPS = 256, FIN_STRIDE = 32;   // fin_ctr: (FIN_GROUPS + 1) * FIN_STRIDE words
+template <bool COMPACT, int P, int NT, int MINW = 1>
+__global__ __launch_bounds__(256, MINW) void k_unmask(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src,
+                                                uint64_t src_bytes, uint64_t total,
+                                                const Span* __restrict__ spans,
+                                                const uint32_t* __restrict__ tile_first,
+                                                const wsc_summary* __restrict__ summary,
+                                                uint32_t* __restrict__ lb_state, uint32_t n_walk_blocks,
+                                                uint32_t* fin_ctr, uint32_t* fin_host, uint32_t fin_seq) {
+    unmask_all<COMPACT, P, NT>(dst, src, src_bytes, total, spans, tile_first, summary, lb_state, n_walk_blocks);
+    if (fin_host == nullptr) return;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (blockIdx.x * blockDim.x < n_walk_blocks + 2) __threadfence();   // lb_state re-arm visible first
+        const uint32_t g = blockIdx.x % FIN_GROUPS;
+        const uint32_t in_g = (gridDim.x - g + FIN_GROUPS - 1) / FIN_GROUPS;   // workgroups of group g
+        uint32_t* cg = fin_ctr + (1 + g) * FIN_STRIDE;
+        if (__hip_atomic_fetch_add(cg, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == in_g - 1) {
+            __hip_atomic_store(cg, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t groups = gridDim.x < FIN_GROUPS ? gridDim.x : FIN_GROUPS;
+            if (__hip_atomic_fetch_add(fin_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == groups - 1) {
+                __hip_atomic_store(fin_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __threadfence_system();
+                __hip_atomic_store(fin_host, fin_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __threadfence_system();
+            }
+        }
     }
 }
 

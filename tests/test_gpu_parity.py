@@ -438,14 +438,18 @@ def test_session_undrained_events_survive_next_decode(codec_lib):
 
 
 # ---- split pipeline (wsc_decode_split): walk on a CU-masked stream, unmask on others ----------
-@pytest.mark.parametrize("compact,layout,inline_max", [(False, "bench", 256), (True, "bench", 256), (False, "rest2", 256),
-                                                     (True, "rest2", 256), (False, "bench", 0), (True, "rest2", 0)])
-def test_decode_split_pipeline_matches_oracle(codec_lib, compact, layout, inline_max):
+@pytest.mark.parametrize("compact,layout,inline_max,staged", [
+    (False, "bench", 256, False), (True, "bench", 256, False), (False, "rest2", 256, False),
+    (True, "rest2", 256, False), (False, "bench", 0, False), (True, "rest2", 0, False),
+    (False, "bench", 256, True), (True, "bench", 0, True), (False, "rest2", 0, True), (True, "bench", 256, True)])
+def test_decode_split_pipeline_matches_oracle(codec_lib, compact, layout, inline_max, staged):
     """two contexts in flight, walk stream on 16 CUs; the unmasks on one stream over every CU (the
     bench's pipeline) or on one stream per context over the other CUs; every round re-arms the
     wires and decodes both batches back to back, so one batch's walk runs beside the other's
     unmask; each is compared with the oracle.  inline_max 0 sends every text check to the
-    chip-wide UTF-8 kernel (which runs on the unmask stream)"""
+    chip-wide UTF-8 kernel (which runs on the unmask stream).  staged: wsc_decode_walk, the host
+    waits for the walk, wsc_decode_finish (the check is skipped when nothing was deferred, the
+    unmask signals the host instead of recording an event)"""
     import os
     torch = pytest.importorskip("torch")
     dev = torch.device("cuda:0")
@@ -490,7 +494,12 @@ def test_decode_split_pipeline_matches_oracle(codec_lib, compact, layout, inline
                 t["wire"].copy_(torch.from_numpy(wire))
             torch.cuda.synchronize()
             for j in range(2):
-                ctxs[j].decode_split(bats[j], ws, us[j % len(us)])
+                if staged:
+                    ctxs[j].decode_walk(bats[j], ws)
+                    ctxs[j].walk_wait()
+                    ctxs[j].decode_finish(bats[j], us[j % len(us)])
+                else:
+                    ctxs[j].decode_split(bats[j], ws, us[j % len(us)])
             torch.cuda.synchronize()
             for j, (wire, off, streams) in enumerate(packed):
                 t = ts[j]
@@ -510,6 +519,67 @@ def test_decode_split_pipeline_matches_oracle(codec_lib, compact, layout, inline
     finally:
         torch.cuda.synchronize()
         for s in [ws] + us:
+            ctxs[0].stream_destroy(s)
+        for c in ctxs:
+            c.close()
+
+
+@pytest.mark.parametrize("inline_max", [256, 0])
+def test_staged_pipeline_back_to_back(codec_lib, monkeypatch, inline_max):
+    """COMPACT (the wire is only read), two contexts, eight staged decodes per context with no
+    host synchronisation between them: each context's next walk must wait (on the host, for the
+    unmask's pinned done word) until its previous unmask has read the spans and window index it
+    overwrites.  A race would corrupt the arena; the last decode of each is checked with the oracle."""
+    monkeypatch.setenv("WSC_U8_INLINE_MAX", str(inline_max))
+    torch = pytest.importorskip("torch")
+    dev = torch.device("cuda:0")
+    ctxs, bats, ts, packed = [], [], [], []
+    for j in range(2):
+        streams = [random_stream(9100 + 500 * j + i, n_units=12) for i in range(400)]
+        wire, off = pack_streams(streams)
+        c = K.Codec(0, max_batch_bytes=len(wire) + 4096, max_segs=len(streams), max_frames=1 << 15)
+        n = len(streams)
+        t = dict(wire=torch.from_numpy(wire.copy()).to(dev), seg_off=torch.from_numpy(off.view(np.int64)).to(dev),
+                 st_out=torch.zeros(n * 16, dtype=torch.uint8, device=dev),
+                 seg_out=torch.zeros(n * 32, dtype=torch.uint8, device=dev),
+                 frames=torch.zeros((1 << 15) * 32, dtype=torch.uint8, device=dev),
+                 summ=torch.zeros(32, dtype=torch.uint8, device=dev),
+                 arena=torch.zeros(len(wire) + 64, dtype=torch.uint8, device=dev),
+                 frame_dst=torch.zeros(1 << 15, dtype=torch.int64, device=dev))
+        ctxs.append(c)
+        ts.append(t)
+        packed.append((wire, off, streams))
+        bats.append(c.make_batch(t["wire"], t["seg_off"], None, t["st_out"], t["seg_out"], t["frames"], t["summ"],
+                                 compact=True, arena=t["arena"], frame_dst=t["frame_dst"]))
+    torch.cuda.synchronize()
+    n_cu = torch.cuda.get_device_properties(0).multi_processor_count
+    ws = ctxs[0].stream_create(K.cu_mask(range(16), n_cu))
+    us = ctxs[0].stream_create(None)
+    try:
+        for i in range(16):
+            j = i % 2
+            ctxs[j].decode_walk(bats[j], ws)
+            ctxs[j].walk_wait()
+            ctxs[j].decode_finish(bats[j], us)
+        torch.cuda.synchronize()
+        for j, (wire, off, streams) in enumerate(packed):
+            t = ts[j]
+            summ = t["summ"].cpu().numpy().copy().view(K.SUMMARY_DTYPE)[0]
+            nf = int(summ["n_frames"])
+            res = K.DecodeResult(
+                seg=t["seg_out"].cpu().numpy().copy().view(K.SEG_RESULT_DTYPE),
+                state=t["st_out"].cpu().numpy().copy().view(K.CONN_STATE_DTYPE),
+                frames=t["frames"].cpu().numpy().copy().view(K.FRAME_DTYPE)[:nf], summary=summ,
+                frame_dst=t["frame_dst"].cpu().numpy().copy().view(np.uint64)[:nf],
+                arena=t["arena"].cpu().numpy().copy())
+            after = t["wire"].cpu().numpy().copy()
+            assert np.array_equal(after, wire)
+            for i, s in enumerate(streams):
+                compare_segment(i, s, int(off[i]), res, O.run(s), wire_after=after, compact=True)
+            assert ctxs[j].error_flags() == 0
+    finally:
+        torch.cuda.synchronize()
+        for s in (ws, us):
             ctxs[0].stream_destroy(s)
         for c in ctxs:
             c.close()

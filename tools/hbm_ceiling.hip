@@ -40,6 +40,30 @@ __global__ __launch_bounds__(256) void xor_inplace(uint8_t* __restrict__ buf, ui
     }
 }
 
+// cache-policy sweep: the same in-place XOR through buffer instructions with explicit policy bits
+// (gfx940+ aux: bit 0 = sc0, bit 1 = nt, bit 4 = sc1); XCD: remap workgroups so each XCD (the
+// dispatcher deals workgroups round-robin over 8) walks one contiguous eighth of the buffer
+template <int P, int LA, int SA, bool XCD>
+__global__ __launch_bounds__(256) void xor_policy(uint8_t* __restrict__ buf, uint64_t n_win, uint32_t key) {
+    uint64_t b = blockIdx.x;
+    if (XCD) {
+        const uint64_t per = gridDim.x / 8;   // grid is a multiple of 8 here
+        b = (b % 8) * per + b / 8;
+    }
+    const uint64_t w = b * 4 + (threadIdx.x >> 6);
+    if (w >= n_win) return;
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(buf + w * (1024u * P), 0, 1024u * P, 0x00020000);
+    const uint32_t lo = (threadIdx.x & 63) * 16u;
+    u32x4 v[P];
+#pragma unroll
+    for (int k = 0; k < P; ++k) v[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, lo + k * 1024u, 0, LA));
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+        v[k] ^= key;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v[k]), r, lo + k * 1024u, 0, SA);
+    }
+}
+
 __global__ __launch_bounds__(256) void copy16(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, uint64_t n16) {
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (i < n16) reinterpret_cast<float4*>(dst)[i] = reinterpret_cast<const float4*>(src)[i];
@@ -103,6 +127,24 @@ int main(int argc, char** argv) {
     CK(hipMemset(dst, 0, n));
     printf("buffer %llu bytes\n", (unsigned long long)n);
     const double rw = 2.0 * (double)n;
+    if (argc > 2) {   // policy sweep only
+        const uint64_t nw = n / 4096;
+        const dim3 g((uint32_t)(((nw + 3) / 4 + 7) / 8 * 8));
+#define POL(LA, SA, X)                                                                          \
+        timeit("pol L" #LA " S" #SA " x" #X, rw, [&] {                                            \
+            hipLaunchKernelGGL((xor_policy<4, LA, SA, X>), g, dim3(256), 0, 0, buf, nw, 0x12345678u); \
+        });
+        timeit("xor_inplace<4>", rw, [&] {
+            hipLaunchKernelGGL(xor_inplace<4>, dim3((uint32_t)((nw + 3) / 4)), dim3(256), 0, 0, buf, nw, 0x12345678u);
+        });
+        POL(2, 2, false) POL(0, 2, false) POL(2, 0, false) POL(0, 0, false)
+        POL(3, 3, false) POL(2, 3, false) POL(2, 19, false) POL(19, 2, false) POL(19, 19, false) POL(2, 18, false)
+        POL(2, 16, false) POL(2, 1, false) POL(2, 2, true) POL(0, 0, true)
+        timeit("xor_inplace<4>", rw, [&] {
+            hipLaunchKernelGGL(xor_inplace<4>, dim3((uint32_t)((nw + 3) / 4)), dim3(256), 0, 0, buf, nw, 0x12345678u);
+        });
+        return 0;
+    }
     timeit("xor_inplace<4>", rw, [&] {
         const uint64_t nw = n / 4096;
         hipLaunchKernelGGL(xor_inplace<4>, dim3((uint32_t)((nw + 3) / 4)), dim3(256), 0, 0, buf, nw, 0x12345678u);
