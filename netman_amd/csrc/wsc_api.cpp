@@ -61,11 +61,9 @@ struct wsc_ctx {
     bool fin_pending = false;         // a staged unmask was enqueued without ev_done
     hipStream_t fin_stream = nullptr; // ... on this stream
     bool walk_waited = false;         // wsc_walk_wait saw the last walk complete
-    int walk_delay_us = 0;            // WSC_WALK_DELAY_US (A/B experiment)
     int unmask_buf = 3;               // WSC_UNMASK_BUF: in-place windows through buffer ops (1 nt, 2 nt sc1, 3 sc0 nt sc1
                                       // stores; 0 = 64-bit global addresses).  3: headline 2,890-2,898 -> 2,911-2,918
                                       // GiB/s (A/B on one box, profiles/r02_unmask_policy.log)
-    int stage_variant = 0;            // WSC_STAGE_VARIANT (A/B): bit 0 = wsc_walk_wait polls hipEventQuery
     wsc_config cfg{};
     uint32_t pieces = 8;          // 16 B pieces per lane -> window = pieces KiB
     uint32_t* sticky = nullptr;      // error bits of every decode/encode (wsc_error_flags), never re-armed
@@ -252,8 +250,6 @@ int wsc_create(int device, const wsc_config* cfg_in, wsc_ctx** out) {
     chk(hipMalloc(&c->u8items, (uint64_t)c->u8items_cap * sizeof(U8Item)), "hipMalloc u8items");
     chk(hipMalloc(&c->u8maps, (uint64_t)c->u8items_cap * sizeof(uint64_t)), "hipMalloc u8maps");
     chk(hipMalloc(&c->u8seg, (uint64_t)cfg.max_segs * sizeof(U8Seg)), "hipMalloc u8seg");
-    if (const char* e = std::getenv("WSC_STAGE_VARIANT"); e && *e) c->stage_variant = std::atoi(e);
-    if (const char* e = std::getenv("WSC_WALK_DELAY_US"); e && *e) c->walk_delay_us = std::atoi(e);
     if (const char* e = std::getenv("WSC_UNMASK_BUF"); e && *e) c->unmask_buf = std::atoi(e);
     if (const char* e = std::getenv("WSC_U8_GRID"); e && *e) c->u8_grid = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("WSC_WALK_MODE"); e && *e) {   // pin a walk geometry (tests, A/B): 64, 256 or 3
@@ -388,10 +384,6 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     const hipStream_t ws = split ? sw : st;
     if (phase != 2) {
     if (const int r = fin_wait(c)) return r;
-    if (c->walk_delay_us) {   // A/B experiment: start the walk later than the unmask boundary
-        const auto t0 = std::chrono::steady_clock::now();
-        while (std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(c->walk_delay_us)) __builtin_ia32_pause();
-    }
     __atomic_store_n(&c->hflag[0], 0u, __ATOMIC_RELEASE);
     c->walk_waited = false;
     if (split) HIP_TRY(hipStreamWaitEvent(ws, c->ev_done, 0));
@@ -514,13 +506,7 @@ int wsc_decode_finish(wsc_ctx* c, const wsc_batch* b, void* unmask_stream) {
 int wsc_walk_wait(wsc_ctx* c) {
     if (!c) return fail(WSC_E_INVAL, "NULL ctx");
     HIP_TRY(hipSetDevice(c->device));
-    if (c->stage_variant & 1) {
-        hipError_t q;
-        while ((q = hipEventQuery(c->ev_walked)) == hipErrorNotReady) __builtin_ia32_pause();
-        HIP_TRY(q);
-    } else {
-        HIP_TRY(hipEventSynchronize(c->ev_walked));
-    }
+    HIP_TRY(hipEventSynchronize(c->ev_walked));
     c->walk_waited = true;
     return WSC_OK;
 }
