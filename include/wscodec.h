@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define WSC_ABI_VERSION 1
+#define WSC_ABI_VERSION 2   /* 2: wsc_frame.payload_len_hi (40-bit payload lengths), staged split */
 
 /* ---- return codes --------------------------------------------------------------------------- */
 #define WSC_OK 0
@@ -97,7 +97,7 @@ typedef struct wsc_conn_state {
 /* One record per frame whose header was parsed and acted on, in stream order.                  */
 typedef struct wsc_frame {
     uint64_t hdr_off;      /* batch offset of the frame's first header byte                      */
-    uint32_t payload_len;  /* fragmentLength                                                     */
+    uint32_t payload_len;  /* fragmentLength, low 32 bits (the reference parses 64: websocket.go:291-299) */
     uint32_t mask;         /* the 4 mask bytes, wire byte 0 in bits 0..7                         */
     uint32_t seg;          /* segment (connection slot) index                                    */
     uint32_t msg_id;       /* msgID before this frame (Message.MsgID for WSC_FK_MESSAGE)         */
@@ -108,7 +108,7 @@ typedef struct wsc_frame {
     uint8_t err;           /* WSC_ERR_* for WSC_FK_ERROR                                         */
     uint8_t hdr_len;       /* 6 / 8 / 14 for complete masked headers; payload_off = hdr_off+hdr_len */
     uint8_t flags;         /* WSC_FF_*                                                           */
-    uint8_t pad;
+    uint8_t payload_len_hi; /* fragmentLength bits 32..39: length = payload_len | hi << 32         */
 } wsc_frame;               /* 32 B */
 
 /* Per-segment result.                                                                          */
@@ -157,7 +157,7 @@ typedef struct wsc_config {
     uint64_t max_batch_bytes;  /* largest n_bytes a batch may have                               */
     uint32_t max_segs;         /* largest n_segs                                                 */
     uint32_t max_frames;       /* largest number of frames in one batch                          */
-    uint64_t max_frame_len;    /* payloads above this -> WSC_ERR_TOO_LARGE (<= 0xFFFFFFFF)       */
+    uint64_t max_frame_len;    /* payloads above this -> WSC_ERR_TOO_LARGE (<= 2^40 - 1)         */
     uint32_t unmask_window;    /* bytes per wave-window in the unmask kernel: 4096 / 8192 (0 = 4096) */
     uint32_t unmask_waves_per_cu; /* unmask grid sizing (0 = default)                            */
     uint32_t unmask_nt;        /* in place: bit0 non-temporal payload loads, bit1 non-temporal    */

@@ -45,12 +45,17 @@ CONN_STATE_DTYPE = np.dtype([("cont_len", "<u8"), ("msg_id", "<u4"), ("message_m
 FRAME_DTYPE = np.dtype([("hdr_off", "<u8"), ("payload_len", "<u4"), ("mask", "<u4"), ("seg", "<u4"),
                         ("msg_id", "<u4"), ("opcode", "u1"), ("fin", "u1"), ("kind", "u1"),
                         ("mode", "u1"), ("err", "u1"), ("hdr_len", "u1"), ("flags", "u1"),
-                        ("pad", "u1")])
+                        ("payload_len_hi", "u1")])
 SEG_RESULT_DTYPE = np.dtype([("consumed", "<u8"), ("frame_begin", "<u4"), ("frame_count", "<u4"),
                              ("status", "<u4"), ("close_code", "<u4"), ("err", "<u4"), ("pad", "<u4")])
 SUMMARY_DTYPE = np.dtype([("data_bytes", "<u8"), ("ctrl_bytes", "<u8"), ("n_frames", "<u4"),
                           ("n_spans", "<u4"), ("overflow", "<u4"), ("pad", "<u4")])
 assert CONN_STATE_DTYPE.itemsize == 16 and FRAME_DTYPE.itemsize == 32
+
+
+def frame_len(rec) -> int:
+    """a wsc_frame record's payload length (40 bits: payload_len | payload_len_hi << 32)"""
+    return int(rec["payload_len"]) | int(rec["payload_len_hi"]) << 32
 assert SEG_RESULT_DTYPE.itemsize == 32 and SUMMARY_DTYPE.itemsize == 32
 # wsc_out_msg: one outbound frame for wsc_encode (websocket_ctrl.go:23-70 encode(firstByte, bs))
 OUT_MSG_DTYPE = np.dtype([("src_off", "<u8"), ("len", "<u8"), ("first_byte", "u1"), ("pad", "u1", (7,))])
@@ -125,6 +130,7 @@ SIGNATURES = {
 }
 
 _lib = None
+ABI_VERSION = 2   # include/wscodec.h WSC_ABI_VERSION: the record layouts above
 
 
 def load_library(path: str = LIB_PATH):
@@ -147,6 +153,8 @@ def load_library(path: str = LIB_PATH):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if lib.wsc_abi_version() != ABI_VERSION:
+        raise OSError(f"{path}: ABI version {lib.wsc_abi_version()}, this module speaks {ABI_VERSION}: rebuild")
     _lib = lib
     return lib
 

@@ -195,7 +195,7 @@ int wsc_create(int device, const wsc_config* cfg_in, wsc_ctx** out) {
     if (cfg_in) cfg = *cfg_in; else wsc_config_default(&cfg);
     if (cfg.max_segs == 0 || cfg.max_frames == 0 || cfg.max_batch_bytes == 0)
         return fail(WSC_E_INVAL, "zero capacity in config");
-    if (cfg.max_frame_len > 0xFFFFFFFFull) return fail(WSC_E_INVAL, "max_frame_len > 2^32-1");
+    if (cfg.max_frame_len > 0xFFFFFFFFFFull) return fail(WSC_E_INVAL, "max_frame_len > 2^40-1");
     uint32_t win = cfg.unmask_window ? cfg.unmask_window : 4096;
     if (win != 4096 && win != 8192) return fail(WSC_E_INVAL, "unmask_window must be 4096 or 8192");
     cfg.unmask_window = win;

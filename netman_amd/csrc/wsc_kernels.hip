@@ -124,7 +124,7 @@ __device__ __forceinline__ EmitCtx emit_begin(const WalkArgs& a, uint32_t s, uin
 }
 
 template <bool COMPACT>
-__device__ __forceinline__ void emit_frame(const WalkArgs& a, EmitCtx& e, const wsc_frame& fr, uint32_t plen,
+__device__ __forceinline__ void emit_frame(const WalkArgs& a, EmitCtx& e, const wsc_frame& fr, uint64_t plen,
                                            bool have_span, uint32_t region) {
     const uint32_t fi = e.fbase + e.nf;
     if (fi < a.frames_cap) {
@@ -133,7 +133,8 @@ __device__ __forceinline__ void emit_frame(const WalkArgs& a, EmitCtx& e, const 
         const uint4 r1 = make_uint4(fr.seg, fr.msg_id,
                                     (uint32_t)fr.opcode | (uint32_t)fr.fin << 8 | (uint32_t)fr.kind << 16 |
                                         (uint32_t)fr.mode << 24,
-                                    (uint32_t)fr.err | (uint32_t)fr.hdr_len << 8 | (uint32_t)fr.flags << 16);
+                                    (uint32_t)fr.err | (uint32_t)fr.hdr_len << 8 | (uint32_t)fr.flags << 16 |
+                                        (uint32_t)fr.payload_len_hi << 24);
         reinterpret_cast<uint4*>(a.frames + fi)[0] = r0;
         reinterpret_cast<uint4*>(a.frames + fi)[1] = r1;
         if constexpr (COMPACT) {
@@ -143,28 +144,38 @@ __device__ __forceinline__ void emit_frame(const WalkArgs& a, EmitCtx& e, const 
         }
     }
     if (have_span) {
-        Span sp;
-        sp.src = fr.hdr_off + fr.hdr_len;
-        sp.len = plen;
-        if (COMPACT && region) sp.dst = e.abase + e.own_bytes0 + e.nb1;
-        else sp.dst = COMPACT ? e.abase + e.nb0 : sp.src;
-        const uint32_t idx = e.sbase + e.ns0 + e.ns1;   // stream order
+        // a payload of 4 GiB or more is cut into SPAN_CHUNK-byte spans (multiples of 4 bytes, so
+        // every piece keeps the frame's wire-phased key); span_chunks() counted them the same way
+        const uint32_t nch = span_chunks(plen);
+        const uint64_t src0 = fr.hdr_off + fr.hdr_len;
+        uint64_t dst0 = src0;
+        if (COMPACT && region) dst0 = e.abase + e.own_bytes0 + e.nb1;
+        else if (COMPACT) dst0 = e.abase + e.nb0;
         // the key is phased at the wire: every aligned wire dword XORs with one register
-        sp.key = rotr32(fr.mask, 8u * ((uint32_t)(0u - (uint32_t)sp.src) & 3u));
-        if (idx < a.spans_cap) a.spans[idx] = sp;
-        const uint64_t dend = sp.src + plen;
-        uint64_t& nx = e.nx0;
-        if (nx < dend) {   // windows [nx, dend) start inside this span: consecutive entries
-            uint64_t t = nx >> a.win_shift;
-            const uint64_t t_end = ((dend - 1) >> a.win_shift) + 1;
-            nx = t_end << a.win_shift;
-            for (; t < t_end && (t & 3); ++t) a.tile_first[t] = idx;
-            const uint4 q = make_uint4(idx, idx, idx, idx);
-            for (; t + 4 <= t_end; t += 4) *reinterpret_cast<uint4*>(a.tile_first + t) = q;
-            for (; t < t_end; ++t) a.tile_first[t] = idx;
+        const uint32_t key = rotr32(fr.mask, 8u * ((uint32_t)(0u - (uint32_t)src0) & 3u));
+        for (uint32_t c = 0; c < nch; ++c) {
+            const uint64_t off = (uint64_t)c * SPAN_CHUNK;
+            Span sp;
+            sp.src = src0 + off;
+            sp.dst = dst0 + off;
+            sp.len = (uint32_t)(c + 1 == nch ? plen - off : SPAN_CHUNK);
+            sp.key = key;
+            const uint32_t idx = e.sbase + e.ns0 + e.ns1 + c;   // stream order
+            if (idx < a.spans_cap) a.spans[idx] = sp;
+            const uint64_t dend = sp.src + sp.len;
+            uint64_t& nx = e.nx0;
+            if (nx < dend) {   // windows [nx, dend) start inside this span: consecutive entries
+                uint64_t t = nx >> a.win_shift;
+                const uint64_t t_end = ((dend - 1) >> a.win_shift) + 1;
+                nx = t_end << a.win_shift;
+                for (; t < t_end && (t & 3); ++t) a.tile_first[t] = idx;
+                const uint4 q = make_uint4(idx, idx, idx, idx);
+                for (; t + 4 <= t_end; t += 4) *reinterpret_cast<uint4*>(a.tile_first + t) = q;
+                for (; t < t_end; ++t) a.tile_first[t] = idx;
+            }
         }
-        if (COMPACT && region) { e.ns1 += 1; e.nb1 += plen; }
-        else { e.ns0 += 1; e.nb0 += plen; }
+        if (COMPACT && region) { e.ns1 += nch; e.nb1 += plen; }
+        else { e.ns0 += nch; e.nb0 += plen; }
     }
     e.nf += 1;
 }
@@ -174,6 +185,7 @@ struct WalkEnd {
     uint64_t pos, cont;
     uint64_t last_dend;      // wire end of the segment's last payload span (seg_start if none)
     uint32_t msg, mode, status, close_code, err, u8dfa;
+    bool replay;             // counting pass: the LDS records hold the whole segment
 };
 
 template <bool COMPACT>
@@ -284,6 +296,7 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
         wsc_frame fr;
         fr.hdr_off = pos;
         fr.payload_len = 0;
+        fr.payload_len_hi = 0;
         fr.mask = 0;
         fr.seg = s;
         fr.msg_id = msg;
@@ -294,7 +307,6 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
         fr.err = 0;
         fr.hdr_len = 2;
         fr.flags = 0;
-        fr.pad = 0;
 
         uint64_t next = pos;
         bool have_span = false;
@@ -330,7 +342,12 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
                 else mask = h[10] | h[11] << 8 | h[12] << 16 | h[13] << 24;
                 fr.hdr_len = (uint8_t)hl;
                 fr.mask = mask;
-                fr.payload_len = (uint32_t)plen;
+                {   // 40-bit record length; longer is always TOO_LARGE (max_frame_len < 2^40): saturated
+                    const uint64_t rl = plen < (1ull << 40) ? plen : (1ull << 40) - 1;
+                    if (rl > 0xFFFFFFFFull) sflags |= SEGF_LONG;
+                    fr.payload_len = (uint32_t)rl;
+                    fr.payload_len_hi = (uint8_t)(rl >> 32);
+                }
                 const uint64_t pstart = pos + hl;
 
                 // opcode switch, websocket.go:136-208
@@ -475,15 +492,15 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
         if constexpr (COMPACT) if (region) fr.flags |= WSC_FF_CTRL_ARENA;
 
         if constexpr (EMIT) {
-            emit_frame<COMPACT>(a, e, fr, (uint32_t)plen, have_span, region);
+            emit_frame<COMPACT>(a, e, fr, plen, have_span, region);
         } else {
             record(fr, have_span, region,
                    fr.kind == WSC_FK_MESSAGE || fr.kind == WSC_FK_PING || fr.kind == WSC_FK_PONG, plen);
         }
         nf += 1;
         if (have_span) {
-            if (COMPACT && region) { ns1 += 1; nb1 += plen; }
-            else { ns0 += 1; nb0 += plen; }
+            if (COMPACT && region) { ns1 += 1; nb1 += plen; }   // control payloads: <= 125 B
+            else { ns0 += span_chunks(plen); nb0 += plen; }
         }
         pos = next;
         return status == WSC_SEG_OPEN;
@@ -518,6 +535,7 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
         wsc_frame fr;
         fr.hdr_off = pos;
         fr.payload_len = (uint32_t)plen;
+        fr.payload_len_hi = (uint8_t)(plen >> 32);
         fr.mask = mask;
         fr.seg = s;
         fr.msg_id = msg;
@@ -528,14 +546,13 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
         fr.err = 0;
         fr.hdr_len = (uint8_t)hl;
         fr.flags = WSC_FF_UNMASKED;
-        fr.pad = 0;
         const bool have_span = plen > 0;
-        if constexpr (EMIT) emit_frame<COMPACT>(a, e, fr, (uint32_t)plen, have_span, 0);
+        if constexpr (EMIT) emit_frame<COMPACT>(a, e, fr, plen, have_span, 0);
         else record(fr, have_span, 0, true, plen);
         msg += 1;
         mode = 0;
         nf += 1;
-        if (have_span) { ns0 += 1; nb0 += plen; }
+        if (have_span) { ns0 += span_chunks(plen); nb0 += plen; }
         pos += hl + plen;
         return true;
     };
@@ -571,10 +588,13 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
     }
 
     SegCount c;
+    bool replay = false;
     c.frames = nf; c.spans0 = ns0; c.spans1 = ns1; c.flags = sflags;
     c.bytes0 = nb0; c.bytes1 = nb1;
     if constexpr (!EMIT) {
-        if (nf > cap || !lrec) {   // only a re-walking emit pass reads them back
+        // the LDS records replay the segment only if all fit and every offset / length fits 32 bits
+        replay = lrec && nf <= cap && seg_end - seg_start <= 0xFFFFFFFFull && !(sflags & SEGF_LONG);
+        if (!replay) {   // only a re-walking emit pass reads them back
             a.u8info[2 * s] = u8fail;
             a.u8info[2 * s + 1] = u8dfa;
         }
@@ -592,6 +612,7 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
     we.pos = pos; we.cont = cont; we.msg = msg; we.mode = mode; we.status = status;
     we.close_code = close_code; we.err = err_out; we.u8dfa = u8dfa;
     we.last_dend = pend;
+    we.replay = replay;
     if (wend) *wend = we;
     if constexpr (EMIT) emit_end<COMPACT>(a, e, we);
     return c;
@@ -816,7 +837,7 @@ __global__ __launch_bounds__(NT) void k_walk_fused(WalkArgs a) {
         const SegCount c = walk_segment<false, COMPACT, NT>(a, s, zero, zero, sh_rec + nrec * NT + lane, &we,
                                                             sh_rec2 + nrec * NT + lane, cap, j);
         const uint64_t ss = a.seg_off[s];
-        const bool rep = c.frames <= cap && a.seg_off[s + 1] - ss <= 0xFFFFFFFFull;
+        const bool rep = we.replay;
         sh_r0[q] = (uint8_t)nrec;
         if (rep) nrec += c.frames;
         sh_rep[q] = rep ? 1 : 0;
@@ -1156,7 +1177,7 @@ __device__ __forceinline__ void u8_finish(const U8Args& a, uint32_t it, uint32_t
     wsc_frame* f = a.frames + g.fbase + fail;
     f->kind = WSC_FK_ERROR;
     f->err = WSC_ERR_MUST_UTF8;
-    const uint64_t fend = f->hdr_off + f->hdr_len + f->payload_len;
+    const uint64_t fend = f->hdr_off + f->hdr_len + (f->payload_len | (uint64_t)f->payload_len_hi << 32);
     wsc_seg_result r = a.seg_out[s];
     r.consumed = fend - a.seg_off[s];
     r.frame_count = fail + 1;

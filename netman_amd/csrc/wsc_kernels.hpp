@@ -30,7 +30,8 @@ struct SegCountAdd {
     }
 };
 
-enum : uint32_t { SEGF_UTF8 = 1u, SEGF_U8DEFER = 2u };
+// SEGF_LONG: a record's length needs more than 32 bits (the LDS replay keeps 32): emit by re-walking
+enum : uint32_t { SEGF_UTF8 = 1u, SEGF_U8DEFER = 2u, SEGF_LONG = 4u };
 
 // ---- chip-wide UTF-8 (k_u8_check) ------------------------------------------------------------
 // The walk validates text payloads of at most u8_inline_max bytes itself (serial DFA per lane);
@@ -58,6 +59,13 @@ struct U8Seg {          // per segment with deferred items (written by the walk)
 // One contiguous run of masked payload bytes to XOR: source in the wire, destination either the
 // same bytes (in place) or the arena (COMPACT).  `key` is the mask word rotated so that it XORs
 // 4-byte-aligned destination dwords directly: key = rotr(mask, 8 * ((-dst) & 3)).
+// spans carry u32 lengths: a payload of 4 GiB or more (64-bit length, websocket.go:291-299) is
+// cut into spans of SPAN_CHUNK bytes; everything shorter is one span
+constexpr uint64_t SPAN_CHUNK = 1ull << 31;
+__host__ __device__ __forceinline__ uint32_t span_chunks(uint64_t plen) {
+    return plen <= 0xFFFFFFFFull ? 1u : (uint32_t)((plen + SPAN_CHUNK - 1) >> 31);
+}
+
 struct Span {
     uint64_t src;
     uint64_t dst;

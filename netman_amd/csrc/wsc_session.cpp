@@ -241,20 +241,21 @@ void harvest(wsc_session* s, int set, Conn& c, uint32_t slot, const uint8_t* in_
     bool views = false;
     for (uint32_t i = r.frame_begin; i < r.frame_begin + r.frame_count; ++i) {
         const wsc_frame& f = frames[i];
+        const uint64_t flen = f.payload_len | (uint64_t)f.payload_len_hi << 32;   // 40-bit length
         const uint8_t* p = compact ? res_base + arena_base + frame_dst[i] : res_base + f.hdr_off + f.hdr_len;
         Event e;
         std::memset(&e.ev, 0, sizeof(e.ev));
         switch (f.kind) {
         case WSC_FK_FRAG:                                     // websocket_frame.go:95-98
-            c.cont.insert(c.cont.end(), p, p + f.payload_len);
+            c.cont.insert(c.cont.end(), p, p + flen);
             continue;
         case WSC_FK_MESSAGE:                                  // websocket_frame.go:62-91
             if (f.flags & WSC_FF_CONT_MSG) {
                 e.data.swap(c.cont);
-                e.data.insert(e.data.end(), p, p + f.payload_len);
+                e.data.insert(e.data.end(), p, p + flen);
             } else {
                 e.view = p;
-                e.view_len = f.payload_len;
+                e.view_len = flen;
                 e.set = set;
                 views = true;
             }
@@ -264,7 +265,7 @@ void harvest(wsc_session* s, int set, Conn& c, uint32_t slot, const uint8_t* in_
             break;
         case WSC_FK_PING:                                     // websocket_ctrl.go:128-153
             e.view = p;
-            e.view_len = f.payload_len;
+            e.view_len = flen;
             e.set = set;
             views = true;
             e.ev.type = WSC_EV_PONG;

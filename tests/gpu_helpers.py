@@ -31,7 +31,7 @@ def compare_segment(si, stream, seg_start, res: K.DecodeResult, ora: O.OracleOut
             assert int(d[f]) == int(o[f]), f + " " + ctx
         assert int(d["err"]) == int(o["err"]), "err " + ctx
         if int(d["kind"]) != K.FK_STALL and int(d["err"]) != K.ERR_RSV_FAIL:
-            assert int(d["payload_len"]) == int(o["payload_len"]), ctx
+            assert K.frame_len(d) == min(int(o["payload_len"]), (1 << 40) - 1), ctx   # 40-bit record, saturated
             assert int(d["mask"]) == int(o["mask"]), ctx
             assert int(d["hdr_off"]) + int(d["hdr_len"]) - seg_start == int(o["payload_off"]), ctx
     # terminal status
@@ -59,9 +59,9 @@ def compare_segment(si, stream, seg_start, res: K.DecodeResult, ora: O.OracleOut
     else:
         for i in range(fc):
             d = fr[i]
-            if int(d["flags"]) & K.FF_UNMASKED and int(d["payload_len"]):
+            if int(d["flags"]) & K.FF_UNMASKED and K.frame_len(d):
                 p = int(d["hdr_off"]) + int(d["hdr_len"]) - seg_start
-                L = int(d["payload_len"])
+                L = K.frame_len(d)
                 dst = int(res.frame_dst[fb + i])
                 assert np.array_equal(res.arena[dst:dst + L], ref[p:p + L]), f"seg {si} frame {i} arena"
 

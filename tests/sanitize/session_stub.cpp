@@ -104,6 +104,7 @@ static void walk(const wsc_ctx* c, uint8_t* w, uint64_t a, uint64_t b, uint32_t 
         for (uint64_t i = 0; i < plen; ++i) w[pos + hl + i] ^= m[i & 3];
         f.hdr_len = (uint8_t)hl;
         f.payload_len = (uint32_t)plen;
+        f.payload_len_hi = (uint8_t)(plen >> 32);
         std::memcpy(&f.mask, m, 4);
         f.flags = WSC_FF_UNMASKED;
         bool stop = false;
