@@ -405,12 +405,16 @@ def config3_dealt(a, torch, dist, K, synth, world, rank, dev, cdev):
             "n_gpus": world, "scaling": "weak", "parity_ok": ok}
 
 
-def other_configs(torch, K, synth):
-    """Device time of the full decode for the other single-GPU BASELINE.json configs (hipEvents,
-    median of 10), reported beside the headline; parity for each is in tests/test_gpu_parity.py.
-    `pipelined_gib_s`: two batches in flight through the split pipeline, as the headline runs
-    (walk on a stream masked to max(16, walk blocks) CUs, at most half the chip; unmask over all
-    CUs), wall time of 20 steps after 5 warm-up steps."""
+def other_configs(torch, K, synth, only=None):
+    """The other single-GPU BASELINE.json configs, beside the headline; parity for each is in
+    tests/test_gpu_parity.py.  `ms`: one batch in flight -- back-to-back decodes of one batch on
+    one stream (each walk waits for the previous unmask), wall time of 20 after 3 warm-up;
+    `walk_ms` / `unmask_ms`: per-kernel device time (wsc_profile hipEvents, median of 10);
+    `pipelined_*`: two batches in flight through the staged split pipeline the headline runs
+    (walk on a stream masked to max(16, walk blocks) CUs, at most half the chip, the host waits
+    for it, unmask over all CUs), wall time of 20 steps after 5 warm-up steps.  `frac`: the
+    decode's algorithmic bytes (2 x payload + header + 32 B record per frame) per second over
+    the 8 TB/s HBM peak."""
     dev = torch.device("cuda", torch.cuda.current_device())
     n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
     res = {}
@@ -426,6 +430,8 @@ def other_configs(torch, K, synth):
              ("TEXT 262144 x 1 KiB valid UTF-8, 16 frames/segment",
               lambda: synth.text_batch(262144, 1024, 16, seed=synth.SEED_BASE + 8), False)]
     for name, make, compact in cases:
+        if only and not any(o in name for o in only):
+            continue
         cfg = make()
         n = len(cfg["seg_off"]) - 1
 
@@ -444,35 +450,53 @@ def other_configs(torch, K, synth):
             return c, t, b
 
         c, t, b = one()
-        c.decode(b)
+        st = torch.cuda.Stream(device=dev)
+        for _ in range(3):
+            c.decode(b, st.cuda_stream)
         torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(20):
+            c.decode(b, st.cuda_stream)
+        torch.cuda.synchronize()
+        tot = (time.perf_counter() - t0) / 20 * 1e3
+        ok = c.error_flags() == 0
         p = [c.profile(b, 1) for _ in range(10)]
-        tot = float(np.median([q["total"] for q in p]))
         um = float(np.median([q["unmask"] for q in p]))
+        wk = float(np.median([q["walk"] for q in p]))
         hdr = np.where(cfg["plen"] <= 125, 6, np.where(cfg["plen"] <= 65535, 8, 14))
         alg = int((2 * cfg["plen"].astype(np.int64) + hdr + 32).sum())
-        # two batches in flight through the split pipeline
+        # two batches in flight through the staged split pipeline
         torch.cuda.synchronize()
         c2, t2, b2 = one()
         wcus = min(n_cu // 2, max(16, (n + 255) // 256))
         ws = c.stream_create(K.cu_mask(range(wcus), n_cu))
         us = c.stream_create(None)
         pair = [(c, b), (c2, b2)]
-        for i in range(5):
-            pair[i % 2][0].decode_split(pair[i % 2][1], ws, us)
+
+        def staged(k):
+            for i in range(k):
+                cx, bx = pair[i % 2]
+                cx.decode_walk(bx, ws)
+                cx.walk_wait()
+                cx.decode_finish(bx, us)
+
+        staged(5)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for i in range(20):
-            pair[i % 2][0].decode_split(pair[i % 2][1], ws, us)
+        staged(20)
         torch.cuda.synchronize()
         pms = (time.perf_counter() - t0) / 20 * 1e3
+        ok = ok and c.error_flags() == 0 and c2.error_flags() == 0
         c.stream_destroy(ws)
         c.stream_destroy(us)
         res[name] = {"gib_s": round(cfg["payload_bytes"] / (tot * 1e-3) / 2**30, 1), "ms": round(tot, 4),
-                     "unmask_ms": round(um, 4), "unmask_gb_s": round(alg / (um * 1e-3) / 1e9, 1),
+                     "frac": round(alg / (tot * 1e-3) / 1e9 / HBM_PEAK_GBS, 3),
+                     "walk_ms": round(wk, 4), "unmask_ms": round(um, 4), "unmask_gb_s": round(alg / (um * 1e-3) / 1e9, 1),
                      "pipelined_gib_s": round(cfg["payload_bytes"] / (pms * 1e-3) / 2**30, 1),
-                     "pipelined_ms_per_batch": round(pms, 4), "pipelined_walk_cus": wcus,
-                     "frames": int(cfg["n_frames"]), "payload_bytes": int(cfg["payload_bytes"])}
+                     "pipelined_ms_per_batch": round(pms, 4),
+                     "pipelined_frac": round(alg / (pms * 1e-3) / 1e9 / HBM_PEAK_GBS, 3), "pipelined_walk_cus": wcus,
+                     "frames": int(cfg["n_frames"]), "payload_bytes": int(cfg["payload_bytes"]), "alg_bytes": alg,
+                     "device_errors": not ok}
         c.close()
         c2.close()
         del t, t2

@@ -114,6 +114,26 @@ __device__ __forceinline__ u32x4 range_mask16(int32_t lo, int32_t hi) {
     return m;
 }
 
+// Byte masks from a 17-entry LDS table: pm[L] = the first L bytes of a 16-byte piece, so the
+// bytes [lo, hi) are pm[hi] & ~pm[lo] (one v_bfi per dword; empty when hi <= lo).  Replaces the
+// per-dword shift / compare chains of range_mask16 in the window paths that run per piece:
+// the lane-parallel window of small frames was VALU-bound (PMC: 725 VALU instructions per wave
+// window at 1 KiB frames, ~77 % of the chip's VALU cycles during the kernel).
+__device__ __forceinline__ u32x4 prefix_mask16(uint32_t L) {
+    u32x4 m;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t n = L > 4u * j ? (L - 4u * j > 4u ? 4u : L - 4u * j) : 0u;
+        m[j] = n == 4 ? 0xFFFFFFFFu : ((1u << (8 * n)) - 1u);
+    }
+    return m;
+}
+__device__ __forceinline__ int32_t clamp16(int32_t x) { return x < 0 ? 0 : (x > 16 ? 16 : x); }
+__device__ __forceinline__ u32x4 pm_range(const u32x4* __restrict__ pm, int32_t lo, int32_t hi) {
+    const u32x4 h = pm[clamp16(hi)], l = pm[clamp16(lo)];
+    return h & ~l;
+}
+
 // The span lane r0 + lane of a window, as loaded (valid = the span exists).
 __device__ __forceinline__ bool load_span_lane(const Span* __restrict__ spans, uint32_t n_spans, uint32_t r0,
                                                uint32_t lane, Span& sp) {
@@ -135,7 +155,7 @@ __device__ __forceinline__ bool load_span_lane(const Span* __restrict__ spans, u
 template <bool COMPACT, int P, int NT>
 __device__ __forceinline__ bool unmask_window_lanes(uint8_t* __restrict__ dst, const Span& sp, bool valid,
                                                     uint32_t n_spans, uint32_t r0, uint64_t wbase, uint32_t lane,
-                                                    const u32x4 (&v)[P]) {
+                                                    const u32x4 (&v)[P], const u32x4* __restrict__ pm) {
     constexpr int32_t WB = 1024 * P;
     int32_t rd = WB + 64, re = WB + 64;   // window-relative wire [start, end), clipped to [-1, WB + 64]
     uint32_t key = 0;
@@ -217,8 +237,8 @@ __device__ __forceinline__ bool unmask_window_lanes(uint8_t* __restrict__ dst, c
         u32x4 acc[P];
 #pragma unroll
         for (int k = 0; k < P; ++k) {
-            const u32x4 ma = alo[k] < ahi[k] ? range_mask16(alo[k], ahi[k]) : u32x4{0, 0, 0, 0};
-            const u32x4 mb = blo[k] < bhi[k] ? range_mask16(blo[k], bhi[k]) : u32x4{0, 0, 0, 0};
+            const u32x4 ma = pm_range(pm, alo[k], ahi[k]);
+            const u32x4 mb = pm_range(pm, blo[k], bhi[k]);
             acc[k] = v[k] ^ ((ka[k] & ma) | (kb[k] & mb));
             // span B ends inside the piece and another span follows it there (spans < 16 B)
             more |= bhi[k] == 16 ? false : (bhi[k] >= 0 && ta[k] + 2 < (int32_t)nl);
@@ -235,7 +255,7 @@ __device__ __forceinline__ bool unmask_window_lanes(uint8_t* __restrict__ dst, c
                     act = act && t < (int32_t)nl && dt < pr + 16;
                     if (act) {
                         const int32_t l = (dt > pr ? dt : pr) - pr, h = (et < pr + 16 ? et : pr + 16) - pr;
-                        if (l < h) acc[k] ^= kt & range_mask16(l, h);
+                        acc[k] ^= kt & pm_range(pm, l, h);
                     }
                     ++t;
                 }
@@ -289,6 +309,9 @@ __device__ __forceinline__ void unmask_all(uint8_t* __restrict__ dst, const uint
                                            uint32_t* __restrict__ lb_state, uint32_t n_walk_blocks) {
     constexpr uint32_t WB = 1024u * P;
     static_assert(NT < 16 || !COMPACT, "buffer-instruction windows are the in-place path");
+    __shared__ u32x4 pm[17];
+    if (threadIdx.x < 17) pm[threadIdx.x] = prefix_mask16(threadIdx.x);
+    __syncthreads();
     // re-arm the walk's look-back state for the next decode (this launch is ordered after it):
     // lb_state[0] = ticket, [1] = timeout flag, [2 ...] = per-block flags
     for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n_walk_blocks + 2; t += gridDim.x * blockDim.x)
@@ -344,7 +367,7 @@ __device__ __forceinline__ void unmask_all(uint8_t* __restrict__ dst, const uint
         // span lookup; more than 64 spans in one window falls back to the serial span walk.
         Span sp;
         const bool valid = load_span_lane(spans, n_spans, r, lane, sp);
-        if (!unmask_window_lanes<COMPACT, P, NT>(dst, sp, valid, n_spans, r, wbase, lane, v))
+        if (!unmask_window_lanes<COMPACT, P, NT>(dst, sp, valid, n_spans, r, wbase, lane, v, pm))
             unmask_window_general<COMPACT, P, NT>(dst, src, src_bytes, total, spans, n_spans, r, wbase, lofs);
     }
 }

@@ -1,0 +1,16 @@
+"""bench.py's other_configs lines alone (optionally a subset by name fragment), one JSON line:
+    python tools/cfg_bench.py ["configs[2]" ...]"""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from netman_amd import codec as K  # noqa: E402
+from netman_amd import synth  # noqa: E402
+
+if __name__ == "__main__":
+    print(json.dumps(bench.other_configs(torch, K, synth, only=sys.argv[1:] or None)))

@@ -1,0 +1,45 @@
+"""Back-to-back decodes of one device batch on one stream (one batch in flight), for kernel-trace
+gap analysis:  python tools/single_loop.py <config> [iters]
+config: head (16384 x 64 KiB, 4/seg) | c1 (1M x 1 KiB, 16/seg) | c2 (256k mixed, 16/seg)"""
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from netman_amd import codec as K  # noqa: E402
+from netman_amd import synth  # noqa: E402
+
+
+def main():
+    which = sys.argv[1] if len(sys.argv) > 1 else "c1"
+    iters = int(sys.argv[2]) if len(sys.argv) > 2 else 30
+    cfg = {"head": lambda: synth.uniform_batch(16384, 65536, 4, seed=synth.SEED_BASE + 1),
+           "c1": lambda: synth.uniform_batch(1 << 20, 1024, 16, seed=synth.SEED_BASE + 1),
+           "c2": lambda: synth.mixed_batch()}[which]()
+    dev = torch.device("cuda:0")
+    n = len(cfg["seg_off"]) - 1
+    kw = {"unmask_window": int(os.environ["WIN"])} if os.environ.get("WIN") else {}
+    c = K.Codec(0, max_batch_bytes=len(cfg["wire"]) + 4096, max_segs=n, max_frames=cfg["n_frames"] + 16, **kw)
+    t = dict(wire=torch.from_numpy(cfg["wire"]).to(dev), seg_off=torch.from_numpy(cfg["seg_off"].view(np.int64)).to(dev),
+             st=torch.zeros(n * 16, dtype=torch.uint8, device=dev), so=torch.zeros(n * 32, dtype=torch.uint8, device=dev),
+             fr=torch.zeros((cfg["n_frames"] + 16) * 32, dtype=torch.uint8, device=dev), sm=torch.zeros(32, dtype=torch.uint8, device=dev))
+    b = c.make_batch(t["wire"], t["seg_off"], None, t["st"], t["so"], t["fr"], t["sm"])
+    st = torch.cuda.Stream(device=dev)
+    for _ in range(3):
+        c.decode(b, st.cuda_stream)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        c.decode(b, st.cuda_stream)
+    torch.cuda.synchronize()
+    el = (time.perf_counter() - t0) / iters * 1e3
+    print(f"{which}: {el:.4f} ms per decode, {cfg['payload_bytes'] / (el * 1e-3) / 2**30:.1f} GiB/s, errors {c.error_flags()}")
+    c.close()
+
+
+if __name__ == "__main__":
+    main()
