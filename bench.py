@@ -300,6 +300,7 @@ def main():
     if solo and not a.no_host_inclusive:
         out["host_inclusive"] = host_inclusive(codec, cfg, K)
         out["host_inclusive_pipelined"] = host_inclusive_pipelined(torch, codecs, streams, cfg, K)
+        out["host_inclusive_zero_copy"] = host_inclusive_zero_copy(torch, codecs, streams, cfg, K)
     for c in codecs:
         c.close()
     if solo and not a.no_other_configs:
@@ -674,6 +675,94 @@ def host_inclusive_pipelined(torch, codecs, streams, cfg, K, chunks=16, iters=3)
     return {"gib_s": round(cfg["payload_bytes"] / el / 2**30, 2), "ms_per_batch": round(el * 1e3, 2),
             "chunks": len(pieces), "streams": P, "parity_ok": ok,
             "note": "pinned host wire -> H2D -> decode -> D2H wire+records, pieces alternating over streams"}
+
+
+def host_inclusive_zero_copy(torch, codecs, streams, cfg, K, chunks=16, iters=3):
+    """Host-inclusive with the outbound copy done by the unmask itself: H2D of each piece's wire on
+    the copy engine (stream j), walk on the device copy, then the COMPACT unmask writes each
+    payload straight into a pinned, device-mapped host arena over PCIe -- the host receives the
+    messages' bytes (headers stripped, wsc_session's COMPACT layout) and the records.  The next
+    piece's H2D (copy engine, host -> device) runs while this piece's unmask writes device -> host:
+    both PCIe directions busy at once, which the copy engines alone do not do for one process
+    (DESIGN.md, profiles/r01_pcie_duplex.log).  Reported in DESIGN.md, never as `value`."""
+    from netman_amd import synth
+    P = len(codecs)
+    if P < 2:
+        return None
+    lib = K.load_library()
+    dev = torch.device("cuda", torch.cuda.current_device())
+    wire_h = torch.from_numpy(cfg["wire"]).pin_memory()
+    so = cfg["seg_off"].astype(np.int64)
+    n_segs = len(so) - 1
+    cuts = [int(round(i * n_segs / chunks)) for i in range(chunks + 1)]
+    poff = cfg["payload_off"].astype(np.int64)
+    plen = cfg["plen"].astype(np.int64)
+    pieces, abase = [], 0
+    for i in range(chunks):
+        s0, s1 = cuts[i], cuts[i + 1]
+        if s1 <= s0:
+            continue
+        a0, a1 = int(so[s0]), int(so[s1])
+        sel = (poff >= a0) & (poff < a1)
+        nb = int(plen[sel].sum())
+        rel = torch.from_numpy((so[s0:s1 + 1] - so[s0]).copy()).pin_memory()
+        pieces.append((a0, a1, s1 - s0, rel, abase, int(np.count_nonzero(sel))))
+        abase += (nb + 15) // 16 * 16
+    arena_bytes = abase + 64
+    ap = C.c_void_p()
+    if lib.wsc_host_alloc(arena_bytes, C.byref(ap)) != 0:
+        return None
+    try:
+        arena_h = np.frombuffer((C.c_uint8 * arena_bytes).from_address(ap.value), dtype=np.uint8)
+        max_bytes = max(p[1] - p[0] for p in pieces)
+        max_segs = max(p[2] for p in pieces)
+        max_frames = int(codecs[0].cfg.max_frames)
+        bufs = []
+        for j in range(P):
+            bufs.append(dict(wire=torch.empty(max_bytes + 16, dtype=torch.uint8, device=dev),
+                             seg_off=torch.empty(max_segs + 1, dtype=torch.int64, device=dev),
+                             st=torch.empty(max_segs * 16, dtype=torch.uint8, device=dev),
+                             so=torch.empty(max_segs * 32, dtype=torch.uint8, device=dev),
+                             fr=torch.empty(max_frames * 32, dtype=torch.uint8, device=dev),
+                             fd=torch.empty(max_frames, dtype=torch.int64, device=dev),
+                             sm=torch.empty(32, dtype=torch.uint8, device=dev)))
+        rec_h = [torch.empty(max(1, p[5]) * 32, dtype=torch.uint8).pin_memory() for p in pieces]
+
+        def one_pass():
+            for i, (a0, a1, k, rel, ab, nf) in enumerate(pieces):
+                j = i % P
+                st, b = streams[j], bufs[j]
+                with torch.cuda.stream(st):
+                    b["wire"][: a1 - a0].copy_(wire_h[a0:a1], non_blocking=True)
+                    b["seg_off"][: k + 1].copy_(rel, non_blocking=True)
+                    batch = codecs[j].make_batch(b["wire"], b["seg_off"][: k + 1], None, b["st"], b["so"], b["fr"],
+                                                 b["sm"], compact=True, arena=None, frame_dst=b["fd"], n_bytes=a1 - a0)
+                    batch.arena = ap.value + ab
+                    codecs[j].decode(batch, st.cuda_stream)
+                    rec_h[i][: nf * 32].copy_(b["fr"][: nf * 32], non_blocking=True)
+
+        one_pass()
+        torch.cuda.synchronize()
+        # parity: the first piece's messages, in order, are the unmasked payloads
+        a0, a1, _, _, ab, nf = pieces[0]
+        k = min(nf, 64)
+        ref = synth.unmask_reference(cfg["wire"][: int(poff[k - 1] + plen[k - 1])], cfg["payload_off"][:k],
+                                     cfg["plen"][:k], cfg["mask"][:k])
+        want = np.concatenate([ref[int(poff[i]):int(poff[i] + plen[i])] for i in range(k)])
+        ok = bool(np.array_equal(arena_h[ab:ab + len(want)], want))
+        ok = ok and all(c.error_flags() == 0 for c in codecs)
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            one_pass()
+        torch.cuda.synchronize()
+        el = (time.perf_counter() - t0) / iters
+        return {"gib_s": round(cfg["payload_bytes"] / el / 2**30, 2), "ms_per_batch": round(el * 1e3, 2),
+                "chunks": len(pieces), "streams": P, "parity_ok": ok,
+                "note": "pinned host wire -> H2D (copy engine) -> walk -> COMPACT unmask writing the messages "
+                        "into a pinned host arena over PCIe (+ records D2H), pieces alternating over streams"}
+    finally:
+        torch.cuda.synchronize()
+        lib.wsc_host_free(ap)
 
 
 def synth_unmask_prefix(cfg, n):
