@@ -16,7 +16,7 @@ template <bool COMPACT, uint32_t KR, uint32_t NT, uint32_t G> __global__ void k_
 template <bool COMPACT> __global__ void k_walk_count(WalkArgs);
 __global__ void k_walk_scan(WalkArgs, uint32_t);
 template <bool COMPACT> __global__ void k_walk_emit(WalkArgs);
-__global__ void k_u8_check(U8Args);
+template <uint32_t NCH> __global__ void k_u8_check(U8Args);
 template <bool COMPACT, int P, int NT, int MINW>
 __global__ void k_unmask(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*,
                          const wsc_summary*, uint32_t*, uint32_t, uint32_t*, uint32_t*, uint32_t);
@@ -61,6 +61,7 @@ struct wsc_ctx {
     bool fin_pending = false;         // a staged unmask was enqueued without ev_done
     hipStream_t fin_stream = nullptr; // ... on this stream
     bool walk_waited = false;         // wsc_walk_wait saw the last walk complete
+    int u8_chains = 2;                // WSC_U8_CHAINS: independent byte chains per 64-byte lane chunk (1, 2, 4)
     int unmask_buf = 3;               // WSC_UNMASK_BUF: in-place windows through buffer ops (1 nt, 2 nt sc1, 3 sc0 nt sc1
                                       // stores; 0 = 64-bit global addresses).  3: headline 2,890-2,898 -> 2,911-2,918
                                       // GiB/s (A/B on one box, profiles/r02_unmask_policy.log)
@@ -251,6 +252,7 @@ int wsc_create(int device, const wsc_config* cfg_in, wsc_ctx** out) {
     chk(hipMalloc(&c->u8maps, (uint64_t)c->u8items_cap * sizeof(uint64_t)), "hipMalloc u8maps");
     chk(hipMalloc(&c->u8seg, (uint64_t)cfg.max_segs * sizeof(U8Seg)), "hipMalloc u8seg");
     if (const char* e = std::getenv("WSC_UNMASK_BUF"); e && *e) c->unmask_buf = std::atoi(e);
+    if (const char* e = std::getenv("WSC_U8_CHAINS"); e && *e) c->u8_chains = std::atoi(e);
     if (const char* e = std::getenv("WSC_U8_GRID"); e && *e) c->u8_grid = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("WSC_WALK_MODE"); e && *e) {   // pin a walk geometry (tests, A/B): 64, 256 or 3
         const int m = std::atoi(e);
@@ -430,7 +432,10 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
         ua.seg_out = b->seg_out;
         ua.state_out = b->state_out;
         ua.summary = b->summary;
-        hipLaunchKernelGGL(k_u8_check, dim3(c->u8_grid ? c->u8_grid : (uint32_t)c->n_cu * 5), dim3(256), 0, st, ua);   // resident: 5 waves/SIMD (96 VGPRs)
+        const dim3 ug(c->u8_grid ? c->u8_grid : (uint32_t)c->n_cu * 5);   // resident: 5 waves/SIMD (96 VGPRs)
+        if (c->u8_chains == 1) hipLaunchKernelGGL(k_u8_check<1>, ug, dim3(256), 0, st, ua);
+        else if (c->u8_chains == 4) hipLaunchKernelGGL(k_u8_check<4>, ug, dim3(256), 0, st, ua);
+        else hipLaunchKernelGGL(k_u8_check<2>, ug, dim3(256), 0, st, ua);
         HIP_TRY(hipGetLastError());
     }
     rec(2);

@@ -1190,91 +1190,156 @@ __device__ __forceinline__ void u8_finish(const U8Args& a, uint32_t it, uint32_t
         if (a.spans[g.sbase + k].src >= fend) a.spans[g.sbase + k].key = 0;
 }
 
-// 5 waves per SIMD (96 VGPRs, a few spilled): 4 waves without spills measured 8-30 % slower
+// 5 waves per SIMD (96 VGPRs).  Each lane folds a 64-byte chunk (4 x 16 B loads) into one map, so
+// the wave-level composition (DPP row levels + 4 readlanes) is paid once per 64 bytes instead of
+// per 16: PMC showed the 16-byte-piece version at 12.5 VALU per text byte, VALU-bound (77 % of
+// the chip's VALU cycles).  Inside a chunk the first 4 bytes compose full maps (two v_perm per
+// byte from the 8-byte rows of `tab`); every entry state that survives them is then in one state
+// X (see chunk_map), which steps through the other 60 bytes one byte-table read each
+// (`tab8[X][byte]`, state 8 = reject, absorbing): two VALU ops and one LDS read per byte.
+template <uint32_t NCH>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_u8_check(U8Args a) {
     const uint32_t n_items = *a.count;
     if (blockIdx.x * 4 >= n_items) return;   // nothing deferred (the common, binary case)
     __shared__ uint64_t tab[256];            // T[byte]: the map of that single byte
+    __shared__ uint8_t tab8[9 * 256];        // [state][byte] -> next state (8 = reject)
     {
         const uint32_t byte = threadIdx.x;
         uint64_t t = 0;
         for (uint32_t st = 0; st < 8; ++st) {
             const uint32_t ns = u8_step(st, byte);
             t |= (uint64_t)(ns == 8 ? 0xFFu : ns) << (8 * st);
+            tab8[st * 256 + byte] = (uint8_t)ns;
         }
+        tab8[8 * 256 + byte] = 8;
         tab[byte] = t;
     }
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
     const uint32_t nw = gridDim.x * 4;
-    // The map of one lane's 16-byte piece (nk valid bytes, masked with `mask`); plain = no
-    // non-ASCII byte among them.
-    auto piece_map = [&](const uint4 v, uint32_t mask, uint32_t nk, bool& plain) -> uint64_t {
-        uint32_t d[4] = {0, 0, 0, 0};
-        if (nk) { d[0] = v.x ^ mask; d[1] = v.y ^ mask; d[2] = v.z ^ mask; d[3] = v.w ^ mask; }
-        uint32_t hib = 0;
+    // Global loads stay coalesced (piece k of a step: 16 B per lane at base_k + 16 * lane, 1 KiB
+    // per instruction); a per-wave LDS stage turns them into one contiguous 64-byte chunk per lane
+    // (chunks padded to 80 B: the 16 lanes of a ds_read_b128 phase then hit 16 distinct bank
+    // groups).  Strided 16-byte global loads at a 64-byte lane stride measured slower.
+    __shared__ uint4 stage[4][64 * 5];
+    uint4* const sw = stage[threadIdx.x >> 6];
+    auto restage = [&](uint4 (&q)[4]) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t lim = nk > 4u * j ? (nk - 4u * j >= 4 ? 4u : nk - 4u * j) : 0u;
-            const uint32_t keep = lim >= 4 ? 0xFFFFFFFFu : ((1u << (8 * lim)) - 1u);
-            hib |= d[j] & keep & 0x80808080u;
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t b = 1024u * k + 16u * lane;
+            sw[(b >> 6) * 5 + ((b >> 4) & 3)] = q[k];
+        }
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int k = 0; k < 4; ++k) q[k] = sw[lane * 5 + k];
+        __builtin_amdgcn_wave_barrier();
+    };
+    // The map of one lane's 64-byte chunk (nk valid bytes, masked with `mask`); plain = no
+    // non-ASCII byte among them.
+    auto chunk_map = [&](const uint4 (&v)[4], uint32_t mask, uint32_t nk, bool& plain) -> uint64_t {
+        // byte i of the chunk, unmasked (i constant after unrolling)
+        auto dw = [&](uint32_t j) -> uint32_t {
+            const uint4& q = v[j >> 2];
+            const uint32_t w = (j & 3) == 0 ? q.x : (j & 3) == 1 ? q.y : (j & 3) == 2 ? q.z : q.w;
+            return w ^ mask;
+        };
+        uint32_t hib = 0;
+        if (nk >= 64) {
+#pragma unroll
+            for (uint32_t j = 0; j < 16; ++j) hib |= dw(j);
+            hib &= 0x80808080u;
+        } else {
+#pragma unroll
+            for (uint32_t j = 0; j < 16; ++j) {
+                const uint32_t lim = nk > 4u * j ? (nk - 4u * j >= 4 ? 4u : nk - 4u * j) : 0u;
+                const uint32_t keep = lim >= 4 ? 0xFFFFFFFFu : ((1u << (8 * lim)) - 1u);
+                hib |= dw(j) & keep & 0x80808080u;
+            }
         }
         plain = true;
         if (nk == 0) return u8m_id();
         if (hib == 0) return u8m_ascii();
         plain = false;
-        if (nk == 16) {
-            // Every entry state that survives the first 4 bytes is in ONE state X there: a survivor
-            // must be in state 0 just before the first lead byte (a lead in a non-zero state
-            // rejects), and 4 continuation bytes reject every state (at most 3 are owed).  So the
-            // first 4 bytes compose full maps (2 v_perm per byte), the other 12 step the single
-            // state X (1 v_perm per byte), and the piece's map is the prefix map with every
-            // surviving entry sent to the final state.
-            uint32_t lo = 0x03020100u, hi = 0x07060504u;
+        // Every entry state that survives the first 4 bytes is in ONE state X there: a survivor
+        // must be in state 0 just before the first lead byte (a lead in a non-zero state rejects),
+        // and 4 continuation bytes reject every state (at most 3 are owed).  So the first 4 bytes
+        // compose full maps, the others step the single state X, and the chunk's map is the
+        // prefix map with every surviving entry sent to the final state.  A partial chunk (the
+        // last of an item) folds its bytes with full maps instead: its map must leave a
+        // character that the item ends inside owed, not rejected by padding.
+        uint32_t lo = 0x03020100u, hi = 0x07060504u;
+        if (nk < 64) {   // (unrolled with a guard: a dynamic index into the chunk would go to scratch)
 #pragma unroll
-            for (uint32_t i = 0; i < 4; ++i) {
-                const uint64_t t = tab[(d[0] >> (8 * i)) & 0xFFu];
-                const uint32_t tl = (uint32_t)t, th = (uint32_t)(t >> 32);
-                lo = (uint32_t)__builtin_amdgcn_perm(th, tl, lo);
-                hi = (uint32_t)__builtin_amdgcn_perm(th, tl, hi);
+            for (uint32_t i = 0; i < 64; ++i) {
+                if (i < nk) {
+                    const uint64_t t = tab[(dw(i >> 2) >> (8 * (i & 3))) & 0xFFu];
+                    const uint32_t tl = (uint32_t)t, th = (uint32_t)(t >> 32);
+                    lo = (uint32_t)__builtin_amdgcn_perm(th, tl, lo);
+                    hi = (uint32_t)__builtin_amdgcn_perm(th, tl, hi);
+                }
             }
-            uint32_t x = lo & hi;             // non-rejected bytes all equal X, rejects are 0xFF
-            x &= x >> 16;
-            x &= x >> 8;
-#pragma unroll
-            for (uint32_t i = 4; i < 16; ++i) {
-                const uint64_t t = tab[(d[i >> 2] >> (8 * (i & 3))) & 0xFFu];
-                x = (uint32_t)__builtin_amdgcn_perm((uint32_t)(t >> 32), (uint32_t)t, x);   // byte 0 = T[b][X]
-            }
-            const uint32_t fr = (x & 0xFFu) * 0x01010101u;
-            lo = (uint32_t)__builtin_amdgcn_perm(fr, fr, lo);   // 0..7 -> final state, 0xFF stays
-            hi = (uint32_t)__builtin_amdgcn_perm(fr, fr, hi);
             return (uint64_t)hi << 32 | lo;
         }
-        uint32_t lo = 0x03020100u, hi = 0x07060504u;
+        // NCH independent chains of 64 / NCH bytes, interleaved byte by byte (latency: each chain
+        // is a dependent sequence of LDS reads), composed in order at the end
+        constexpr uint32_t CW = 16 / NCH;     // dwords per chain
+        uint32_t clo[NCH], chi[NCH], st[NCH];
 #pragma unroll
-        for (uint32_t i = 0; i < 16; ++i) {
-            if (i < nk) {
-                const uint64_t t = tab[(d[i >> 2] >> (8 * (i & 3))) & 0xFFu];
+        for (uint32_t c = 0; c < NCH; ++c) {
+            const uint32_t d0 = dw(c * CW);
+            uint32_t l = 0x03020100u, h = 0x07060504u;
+#pragma unroll
+            for (uint32_t i = 0; i < 4; ++i) {
+                const uint64_t t = tab[(d0 >> (8 * i)) & 0xFFu];
                 const uint32_t tl = (uint32_t)t, th = (uint32_t)(t >> 32);
-                lo = (uint32_t)__builtin_amdgcn_perm(th, tl, lo);
-                hi = (uint32_t)__builtin_amdgcn_perm(th, tl, hi);
+                l = (uint32_t)__builtin_amdgcn_perm(th, tl, l);
+                h = (uint32_t)__builtin_amdgcn_perm(th, tl, h);
+            }
+            uint32_t x = l & h;             // non-rejected bytes all equal X, rejects are 0xFF
+            x &= x >> 16;
+            x &= x >> 8;
+            x &= 0xFFu;
+            st[c] = x > 7 ? 8u : x;
+            clo[c] = l;
+            chi[c] = h;
+        }
+        // one v_perm per byte builds the table index st << 8 | byte (and, depending on st, keeps
+        // the compiler from hoisting the byte extractions into live registers)
+#pragma unroll
+        for (uint32_t j = 1; j < CW; ++j) {
+#pragma unroll
+            for (uint32_t i = 0; i < 4; ++i) {
+#pragma unroll
+                for (uint32_t c = 0; c < NCH; ++c)
+                    st[c] = tab8[__builtin_amdgcn_perm(st[c], dw(c * CW + j), i | 4u << 8 | 0x0Cu << 16 | 0x0Cu << 24)];
             }
         }
-        return (uint64_t)hi << 32 | lo;
+        uint64_t m = u8m_id();
+#pragma unroll
+        for (uint32_t c = 0; c < NCH; ++c) {
+            const uint32_t fr = (st[c] > 7 ? 0xFFu : st[c]) * 0x01010101u;
+            const uint32_t l = (uint32_t)__builtin_amdgcn_perm(fr, fr, clo[c]);   // 0..7 -> final state
+            const uint32_t h = (uint32_t)__builtin_amdgcn_perm(fr, fr, chi[c]);
+            m = c == 0 ? ((uint64_t)h << 32 | l) : u8m_then(m, (uint64_t)h << 32 | l);
+        }
+        return m;
     };
-    // The map of one 1 KiB wave piece (the 64 lanes' maps in lane order), wave-uniform.
-    auto wave_map = [&](uint64_t pm, bool plain) -> uint64_t {
-        if (__ballot(!plain) == 0)            // ASCII (or empty) everywhere: one constant map
-            return __ballot(pm == u8m_ascii()) ? u8m_ascii() : u8m_id();
-        // compose the 16 lanes of each row in order with DPP row shifts (VALU, no LDS crossbar:
-        // the table reads already keep the LDS pipe busy), then the 4 rows
+    // The 16-lane rows' maps in lane order (DPP row shifts), left in lanes 0, 16, 32, 48.
+    auto row_maps = [&](uint64_t pm) -> uint64_t {
         uint32_t mlo = (uint32_t)pm, mhi = (uint32_t)(pm >> 32);
         u8m_row_level<1>(mlo, mhi, lane);
         u8m_row_level<2>(mlo, mhi, lane);
         u8m_row_level<4>(mlo, mhi, lane);
         u8m_row_level<8>(mlo, mhi, lane);
+        return (uint64_t)mhi << 32 | mlo;
+    };
+    // The map of a 4 KiB wave step (the 64 lanes' chunk maps in lane order), wave-uniform.
+    auto wave_map = [&](uint64_t pm, bool plain) -> uint64_t {
+        if (__ballot(!plain) == 0)            // ASCII (or empty) everywhere: one constant map
+            return __ballot(pm == u8m_ascii()) ? u8m_ascii() : u8m_id();
+        const uint64_t rm = row_maps(pm);
+        const uint32_t mlo = (uint32_t)rm, mhi = (uint32_t)(rm >> 32);
         uint64_t m = u8m_id();
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -1285,58 +1350,60 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
         }
         return m;
     };
-    // 4 KiB of x.src + b0 into q (bytes past the item read as 0)
+    // a 4 KiB step of item x at item offset b0, coalesced (bytes past the item read as 0)
     auto fetch = [&](const U8Item& x, uint32_t b0, uint4 (&q)[4]) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const uint32_t off = b0 + k * 1024 + lane * 16;
-            q[k] = off < x.len ? load16_unaligned(a.wire, (int64_t)(x.src + off), a.n_bytes) : make_uint4(0, 0, 0, 0);
+            const uint32_t o = b0 + 1024u * k + 16u * lane;
+            q[k] = o < x.len ? load16_unaligned(a.wire, (int64_t)(x.src + o), a.n_bytes) : make_uint4(0, 0, 0, 0);
         }
     };
+    auto chunk_len = [](uint32_t len, uint32_t off) -> uint32_t {
+        return off < len ? (len - off >= 64 ? 64u : len - off) : 0u;
+    };
     // A unit is 4 consecutive items.  Units of small items (<= 1 KiB each: 1 KiB text frames) take
-    // one step: piece k is item k's first KiB, and lanes 0..3 publish the 4 items' maps at once
-    // (a 1 KiB item alone would leave 3/4 of the step's loads idle and serialise the per-item
-    // hand-off).  Other units walk their items' 4 KiB steps in order, the next step's loads -- the
-    // next item's first step too -- issued before the current step is folded.
+    // one step: row r (16 lanes x 64 B) holds item r, and lanes 0, 16, 32, 48 publish the 4 items'
+    // maps.  Other units walk their items' 4 KiB steps in order, the next step's loads -- the next
+    // item's first step too -- issued before the current step is folded.
+    // A unit is 4 consecutive items.  Units of small items (<= 1 KiB each: 1 KiB text frames) take
+    // one step: row r (16 lanes x 64 B) holds item r, and lanes 0, 16, 32, 48 publish the 4 items'
+    // maps.  Other units walk their items' 4 KiB steps in order, the next step's loads -- the next
+    // item's first step too -- issued before the current step is folded.  (A ticket counter for
+    // dynamic balance measured far slower: 64 k same-address atomics; a second pass striding big
+    // items one by one paid a scan of every unit's lengths per wave.)
     const uint32_t n_units = (n_items + 3) / 4;
     for (uint32_t u = gw; u < n_units; u += nw) {
         const uint32_t i0 = 4 * u;
         const uint32_t cnt = n_items - i0 < 4 ? n_items - i0 : 4u;
-        U8Item x[4];
         bool small = true;
-#pragma unroll
-        for (uint32_t j = 0; j < 4; ++j) {
-            if (j < cnt) {
-                x[j] = a.items[i0 + j];
-                small = small && x[j].len <= 1024;
-            } else {
-                x[j] = x[0];
-                x[j].len = 0;
-            }
-        }
+        for (uint32_t j = 0; j < cnt; ++j) small = small && a.items[i0 + j].len <= 1024;
         if (small) {
+            // piece k of the step = item k's KiB (16 B per lane, coalesced), restaged so that row r
+            // (lanes 16r..16r+15) holds item r in 64-byte chunks
             uint4 q[4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k)
-                q[k] = lane * 16 < x[k].len ? load16_unaligned(a.wire, (int64_t)(x[k].src + lane * 16), a.n_bytes)
-                                            : make_uint4(0, 0, 0, 0);
-            uint64_t mine = u8m_id();
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const uint32_t off = lane * 16;
-                const uint32_t nk = off < x[k].len ? (x[k].len - off >= 16 ? 16u : x[k].len - off) : 0u;
-                bool plain;
-                const uint64_t pm = piece_map(q[k], x[k].mask, nk, plain);
-                const uint64_t m = wave_map(pm, plain);
-                if (lane == (uint32_t)k) mine = m;
+            for (uint32_t k = 0; k < 4; ++k) {
+                const U8Item xk = a.items[i0 + (k < cnt ? k : 0u)];
+                const uint32_t len = k < cnt ? xk.len : 0u;
+                q[k] = 16u * lane < len ? load16_unaligned(a.wire, (int64_t)(xk.src + 16u * lane), a.n_bytes)
+                                        : make_uint4(0, 0, 0, 0);
             }
-            const uint32_t seg = lane == 0 ? x[0].seg : lane == 1 ? x[1].seg : lane == 2 ? x[2].seg : x[3].seg;
-            if (lane < cnt) u8_finish(a, i0 + lane, seg, mine);
+            restage(q);
+            const uint32_t r = lane >> 4;
+            U8Item xr;
+            if (r < cnt) xr = a.items[i0 + r];
+            else { xr = a.items[i0]; xr.len = 0; }
+            const uint32_t off = (lane & 15) * 64;
+            bool plain;
+            const uint64_t pm = chunk_map(q, xr.mask, chunk_len(xr.len, off), plain);
+            const uint64_t rm = row_maps(pm);
+            if ((lane & 15) == 0 && r < cnt) u8_finish(a, i0 + r, xr.seg, rm);
             continue;
         }
+        const U8Item x0 = a.items[i0];
         uint4 nxt[4];
-        fetch(x[0], 0, nxt);
-        U8Item item2 = x[0];   // (items re-read by index: no dynamically indexed register array)
+        fetch(x0, 0, nxt);
+        U8Item item2 = x0;   // (items re-read by index: no dynamically indexed register array)
         for (uint32_t j = 0; j < cnt; ++j) {
             const U8Item item = item2;
             if (j + 1 < cnt) item2 = a.items[i0 + j + 1];
@@ -1348,33 +1415,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
                 for (int k = 0; k < 4; ++k) cur4[k] = nxt[k];
                 if (b0 + 4096 < item.len) fetch(item, b0 + 4096, nxt);
                 else if (j + 1 < cnt) fetch(item2, 0, nxt);
-                uint64_t pm[4];
-                bool plain = true;
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const uint32_t off = b0 + k * 1024 + lane * 16;
-                    const uint32_t nk = off < item.len ? (item.len - off >= 16 ? 16u : item.len - off) : 0u;
-                    bool pl;
-                    pm[k] = piece_map(cur4[k], item.mask, nk, pl);
-                    plain = plain && pl;
-                }
-                uint64_t stepm;
-                if (__ballot(!plain) == 0) {      // ASCII (or empty) everywhere: one constant map
-                    stepm = __ballot(pm[0] == u8m_ascii()) ? u8m_ascii() : u8m_id();
-                } else {
-                    stepm = u8m_id();
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {     // pieces in order
-                        if (b0 + k * 1024 >= item.len) break;   // the rest of the step is past the item
-                        stepm = u8m_then(stepm, wave_map(pm[k], false));
-                    }
-                }
-                acc = u8m_then(acc, stepm);
+                restage(cur4);
+                bool plain;
+                const uint64_t pm = chunk_map(cur4, item.mask, chunk_len(item.len, b0 + lane * 64), plain);
+                acc = u8m_then(acc, wave_map(pm, plain));
             }
             if (lane == 0) u8_finish(a, i0 + j, item.seg, acc);
         }
     }
 }
+
+template __global__ void k_u8_check<1>(U8Args);
+template __global__ void k_u8_check<2>(U8Args);
+template __global__ void k_u8_check<4>(U8Args);
 
 // explicit instantiations used by the host code: 16 frame records per lane, one segment per
 // lane, blocks of 64 or 256 lanes; batches of more segments use the three-launch walk below
