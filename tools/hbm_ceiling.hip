@@ -64,6 +64,38 @@ __global__ __launch_bounds__(256) void xor_policy(uint8_t* __restrict__ buf, uin
     }
 }
 
+// two windows per wave, software-pipelined: window w+nw's loads are issued before window w's
+// stores (more bytes in flight per wave, stores never wait behind their own loads)
+template <int P, int LA, int SA>
+__global__ __launch_bounds__(256) void xor_pipe2(uint8_t* __restrict__ buf, uint64_t n_win, uint32_t key) {
+    const uint64_t nw = (uint64_t)gridDim.x * 4;
+    const uint64_t w0 = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint32_t lo = (threadIdx.x & 63) * 16u;
+    uint64_t w = w0;
+    if (w >= n_win) return;
+    __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(buf + w * (1024u * P), 0, 1024u * P, 0x00020000);
+    u32x4 v[P];
+#pragma unroll
+    for (int k = 0; k < P; ++k) v[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, lo + k * 1024u, 0, LA));
+    for (;;) {
+        const uint64_t wn = w + nw;
+        u32x4 nv[P];
+        __amdgpu_buffer_rsrc_t rn = r;
+        if (wn < n_win) {
+            rn = __builtin_amdgcn_make_buffer_rsrc(buf + wn * (1024u * P), 0, 1024u * P, 0x00020000);
+#pragma unroll
+            for (int k = 0; k < P; ++k) nv[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rn, lo + k * 1024u, 0, LA));
+        }
+#pragma unroll
+        for (int k = 0; k < P; ++k) __builtin_amdgcn_raw_buffer_store_b128(v[k] ^ key, r, lo + k * 1024u, 0, SA);
+        if (wn >= n_win) break;
+        w = wn;
+        r = rn;
+#pragma unroll
+        for (int k = 0; k < P; ++k) v[k] = nv[k];
+    }
+}
+
 __global__ __launch_bounds__(256) void copy16(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, uint64_t n16) {
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (i < n16) reinterpret_cast<float4*>(dst)[i] = reinterpret_cast<const float4*>(src)[i];
@@ -140,6 +172,22 @@ int main(int argc, char** argv) {
         POL(2, 2, false) POL(0, 2, false) POL(2, 0, false) POL(0, 0, false)
         POL(3, 3, false) POL(2, 3, false) POL(2, 19, false) POL(19, 2, false) POL(19, 19, false) POL(2, 18, false)
         POL(2, 16, false) POL(2, 1, false) POL(2, 2, true) POL(0, 0, true)
+        for (int rep = 0; rep < 2; ++rep) {
+            timeit("pol8 L2 S19", rw, [&] {
+                const uint64_t nw8 = n / 8192;
+                hipLaunchKernelGGL((xor_policy<8, 2, 19, false>), dim3((uint32_t)(((nw8 + 3) / 4 + 7) / 8 * 8)), dim3(256), 0, 0, buf, nw8, 0x12345678u);
+            });
+            timeit("pol4 L2 S19", rw, [&] {
+                hipLaunchKernelGGL((xor_policy<4, 2, 19, false>), g, dim3(256), 0, 0, buf, nw, 0x12345678u);
+            });
+            for (int wpc : {8, 12, 16, 24, 32}) {
+                char name[64];
+                snprintf(name, sizeof name, "pipe2 P4 wpc%d", wpc);
+                timeit(name, rw, [&] {
+                    hipLaunchKernelGGL((xor_pipe2<4, 2, 19>), dim3(256 * wpc / 4), dim3(256), 0, 0, buf, nw, 0x12345678u);
+                });
+            }
+        }
         timeit("xor_inplace<4>", rw, [&] {
             hipLaunchKernelGGL(xor_inplace<4>, dim3((uint32_t)((nw + 3) / 4)), dim3(256), 0, 0, buf, nw, 0x12345678u);
         });
