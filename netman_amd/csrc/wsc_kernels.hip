@@ -445,7 +445,25 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
                     const uint8_t kind = part ? U8K_PART : (chain ? U8K_CHAIN : U8K_SELF);
                     const uint8_t s_in = (part || chain) ? (u8_pending ? 0xFF : (uint8_t)u8dfa) : 0;
                     const uint32_t pieces = n ? (uint32_t)((n + U8_PIECE - 1) / U8_PIECE) : 1u;
-                    const uint32_t b0 = __hip_atomic_fetch_add(a.u8count, pieces, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    // wave-aggregated allocation when every active lane takes one item (text frames
+                    // <= 16 KiB): one atomic per wave instead of one per frame (262 k same-address
+                    // atomics: the 1 KiB TEXT walk 97 -> 74.5 us with aggregation)
+                    uint32_t b0;
+                    {
+                        const uint64_t act = __ballot(true);
+                        if (__ballot(pieces != 1) == 0) {
+                            const uint32_t leader = (uint32_t)__builtin_ctzll(act);
+                            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32),
+                                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
+                            uint32_t base = 0;
+                            if (rank == 0)
+                                base = __hip_atomic_fetch_add(a.u8count, (uint32_t)__builtin_popcountll(act), __ATOMIC_RELAXED,
+                                                              __HIP_MEMORY_SCOPE_AGENT);
+                            b0 = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)leader) + rank;
+                        } else {
+                            b0 = __hip_atomic_fetch_add(a.u8count, pieces, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        }
+                    }
                     if (b0 == 0 && a.u8host) {   // the first deferral tells the host the check has work
                         __hip_atomic_store(a.u8host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                         __threadfence_system();
