@@ -1158,11 +1158,12 @@ __device__ __forceinline__ uint32_t u8m_get(uint64_t m, uint32_t st) {   // st: 
 // Publish one item's map; the segment's last item composes the segment's items in frame order
 // with the walk's states and applies the verdict (one lane).
 __device__ __forceinline__ void u8_finish(const U8Args& a, uint32_t it, uint32_t seg, uint64_t acc) {
+    const uint32_t n = a.seg[seg].n;   // (static: loaded beside the map store, not after the count)
     __hip_atomic_store(a.maps + it, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const uint32_t done = __hip_atomic_fetch_add(&a.seg[seg].done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+    if (done != n) return;
     const U8Seg g = a.seg[seg];
-    if (done != g.n) return;
     // the segment's last item: compose its items in frame order with the walk's states
     uint32_t cur = 0, start = 0, fail = 0xFFFFFFFFu;   // states 0..7, 0xFF = reject
     uint64_t fm = u8m_id();
@@ -1398,6 +1399,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
         if (small) {
             // piece k of the step = item k's KiB (16 B per lane, coalesced), restaged so that row r
             // (lanes 16r..16r+15) holds item r in 64-byte chunks
+            const uint32_t r = lane >> 4;
+            U8Item xr;   // (issued before the data loads: its latency overlaps theirs)
+            if (r < cnt) xr = a.items[i0 + r];
+            else { xr = a.items[i0]; xr.len = 0; }
             uint4 q[4];
 #pragma unroll
             for (uint32_t k = 0; k < 4; ++k) {
@@ -1407,10 +1412,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
                                         : make_uint4(0, 0, 0, 0);
             }
             restage(q);
-            const uint32_t r = lane >> 4;
-            U8Item xr;
-            if (r < cnt) xr = a.items[i0 + r];
-            else { xr = a.items[i0]; xr.len = 0; }
             const uint32_t off = (lane & 15) * 64;
             bool plain;
             const uint64_t pm = chunk_map(q, xr.mask, chunk_len(xr.len, off), plain);
