@@ -27,7 +27,7 @@ FRAMES_PER_SEG = 4
 RECORD_BYTES = 32          # sizeof(wsc_frame)
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 # (walk CUs, unmask only on the other CUs) tried for each other_configs line's pipelined column
-PIPELINE_SPLITS = [(16, 0), (32, 1), (64, 1), (96, 1), (128, 1), (128, 0)]
+PIPELINE_SPLITS = [(16, 0), (32, 1), (64, 1), (80, 1), (96, 1), (112, 1), (128, 1), (128, 0)]
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 
 

@@ -132,10 +132,14 @@ static uint32_t stream_cus(const wsc_ctx* c, hipStream_t s) {
 }
 static uint32_t walk_mode(const wsc_ctx* c, uint32_t n_segs, uint32_t cus) {
     if (c->walk_mode) return (uint32_t)c->walk_mode;
-    if (cus < (uint32_t)c->n_cu)   // a CU-masked walk stream: 4 resident 64-lane blocks per CU
-        return n_segs <= 256u * cus ? 64u : 3u;   // (headline pipeline: 2,941 vs 2,842 GiB/s with 256-lane blocks)
-    if (n_segs <= 64u * cus) return 64;
-    if (n_segs <= 256u * cus) return 256;
+    // a CU-masked walk stream whose CUs hold every segment in 4 resident 64-lane blocks per CU:
+    // 64-lane blocks (headline pipeline, 16 CUs: 2,941 vs 2,842 GiB/s with 256-lane blocks).
+    // Larger batches keep the whole-chip choice: measured, a fused walk whose blocks are not all
+    // resident still beat the three-launch walk there (configs[1] on 32 CUs: 0.435 vs 0.497 ms)
+    if (cus < (uint32_t)c->n_cu && n_segs <= 256u * cus) return 64;
+    const uint32_t all = (uint32_t)c->n_cu;
+    if (n_segs <= 64u * all) return 64;
+    if (n_segs <= 256u * all) return 256;
     return 3;
 }
 
