@@ -171,9 +171,16 @@ __global__ __launch_bounds__(256) void k_encode_scan(EncArgs a) {
 // frame and the next -- header bytes from registers, payload bytes by unaligned gathers issued
 // together; pieces meeting 3+ frames (frames shorter than 16 B) take a uniform tail loop.  Returns
 // false (nothing written) when more than 64 frames overlap the window.
+// byte masks from the 17-entry LDS prefix table (the unmask's idea, wsc_unmask.inl): the bytes
+// [lo, hi) of a 16-byte piece are pm[hi] & ~pm[lo]
+__device__ __forceinline__ void pm_mask(const u32x4* __restrict__ pm, uint32_t lo, uint32_t hi, uint32_t (&m)[4]) {
+    const u32x4 h = pm[hi], l = pm[lo];
+    m[0] = h[0] & ~l[0]; m[1] = h[1] & ~l[1]; m[2] = h[2] & ~l[2]; m[3] = h[3] & ~l[3];
+}
+
 template <int NT>
 __device__ __forceinline__ bool encode_window_lanes(const EncCopyArgs& a, uint32_t m, uint64_t wbase, uint64_t limit,
-                                                    uint32_t lane) {
+                                                    uint32_t lane, const u32x4* __restrict__ pm) {
     constexpr uint32_t P = ENC_WIN / 1024;
     constexpr int64_t WB = ENC_WIN;
     auto clip = [](int64_t x) -> int32_t { return (int32_t)(x < -(1ll << 30) ? -(1ll << 30) : (x > WB + 64 ? WB + 64 : x)); };
@@ -195,13 +202,15 @@ __device__ __forceinline__ bool encode_window_lanes(const EncCopyArgs& a, uint32
     if (nl == 64 && __shfl(re, 63) < (int32_t)WB && m + 64 < a.n_msgs) return false;
     const uint32_t so_lo = (uint32_t)so, so_hi = (uint32_t)((uint64_t)so >> 32);
 
+    // binary search: first step = the power of two with 2*st0 > nl (wave-uniform), as many steps
+    // as the window's frame count needs (3 for 1 KiB frames instead of 6)
+    const int32_t st0 = nl == 0 ? 0 : (nl >= 32 ? 32 : (int32_t)((1u << (32 - __builtin_clz(nl))) >> 1));
     int32_t ta[P];
 #pragma unroll
     for (uint32_t k = 0; k < P; ++k) {
         const int32_t pr = (int32_t)(k * 1024 + lane * 16);
         int32_t lo = -1;
-#pragma unroll
-        for (int st = 32; st >= 1; st >>= 1) {
+        for (int32_t st = st0; st >= 1; st >>= 1) {
             const int32_t c = lo + st;
             const int32_t dv = __shfl(ro, c & 63);
             if (c < (int32_t)nl && dv <= pr) lo = c;
@@ -218,14 +227,14 @@ __device__ __forceinline__ bool encode_window_lanes(const EncCopyArgs& a, uint32
         uint32_t msk[4];
         int32_t lo = fo > pr ? fo : pr, hi = fp < pr + 16 ? fp : pr + 16;
         if (lo < hi) {
-            piece_mask((uint32_t)(lo - pr), (uint32_t)(hi - pr), msk);
+            pm_mask(pm, (uint32_t)(lo - pr), (uint32_t)(hi - pr), msk);
             const uint4 t4 = and4(enc_place(hh, fo - pr), msk);
             acc.x |= t4.x; acc.y |= t4.y; acc.z |= t4.z; acc.w |= t4.w;
         }
         lo = fp > pr ? fp : pr;
         hi = fe < pr + 16 ? fe : pr + 16;
         if (lo < hi) {
-            piece_mask((uint32_t)(lo - pr), (uint32_t)(hi - pr), msk);
+            pm_mask(pm, (uint32_t)(lo - pr), (uint32_t)(hi - pr), msk);
             const int64_t sof = (int64_t)((uint64_t)sh << 32 | sl) + (int64_t)wbase + pr;
             const uint4 t4 = and4(load16_unaligned(a.src, sof, a.src_bytes), msk);
             acc.x |= t4.x; acc.y |= t4.y; acc.z |= t4.z; acc.w |= t4.w;
@@ -282,6 +291,16 @@ __device__ __forceinline__ bool encode_window_lanes(const EncCopyArgs& a, uint32
 template <int NT>
 __global__ __launch_bounds__(256) void k_encode_copy(EncCopyArgs a) {
     constexpr uint32_t P = ENC_WIN / 1024;
+    __shared__ u32x4 pm[17];
+    if (threadIdx.x < 17) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t L = threadIdx.x;
+            const uint32_t nb = L > 4u * j ? (L - 4u * j > 4u ? 4u : L - 4u * j) : 0u;
+            pm[threadIdx.x][j] = nb == 4 ? 0xFFFFFFFFu : ((1u << (8 * nb)) - 1u);
+        }
+    }
+    __syncthreads();
     // re-arm the scan's look-back state for the next encode (this launch is ordered after it)
     for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < a.n_lb; t += gridDim.x * blockDim.x) a.lb_state[t] = 0;
     const uint32_t n = a.n_msgs;
@@ -309,7 +328,7 @@ __global__ __launch_bounds__(256) void k_encode_copy(EncCopyArgs a) {
     }
     // general path: frame edges in the window -> lane-parallel frame lookup (serial walk over the
     // frames only when more than 64 of them overlap the window)
-    if (encode_window_lanes<NT>(a, m, wbase, limit, lane)) return;
+    if (encode_window_lanes<NT>(a, m, wbase, limit, lane, pm)) return;
     uint4 acc[P];
 #pragma unroll
     for (uint32_t k = 0; k < P; ++k) acc[k] = make_uint4(0, 0, 0, 0);
