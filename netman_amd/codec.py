@@ -318,7 +318,7 @@ class Codec:
         out = (C.c_double * 6)()
         _check(self.lib.wsc_profile(self.h, C.byref(batch), iters, out), "wsc_profile")
         v = list(out)
-        return {"walk": v[0], "u8": v[1], "unmask": v[3], "total": v[5]}
+        return {"walk": v[0], "unmask": v[1], "u8": v[2], "total": v[5]}
 
     # ---- encode (server -> client framing, websocket_ctrl.go:23-70) ----
     def encode(self, msgs, n_msgs: int, src, src_bytes: int, out, out_cap: int, out_off, stream=None):

@@ -19,9 +19,9 @@ template <bool COMPACT> __global__ void k_walk_count(WalkArgs);
 __global__ void k_walk_scan(WalkArgs, uint32_t);
 template <bool COMPACT> __global__ void k_walk_emit(WalkArgs);
 template <uint32_t NCH> __global__ void k_u8_check(U8Args);
-template <bool COMPACT, int P, int NT, int MINW>
+template <bool COMPACT, int P, int NT, int MINW, bool U8>
 __global__ void k_unmask(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*,
-                         const wsc_summary*, uint32_t*, uint32_t, uint32_t*, uint32_t*, uint32_t);
+                         const wsc_summary*, uint32_t*, uint32_t, uint32_t*, uint32_t*, uint32_t, U8Win);
 __global__ void k_encode_scan(EncArgs);
 template <int NT> __global__ void k_encode_copy(EncCopyArgs);
 }  // namespace wsc
@@ -82,6 +82,9 @@ struct wsc_ctx {
     uint64_t* u8maps = nullptr;
     uint32_t u8items_cap = 0;
     U8Seg* u8seg = nullptr;
+    uint32_t* win_flag = nullptr;       // per unmask window: inside a deferred text item (walk sets, unmask clears)
+    uint64_t* win_map = nullptr;        // per unmask window: the DFA map the unmask folded
+    uint32_t* u8done = nullptr;         // k_u8_check finished workgroups (self re-arming)
     uint32_t u8_inline_max = 256;
     uint32_t u8_grid = 0;               // WSC_U8_GRID: k_u8_check workgroups (A/B experiments; 0 = 5 per CU)
     int walk_mode = 0;                  // WSC_WALK_MODE: 64, 256 or 3 pins the walk geometry (A/B, tests); 0 = auto
@@ -268,11 +271,20 @@ int wsc_create(int device, const wsc_config* cfg_in, wsc_ctx** out) {
     chk(hipMalloc(&c->spans, (uint64_t)cfg.max_frames * sizeof(Span)), "hipMalloc spans");
     c->tile_entries = cfg.max_batch_bytes / 1024 + 2;
     chk(hipMalloc(&c->tile, c->tile_entries * sizeof(uint32_t)), "hipMalloc tile");
-    // every frame is at most ceil(len / U8_PIECE) items: frames + bytes / U8_PIECE bounds the total
+    // items are cut at U8_PIECE-aligned wire offsets: a frame is one item plus one per aligned
+    // boundary inside its payload, so frames + bytes / U8_PIECE + 1 bounds the total
     c->u8items_cap = cfg.max_frames + (uint32_t)(cfg.max_batch_bytes / U8_PIECE) + 64;
     chk(hipMalloc(&c->u8items, (uint64_t)c->u8items_cap * sizeof(U8Item)), "hipMalloc u8items");
     chk(hipMalloc(&c->u8maps, (uint64_t)c->u8items_cap * sizeof(uint64_t)), "hipMalloc u8maps");
     chk(hipMalloc(&c->u8seg, (uint64_t)cfg.max_segs * sizeof(U8Seg)), "hipMalloc u8seg");
+    chk(hipMalloc(&c->win_flag, c->tile_entries * sizeof(uint32_t)), "hipMalloc win_flag");
+    chk(hipMalloc(&c->win_map, c->tile_entries * sizeof(uint64_t)), "hipMalloc win_map");
+    chk(hipMalloc(&c->u8done, sizeof(uint32_t)), "hipMalloc u8done");
+    if (rc == WSC_OK) {
+        chk(hipMemsetAsync(c->win_flag, 0, c->tile_entries * sizeof(uint32_t), c->stream), "hipMemset win_flag");
+        chk(hipMemsetAsync(c->u8done, 0, sizeof(uint32_t), c->stream), "hipMemset u8done");
+        chk(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+    }
     if (const char* e = std::getenv("WSC_UNMASK_BUF"); e && *e) c->unmask_buf = std::atoi(e);
     if (const char* e = std::getenv("WSC_U8_CHAINS"); e && *e) c->u8_chains = std::atoi(e);
     if (const char* e = std::getenv("WSC_U8_GRID"); e && *e) c->u8_grid = (uint32_t)std::strtoul(e, nullptr, 10);
@@ -309,7 +321,8 @@ int wsc_destroy(wsc_ctx* c) {
     void* ptrs[] = {c->fin_ctr, c->dbg, c->sticky, c->counts, c->lb_state, c->u8info, c->lb_agg, c->lb_incl, c->spans, c->tile, c->d_wire, c->d_arena,
                     c->d_seg_off, c->d_state_in, c->d_state_out, c->d_seg_out, c->d_frames,
                     c->d_frame_dst, c->d_summary, c->enc_lb_state, c->enc_lb_agg, c->enc_lb_incl, c->enc_tile,
-                    c->d_enc_msgs, c->d_enc_src, c->d_enc_out, c->d_enc_off, c->u8items, c->u8maps, c->u8seg};
+                    c->d_enc_msgs, c->d_enc_src, c->d_enc_out, c->d_enc_off, c->u8items, c->u8maps, c->u8seg,
+                    c->win_flag, c->win_map, c->u8done};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -392,6 +405,7 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     wa.u8_inline_max = c->u8_inline_max;
     wa.sticky = c->sticky;
     wa.u8host = c->hflag;
+    wa.win_flag = c->win_flag;
 
     // walk geometry: the fused walk with blocks that fill the CUs once (64 lanes for up to 64
     // segments per CU, else 256), or -- for more segments than the chip holds lanes at once -- the
@@ -437,31 +451,11 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     c->walk_waited = false;
     if (split && !walked) HIP_TRY(hipStreamWaitEvent(st, c->ev_walked, 0));
     rec(1);
-    // deferred UTF-8 (large text): verdicts applied before the unmask.  The kernel exits at once
-    // without deferred text, but it is still a launch between two unmasks: skipped when the walk
-    // has completed and its host-visible flag says it deferred nothing.
-    if (!(walked && __atomic_load_n(&c->hflag[0], __ATOMIC_ACQUIRE) == 0)) {
-        U8Args ua{};
-        ua.wire = b->wire;
-        ua.n_bytes = b->n_bytes;
-        ua.seg_off = b->seg_off;
-        ua.items = c->u8items;
-        ua.count = c->lb_state + 2;
-        ua.maps = c->u8maps;
-        ua.seg = c->u8seg;
-        ua.frames = b->frames;
-        ua.spans = c->spans;
-        ua.seg_out = b->seg_out;
-        ua.state_out = b->state_out;
-        ua.summary = b->summary;
-        const dim3 ug(c->u8_grid ? c->u8_grid : (uint32_t)c->n_cu * 5);   // resident: 5 waves/SIMD (96 VGPRs)
-        if (c->u8_chains == 1) hipLaunchKernelGGL(k_u8_check<1>, ug, dim3(256), 0, st, ua);
-        else if (c->u8_chains == 4) hipLaunchKernelGGL(k_u8_check<4>, ug, dim3(256), 0, st, ua);
-        else hipLaunchKernelGGL(k_u8_check<2>, ug, dim3(256), 0, st, ua);
-        HIP_TRY(hipGetLastError());
-    }
-    rec(2);
-    rec(3);
+    // deferred UTF-8 (large text) runs after the unmask (which folds the text windows it unmasks):
+    // both the fold and the check are skipped when the walk has completed and its host-visible
+    // flag says it deferred nothing -- the check would still be a launch between two unmasks
+    const bool need_u8 = !(walked && __atomic_load_n(&c->hflag[0], __ATOMIC_ACQUIRE) == 0);
+    const bool signal = phase == 2;   // staged: the decode's last kernel signals the host, no ev_done
 
     uint8_t* udst = compact ? b->arena : b->wire;
     const uint64_t wb = (uint64_t)c->pieces * 1024;
@@ -472,26 +466,67 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     if (waves == 0) waves = 1;
     const dim3 ublk(256), ugrid((uint32_t)((waves + 3) / 4));
     using UK = void (*)(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*,
-                        const wsc_summary*, uint32_t*, uint32_t, uint32_t*, uint32_t*, uint32_t);
-    // [compact][pieces 4/8][nt 0..3]
-    static const UK table[2][2][4] = {
-        {{k_unmask<false, 4, 0, 1>, k_unmask<false, 4, 1, 1>, k_unmask<false, 4, 2, 1>, k_unmask<false, 4, 3, 1>},
-         {k_unmask<false, 8, 0, 1>, k_unmask<false, 8, 1, 1>, k_unmask<false, 8, 2, 1>, k_unmask<false, 8, 3, 1>}},
-        {{k_unmask<true, 4, 0, 1>, k_unmask<true, 4, 1, 1>, k_unmask<true, 4, 2, 1>, k_unmask<true, 4, 3, 1>},
-         {k_unmask<true, 8, 0, 1>, k_unmask<true, 8, 1, 1>, k_unmask<true, 8, 2, 1>, k_unmask<true, 8, 3, 1>}}};
+                        const wsc_summary*, uint32_t*, uint32_t, uint32_t*, uint32_t*, uint32_t, U8Win);
+    // [U8 fold][compact][pieces 4/8][nt 0..3]
+#define WSC_UK(C, P, N, U) k_unmask<C, P, N, 1, U>
+#define WSC_UK4(C, P, U) {WSC_UK(C, P, 0, U), WSC_UK(C, P, 1, U), WSC_UK(C, P, 2, U), WSC_UK(C, P, 3, U)}
+    static const UK table[2][2][2][4] = {
+        {{WSC_UK4(false, 4, false), WSC_UK4(false, 8, false)}, {WSC_UK4(true, 4, false), WSC_UK4(true, 8, false)}},
+        {{WSC_UK4(false, 4, true), WSC_UK4(false, 8, true)}, {WSC_UK4(true, 4, true), WSC_UK4(true, 8, true)}}};
     const int pi = c->pieces == 4 ? 0 : 1;
-    static const UK table_buf[2][3] = {
-        {k_unmask<false, 4, 35, 1>, k_unmask<false, 4, 291, 1>, k_unmask<false, 4, 307, 1>},
-        {k_unmask<false, 8, 35, 1>, k_unmask<false, 8, 291, 1>, k_unmask<false, 8, 307, 1>}};
-    UK kern = table[compact ? 1 : 0][pi][compact ? (c->cfg.unmask_nt >> 2) & 3 : c->cfg.unmask_nt & 3];
+    static const UK table_buf[2][2][3] = {
+        {{WSC_UK(false, 4, 35, false), WSC_UK(false, 4, 291, false), WSC_UK(false, 4, 307, false)},
+         {WSC_UK(false, 8, 35, false), WSC_UK(false, 8, 291, false), WSC_UK(false, 8, 307, false)}},
+        {{WSC_UK(false, 4, 35, true), WSC_UK(false, 4, 291, true), WSC_UK(false, 4, 307, true)},
+         {WSC_UK(false, 8, 35, true), WSC_UK(false, 8, 291, true), WSC_UK(false, 8, 307, true)}}};
+#undef WSC_UK4
+#undef WSC_UK
+    const int ui = need_u8 ? 1 : 0;
+    UK kern = table[ui][compact ? 1 : 0][pi][compact ? (c->cfg.unmask_nt >> 2) & 3 : c->cfg.unmask_nt & 3];
     if (!compact && (c->cfg.unmask_nt & 3) == 3 && c->unmask_buf > 0 && c->unmask_buf <= 3)
-        kern = table_buf[pi][c->unmask_buf - 1];
-    const bool signal = phase == 2;   // staged: the last workgroup signals the host, no ev_done
+        kern = table_buf[ui][pi][c->unmask_buf - 1];
+    const bool sig_unmask = signal && !need_u8;
+    U8Win uw{};
+    if (need_u8) {
+        uw.flag = c->win_flag;
+        uw.map = c->win_map;
+        uw.count = c->lb_state + 2;
+    }
     hipLaunchKernelGGL(kern, ugrid, ublk, 0, st, udst, (const uint8_t*)b->wire, b->n_bytes, b->n_bytes,
                        (const Span*)c->spans, (const uint32_t*)c->tile, (const wsc_summary*)b->summary,
-                       c->lb_state, mode == 3 ? 1u : wgrid.x + 1,   // re-arms ticket, timeout, item count, flags
-                       signal ? c->fin_ctr : nullptr, signal ? c->hflag + 1 : nullptr, c->fin_seq + 1);
+                       c->lb_state, mode == 3 ? 1u : wgrid.x + 1,   // re-arms ticket, timeout, flags
+                       sig_unmask ? c->fin_ctr : nullptr, sig_unmask ? c->hflag + 1 : nullptr, c->fin_seq + 1, uw);
     HIP_TRY(hipGetLastError());
+    rec(2);
+    if (need_u8) {
+        U8Args ua{};
+        ua.wire = b->wire;
+        ua.n_bytes = b->n_bytes;
+        ua.seg_off = b->seg_off;
+        ua.items = c->u8items;
+        ua.count = c->lb_state + 2;
+        ua.items_cap = c->u8items_cap;
+        ua.maps = c->u8maps;
+        ua.seg = c->u8seg;
+        ua.frames = b->frames;
+        ua.spans = c->spans;
+        ua.seg_out = b->seg_out;
+        ua.state_out = b->state_out;
+        ua.summary = b->summary;
+        ua.win_map = c->win_map;
+        ua.win_shift = ilog2(c->pieces * 1024);
+        ua.unmasked = compact ? 0u : 1u;
+        ua.out = udst;
+        ua.done = c->u8done;
+        ua.fin_host = signal ? c->hflag + 1 : nullptr;
+        ua.fin_seq = c->fin_seq + 1;
+        const dim3 ug(c->u8_grid ? c->u8_grid : (uint32_t)c->n_cu * 5);   // resident: 5 waves/SIMD (96 VGPRs)
+        if (c->u8_chains == 1) hipLaunchKernelGGL(k_u8_check<1>, ug, dim3(256), 0, st, ua);
+        else if (c->u8_chains == 4) hipLaunchKernelGGL(k_u8_check<4>, ug, dim3(256), 0, st, ua);
+        else hipLaunchKernelGGL(k_u8_check<2>, ug, dim3(256), 0, st, ua);
+        HIP_TRY(hipGetLastError());
+    }
+    rec(3);
     rec(4);
     if (signal) {
         ++c->fin_seq;

@@ -10,6 +10,7 @@
 //   pass on the still-masked wire, so a connection whose text is invalid stops at that frame.
 #include "wsc_kernels.hpp"
 #include "wsc_dev.hpp"
+#include "wsc_u8.hpp"
 
 namespace wsc {
 
@@ -17,6 +18,10 @@ namespace wsc {
 // ---------------------------------------------------------------------------------------------
 // Header walk
 // ---------------------------------------------------------------------------------------------
+
+__device__ __forceinline__ uint32_t lane_id() {
+    return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+}
 
 // close-code validity, websocket_ctrl.go:160-177 (+ reservedCode, websocket.go:31)
 __device__ __forceinline__ bool close_code_ok(uint32_t code) {
@@ -30,32 +35,8 @@ __device__ __forceinline__ bool close_code_ok(uint32_t code) {
 // writes frame records, payload spans, the window->span index and the segment's results at the
 // output offsets `base` (exclusive prefix over segments) for its counts `own` (pass 1 result).
 // COMPACT arena layout per segment: [data payloads][control payloads] at base.bytes0+base.bytes1.
-// ---------------------------------------------------------------------------------------------
-// UTF-8 (Go utf8.Valid semantics): a 9-state DFA, state 0 = between characters, 8 = reject.
-// ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t u8_step(uint32_t s, uint32_t b) {
-    switch (s) {
-    case 0:
-        if (b < 0x80) return 0;
-        if (b >= 0xC2 && b <= 0xDF) return 1;
-        if (b == 0xE0) return 4;
-        if (b == 0xED) return 5;
-        if (b >= 0xE1 && b <= 0xEF) return 2;
-        if (b == 0xF0) return 6;
-        if (b >= 0xF1 && b <= 0xF3) return 3;
-        if (b == 0xF4) return 7;
-        return 8;
-    case 1: return (b >= 0x80 && b <= 0xBF) ? 0 : 8;
-    case 2: return (b >= 0x80 && b <= 0xBF) ? 1 : 8;
-    case 3: return (b >= 0x80 && b <= 0xBF) ? 2 : 8;
-    case 4: return (b >= 0xA0 && b <= 0xBF) ? 1 : 8;
-    case 5: return (b >= 0x80 && b <= 0x9F) ? 1 : 8;
-    case 6: return (b >= 0x90 && b <= 0xBF) ? 2 : 8;
-    case 7: return (b >= 0x80 && b <= 0x8F) ? 2 : 8;
-    default: return 8;
-    }
-}
-
+// UTF-8 (Go utf8.Valid semantics): a 9-state DFA, state 0 = between characters, 8 = reject
+// (u8_step, wsc_u8.hpp).
 // Run the DFA over n payload bytes that are still MASKED on the wire: byte i of the payload is
 // w[p + i] ^ (mask >> 8*(i & 3)).  4-byte ASCII groups are skipped while between characters.
 __device__ __attribute__((noinline)) uint32_t u8_run_masked(uint32_t s, const uint8_t* __restrict__ w, uint64_t p, uint64_t n,
@@ -259,6 +240,7 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
     uint32_t u8dfa = cont ? st.cont_utf8 : 0u;
     bool u8_pending = false;                      // a text chain has a deferred (chip-wide) part
     uint32_t u8_head = 0xFFFFFFFFu, u8_last = 0xFFFFFFFFu, u8_n = 0;
+    bool u8_comp = false;                         // an item whose verdict needs the segment's composition
     if constexpr (EMIT) {
         u8fail = a.u8info[2 * s];
         u8dfa = a.u8info[2 * s + 1];
@@ -444,21 +426,29 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
                     // which also applies the verdict; the walk goes on as if it were valid
                     const uint8_t kind = part ? U8K_PART : (chain ? U8K_CHAIN : U8K_SELF);
                     const uint8_t s_in = (part || chain) ? (u8_pending ? 0xFF : (uint8_t)u8dfa) : 0;
-                    const uint32_t pieces = n ? (uint32_t)((n + U8_PIECE - 1) / U8_PIECE) : 1u;
+                    // a payload up to U8_PIECE is one piece; longer ones are cut at absolute
+                    // U8_PIECE-aligned wire offsets.  Either way every unmask window that lies
+                    // inside a text payload lies inside one item (its map is folded by the unmask
+                    // that has just unmasked it, win_flag / win_map)
+                    const uint32_t pieces = n <= U8_PIECE ? 1u : (uint32_t)((src + n - 1) / U8_PIECE - src / U8_PIECE + 1);
                     // wave-aggregated allocation when every active lane takes one item (text frames
                     // <= 16 KiB): one atomic per wave instead of one per frame (262 k same-address
                     // atomics: the 1 KiB TEXT walk 97 -> 74.5 us with aggregation)
+                    // (the rank counts the lanes below plus those of them that take two pieces)
                     uint32_t b0;
                     {
                         const uint64_t act = __ballot(true);
-                        if (__ballot(pieces != 1) == 0) {
+                        if (__ballot(pieces > 2) == 0) {
+                            const uint64_t two = __ballot(pieces == 2);
                             const uint32_t leader = (uint32_t)__builtin_ctzll(act);
-                            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32),
-                                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
+                            const uint32_t rank =
+                                __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u)) +
+                                __builtin_amdgcn_mbcnt_hi((uint32_t)(two >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)two, 0u));
                             uint32_t base = 0;
-                            if (rank == 0)
-                                base = __hip_atomic_fetch_add(a.u8count, (uint32_t)__builtin_popcountll(act), __ATOMIC_RELAXED,
-                                                              __HIP_MEMORY_SCOPE_AGENT);
+                            if (lane_id() == leader)
+                                base = __hip_atomic_fetch_add(a.u8count,
+                                                              (uint32_t)(__builtin_popcountll(act) + __builtin_popcountll(two)),
+                                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                             b0 = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)leader) + rank;
                         } else {
                             b0 = __hip_atomic_fetch_add(a.u8count, pieces, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -468,13 +458,22 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
                         __hip_atomic_store(a.u8host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                         __threadfence_system();
                     }
-                    for (uint32_t p = 0; p < pieces; ++p) {   // capacity covers every frame + bytes / U8_PIECE
+                    // capacity: frames + wire bytes / U8_PIECE + 1 (each aligned boundary inside a
+                    // payload adds one piece)
+                    const uint64_t W = 1ull << a.win_shift;
+                    for (uint32_t p = 0; p < pieces; ++p) {
                         const uint32_t idx = b0 + p;
                         U8Item it;
-                        it.src = src + (uint64_t)p * U8_PIECE;
-                        const uint64_t rem = n - (uint64_t)p * U8_PIECE;
-                        it.len = (uint32_t)(rem < U8_PIECE ? rem : U8_PIECE);
-                        it.mask = mk;
+                        const uint64_t ps = p == 0 ? src : (src / U8_PIECE + p) * U8_PIECE;
+                        const uint64_t pe0 = pieces == 1 ? src + n : (src / U8_PIECE + p + 1) * U8_PIECE;
+                        const uint64_t pe = pe0 < src + n ? pe0 : src + n;
+                        it.src = ps;
+                        it.len = (uint32_t)(pe - ps);
+                        it.mask = rotr32(mk, 8u * (uint32_t)((ps - src) & 3));   // phase 0 at the piece
+                        if (a.win_flag) {   // windows inside the piece: folded by the unmask
+                            for (uint64_t wi = (ps + W - 1) >> a.win_shift; ((wi + 1) << a.win_shift) <= pe; ++wi)
+                                a.win_flag[wi] = 1u;
+                        }
                         it.seg = s;
                         it.ordinal = nf;
                         it.next = 0xFFFFFFFFu;
@@ -490,6 +489,7 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
                             u8_n += 1;
                         }
                     }
+                    if (part || chain || pieces != 1) u8_comp = true;
                     if (part) u8_pending = true;
                     if (chain) u8_pending = false;   // the message completes here
                 } else {
@@ -621,7 +621,8 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
             g.head = u8_head;
             g.n = u8_n;
             g.done = 0;
-            g.pending_end = u8_pending ? 1u : 0u;
+            g.pending_end = (u8_pending ? 1u : 0u) | (u8_comp ? 2u : 0u);
+            g.minfail = 0xFFFFFFFFu;
             a.u8seg[s] = g;
             c.flags |= SEGF_U8DEFER;
         }
@@ -777,7 +778,9 @@ __global__ __launch_bounds__(256) void k_walk_scan(WalkArgs a, uint32_t n_blocks
         sm.data_bytes = tt.bytes0;
         sm.ctrl_bytes = tt.bytes1;
         sm.n_frames = tt.frames;
-        sm.n_spans = tt.spans0 + tt.spans1;
+        // spans past the capacity were never written: the unmask must not read them (an overflowed
+        // batch unmasks the spans that fit; n_spans = spans unmasked)
+        sm.n_spans = tt.spans0 + tt.spans1 < a.spans_cap ? tt.spans0 + tt.spans1 : a.spans_cap;
         sm.overflow = (tt.frames > a.frames_cap || tt.spans0 + tt.spans1 > a.spans_cap) ? 1u : 0u;
         sm.pad = 0;
         *a.summary = sm;
@@ -1106,7 +1109,9 @@ __global__ __launch_bounds__(NT) void k_walk_fused(WalkArgs a) {
         sm.data_bytes = COMPACT ? tt.bytes0 : 0;
         sm.ctrl_bytes = COMPACT ? tt.bytes1 : 0;
         sm.n_frames = tt.frames;
-        sm.n_spans = tt.spans0 + tt.spans1;
+        // spans past the capacity were never written: the unmask must not read them (an overflowed
+        // batch unmasks the spans that fit; n_spans = spans unmasked)
+        sm.n_spans = tt.spans0 + tt.spans1 < a.spans_cap ? tt.spans0 + tt.spans1 : a.spans_cap;
         sm.overflow = (tt.frames > a.frames_cap || tt.spans0 + tt.spans1 > a.spans_cap) ? 1u : 0u;
         if (__hip_atomic_load(a.lb_err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) sm.overflow |= 2u;
         sm.pad = 0;
@@ -1117,59 +1122,44 @@ __global__ __launch_bounds__(NT) void k_walk_fused(WalkArgs a) {
 
 // ---------------------------------------------------------------------------------------------
 // Chip-wide UTF-8 (utf8.Valid, websocket_frame.go:71-73, websocket.go:170-172) for the text the
-// walk deferred.  A UTF-8 check is a 9-state DFA; what a run of bytes does to it is a map from
-// start state to end state (9 x 4 bits).  Each lane computes the map of its 16 bytes, a wave
-// composes 64 lanes' maps in order (shuffle tree), items are composed step by step.  Per item the
-// map is published (agent-scope store, drained, then an agent-scope counter); the wave that
-// completes a segment's last item composes the segment's items in frame order with the states the
-// walk recorded and applies the verdict: the first failing frame becomes WSC_FK_ERROR / 1007, the
-// segment stops there, and the spans of later frames get key 0 so the unmask leaves them as the
-// reference would (never read).  Runs between the walk and the unmask; exits at once when the
-// walk deferred nothing.
+// walk deferred.  Runs AFTER the unmask, which has folded the map of every unmask window lying
+// inside an item (win_map): this kernel reads only the items' partial windows at their ends, folds
+// them (each lane one 64-byte chunk, waves compose lanes), composes head, window maps and tail per
+// item and publishes the item's map (agent-scope store, drained, then an agent-scope counter); the
+// wave that completes a segment's last item composes the segment's items in frame order with the
+// states the walk recorded and applies the verdict: the first failing frame becomes WSC_FK_ERROR /
+// 1007, the segment stops there, and the spans of later frames -- already unmasked -- are XORed
+// again, so the bytes are left as the reference leaves them (never read).  Maps: wsc_u8.hpp.
 // ---------------------------------------------------------------------------------------------
-// A map is 8 bytes: byte s = the state after the bytes when entering in state s (0..7), 0xFF =
-// reject; the reject state itself is absorbing and not stored.  With this encoding a map is a
-// v_perm_b32 table: applying map b after map a is two v_perm_b32 (a's bytes select from b; 0xFF
-// selects 0xFF), and one input byte is one 8-byte table row T[byte] from LDS.
-__device__ __forceinline__ uint64_t u8m_id() { return 0x0706050403020100ull; }
-__device__ __forceinline__ uint64_t u8m_ascii() { return 0xFFFFFFFFFFFFFF00ull; }   // 0 -> 0, mid-character -> reject
-__device__ __forceinline__ uint64_t u8m_then(uint64_t a, uint64_t b) {   // a, then b
-    const uint32_t bl = (uint32_t)b, bh = (uint32_t)(b >> 32);
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_perm(bh, bl, (uint32_t)a);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_perm(bh, bl, (uint32_t)(a >> 32));
-    return (uint64_t)hi << 32 | lo;
-}
-// one level of the in-row composition: lanes that are multiples of 2*DD take "own map, then the map
-// of lane + DD" (DPP row_shl:DD -- lane i reads lane i + DD of its 16-lane row)
-template <int DD>
-__device__ __forceinline__ void u8m_row_level(uint32_t& mlo, uint32_t& mhi, uint32_t lane) {
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mlo, 0x100 | DD, 0xF, 0xF, false);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mhi, 0x100 | DD, 0xF, 0xF, false);
-    if ((lane & (2 * DD - 1)) == 0) {
-        const uint64_t c = u8m_then((uint64_t)mhi << 32 | mlo, (uint64_t)hi << 32 | lo);
-        mlo = (uint32_t)c;
-        mhi = (uint32_t)(c >> 32);
-    }
-}
-__device__ __forceinline__ uint32_t u8m_get(uint64_t m, uint32_t st) {   // st: 0..7, or >= 8 = reject
-    return st > 7 ? 0xFFu : (uint32_t)(m >> (8 * st)) & 0xFFu;
-}
 
 // Publish one item's map; the segment's last item composes the segment's items in frame order
-// with the walk's states and applies the verdict (one lane).
-__device__ __forceinline__ void u8_finish(const U8Args& a, uint32_t it, uint32_t seg, uint64_t acc) {
+// with the walk's states and applies the verdict (one lane).  Returns the wire end of the failing
+// frame when this call applied a failure verdict (the wave then re-masks the later spans), else ~0.
+__device__ __forceinline__ uint64_t u8_finish(const U8Args& a, uint32_t it, uint32_t seg, uint64_t acc, bool ovf) {
     const uint32_t n = a.seg[seg].n;   // (static: loaded beside the map store, not after the count)
-    __hip_atomic_store(a.maps + it, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const U8Item self = a.items[it];
+    // a whole TEXT message in one piece (SELF, first and last) needs no composition: its verdict
+    // is its own map from state 0, folded into the segment's first failing ordinal
+    if (self.kind == U8K_SELF && self.first && self.last) {
+        if (u8m_get(acc, 0) != 0)
+            __hip_atomic_fetch_min(&a.seg[seg].minfail, self.ordinal, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        __hip_atomic_store(a.maps + it, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const uint32_t done = __hip_atomic_fetch_add(&a.seg[seg].done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
-    if (done != n) return;
+    if (done != n) return ~0ull;
     const U8Seg g = a.seg[seg];
-    // the segment's last item: compose its items in frame order with the walk's states
-    uint32_t cur = 0, start = 0, fail = 0xFFFFFFFFu;   // states 0..7, 0xFF = reject
+    uint32_t cur = 0, start = 0;   // states 0..7, 0xFF = reject
+    uint32_t fail = __hip_atomic_fetch_add(&a.seg[seg].minfail, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // the segment's last item: compose its composite items in frame order with the walk's states
+    // (single-piece SELF items were decided above; a chain never has one inside it)
     uint64_t fm = u8m_id();
-    uint32_t j = g.head;
+    uint32_t j = (g.pending_end & 2u) ? g.head : 0xFFFFFFFFu;
     for (uint32_t c = 0; c < g.n && j != 0xFFFFFFFFu; ++c) {
         const U8Item x = a.items[j];
+        if (x.ordinal >= fail) break;   // a single-piece SELF frame failed first
+        if (x.kind == U8K_SELF && x.first && x.last) { j = x.next; continue; }
         const uint64_t m = __hip_atomic_fetch_add(a.maps + j, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (x.first) {
             start = x.kind == U8K_SELF ? 0u : (x.s_in != 0xFF ? (x.s_in > 7 ? 0xFFu : (uint32_t)x.s_in) : cur);
@@ -1181,16 +1171,17 @@ __device__ __forceinline__ void u8_finish(const U8Args& a, uint32_t it, uint32_t
             if (x.kind == U8K_PART) {
                 cur = end;
             } else {
-                if (end != 0) { fail = x.ordinal; break; }
+                if (end != 0) { fail = x.ordinal; break; }   // (ordinal < fail: checked above)
                 if (x.kind == U8K_CHAIN) cur = 0;
             }
         }
         j = x.next;
     }
     const uint32_t s = seg;
+    if (ovf) return ~0ull;
     if (fail == 0xFFFFFFFFu) {
-        if (g.pending_end && a.state_out[s].cont_len) a.state_out[s].cont_utf8 = (uint8_t)(cur > 7 ? 8u : cur);
-        return;
+        if ((g.pending_end & 1u) && a.state_out[s].cont_len) a.state_out[s].cont_utf8 = (uint8_t)(cur > 7 ? 8u : cur);
+        return ~0ull;
     }
     // frame `fail` fails: CloseCode(1007) there (epoll.go:126-127), nothing after it is read
     wsc_frame* f = a.frames + g.fbase + fail;
@@ -1205,188 +1196,113 @@ __device__ __forceinline__ void u8_finish(const U8Args& a, uint32_t it, uint32_t
     r.err = WSC_ERR_MUST_UTF8;
     a.seg_out[s] = r;
     a.state_out[s].status = WSC_SEG_ERROR;
-    for (uint32_t k = 0; k < g.nspans; ++k)   // later frames stay masked (the reference never reads them)
-        if (a.spans[g.sbase + k].src >= fend) a.spans[g.sbase + k].key = 0;
+    return fend;
+}
+
+// The segment's spans that start at or after `fend` were unmasked although the reference never
+// reads them: XOR them again, the whole wave 16 B per lane (1 KiB per step).  The key is phased at
+// the wire (byte x takes key byte x & 3), in place and in the arena alike.
+__device__ __forceinline__ void u8_remask(const U8Args& a, uint32_t seg, uint64_t fend, uint32_t lane) {
+    const U8Seg g = a.seg[seg];
+    for (uint32_t k = 0; k < g.nspans; ++k) {
+        const Span sp = a.spans[g.sbase + k];
+        if (sp.src < fend) continue;
+        uint8_t* d = a.out + sp.dst;
+        for (uint32_t i = lane * 16u; i < sp.len; i += 1024u) {
+            const uint32_t key = rotr32(sp.key, 8u * (uint32_t)((sp.src + i) & 3));
+            if (sp.len - i >= 16) {
+                u32x4u* p = reinterpret_cast<u32x4u*>(d + i);
+                const u32x4u v = *p;
+                *p = u32x4u{v.x ^ key, v.y ^ key, v.z ^ key, v.w ^ key};
+            } else {
+                for (uint32_t j = 0; i + j < sp.len; ++j) d[i + j] ^= (uint8_t)(key >> (8 * (j & 3)));
+            }
+        }
+    }
 }
 
 // 5 waves per SIMD (96 VGPRs).  Each lane folds a 64-byte chunk (4 x 16 B loads) into one map, so
 // the wave-level composition (DPP row levels + 4 readlanes) is paid once per 64 bytes instead of
 // per 16: PMC showed the 16-byte-piece version at 12.5 VALU per text byte, VALU-bound (77 % of
-// the chip's VALU cycles).  Inside a chunk the first 4 bytes compose full maps (two v_perm per
-// byte from the 8-byte rows of `tab`); every entry state that survives them is then in one state
-// X (see chunk_map), which steps through the other 60 bytes one byte-table read each
-// (`tab8[X][byte]`, state 8 = reject, absorbing): two VALU ops and one LDS read per byte.
+// the chip's VALU cycles).
 template <uint32_t NCH>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_u8_check(U8Args a) {
-    const uint32_t n_items = *a.count;
-    if (blockIdx.x * 4 >= n_items) return;   // nothing deferred (the common, binary case)
-    __shared__ uint64_t tab[256];            // T[byte]: the map of that single byte
-    __shared__ uint8_t tab8[9 * 256];        // [state][byte] -> next state (8 = reject)
-    {
-        const uint32_t byte = threadIdx.x;
-        uint64_t t = 0;
-        for (uint32_t st = 0; st < 8; ++st) {
-            const uint32_t ns = u8_step(st, byte);
-            t |= (uint64_t)(ns == 8 ? 0xFFu : ns) << (8 * st);
-            tab8[st * 256 + byte] = (uint8_t)ns;
-        }
-        tab8[8 * 256 + byte] = 8;
-        tab[byte] = t;
-    }
-    __syncthreads();
+    // (items past the capacity were dropped by the walk: only a batch whose records overflowed
+    // allocates that many, and its verdicts are skipped below)
+    const uint32_t n_items = *a.count < a.items_cap ? *a.count : a.items_cap;
+    // a batch whose records overflowed is invalid as a whole (the caller re-decodes it): its
+    // verdicts are not applied -- the failing frame or its later spans may lie past the capacity
+    const bool ovf = a.summary->overflow != 0;
+    __shared__ U8Lds T;
+    __shared__ uint4 stage[4][U8_STAGE];
     const uint32_t lane = threadIdx.x & 63;
+    if (blockIdx.x * 4 < n_items) {   // (nothing deferred: the workgroup only counts itself done)
+    u8_tables_init(T, threadIdx.x);
+    __syncthreads();
     const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
     const uint32_t nw = gridDim.x * 4;
     // Global loads stay coalesced (piece k of a step: 16 B per lane at base_k + 16 * lane, 1 KiB
-    // per instruction); a per-wave LDS stage turns them into one contiguous 64-byte chunk per lane
-    // (chunks padded to 80 B: the 16 lanes of a ds_read_b128 phase then hit 16 distinct bank
-    // groups).  Strided 16-byte global loads at a 64-byte lane stride measured slower.
-    __shared__ uint4 stage[4][64 * 5];
+    // per instruction); a per-wave LDS stage turns them into one contiguous 64-byte chunk per lane.
+    // Strided 16-byte global loads at a 64-byte lane stride measured slower.
     uint4* const sw = stage[threadIdx.x >> 6];
-    auto restage = [&](uint4 (&q)[4]) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t b = 1024u * k + 16u * lane;
-            sw[(b >> 6) * 5 + ((b >> 4) & 3)] = q[k];
-        }
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (int k = 0; k < 4; ++k) q[k] = sw[lane * 5 + k];
-        __builtin_amdgcn_wave_barrier();
-    };
-    // The map of one lane's 64-byte chunk (nk valid bytes, masked with `mask`); plain = no
-    // non-ASCII byte among them.
-    auto chunk_map = [&](const uint4 (&v)[4], uint32_t mask, uint32_t nk, bool& plain) -> uint64_t {
-        // byte i of the chunk, unmasked (i constant after unrolling)
-        auto dw = [&](uint32_t j) -> uint32_t {
-            const uint4& q = v[j >> 2];
-            const uint32_t w = (j & 3) == 0 ? q.x : (j & 3) == 1 ? q.y : (j & 3) == 2 ? q.z : q.w;
-            return w ^ mask;
-        };
-        uint32_t hib = 0;
-        if (nk >= 64) {
-#pragma unroll
-            for (uint32_t j = 0; j < 16; ++j) hib |= dw(j);
-            hib &= 0x80808080u;
+    const uint64_t W = 1ull << a.win_shift;
+    constexpr uint32_t NONE = 0xFFFFFFFFu;
+    // An item reads its head [0, hl) and tail [tb, len); the unmask windows between them
+    // (w0 .. w0 + nwin - 1) were folded by the unmask.  An item without a whole window is all head.
+    struct Geo { uint32_t hl, tb, nwin; uint64_t w0; };
+    auto geo = [&](const U8Item& x) -> Geo {
+        const uint64_t s = x.src, e = s + x.len;
+        const uint64_t A = (s + W - 1) & ~(W - 1), B = e & ~(W - 1);
+        Geo g;
+        if (A < B) {
+            g.hl = (uint32_t)(A - s);
+            g.tb = (uint32_t)(B - s);
+            g.w0 = A >> a.win_shift;
+            g.nwin = (uint32_t)((B - A) >> a.win_shift);
         } else {
-#pragma unroll
-            for (uint32_t j = 0; j < 16; ++j) {
-                const uint32_t lim = nk > 4u * j ? (nk - 4u * j >= 4 ? 4u : nk - 4u * j) : 0u;
-                const uint32_t keep = lim >= 4 ? 0xFFFFFFFFu : ((1u << (8 * lim)) - 1u);
-                hib |= dw(j) & keep & 0x80808080u;
-            }
+            g.hl = x.len;
+            g.tb = x.len;
+            g.w0 = 0;
+            g.nwin = 0;
         }
-        plain = true;
-        if (nk == 0) return u8m_id();
-        if (hib == 0) return u8m_ascii();
-        plain = false;
-        // Every entry state that survives the first 4 bytes is in ONE state X there: a survivor
-        // must be in state 0 just before the first lead byte (a lead in a non-zero state rejects),
-        // and 4 continuation bytes reject every state (at most 3 are owed).  So the first 4 bytes
-        // compose full maps, the others step the single state X, and the chunk's map is the
-        // prefix map with every surviving entry sent to the final state.  A partial chunk (the
-        // last of an item) folds its bytes with full maps instead: its map must leave a
-        // character that the item ends inside owed, not rejected by padding.
-        uint32_t lo = 0x03020100u, hi = 0x07060504u;
-        if (nk < 64) {   // (unrolled with a guard: a dynamic index into the chunk would go to scratch)
-#pragma unroll
-            for (uint32_t i = 0; i < 64; ++i) {
-                if (i < nk) {
-                    const uint64_t t = tab[(dw(i >> 2) >> (8 * (i & 3))) & 0xFFu];
-                    const uint32_t tl = (uint32_t)t, th = (uint32_t)(t >> 32);
-                    lo = (uint32_t)__builtin_amdgcn_perm(th, tl, lo);
-                    hi = (uint32_t)__builtin_amdgcn_perm(th, tl, hi);
-                }
-            }
-            return (uint64_t)hi << 32 | lo;
-        }
-        // NCH independent chains of 64 / NCH bytes, interleaved byte by byte (latency: each chain
-        // is a dependent sequence of LDS reads), composed in order at the end
-        constexpr uint32_t CW = 16 / NCH;     // dwords per chain
-        uint32_t clo[NCH], chi[NCH], st[NCH];
-#pragma unroll
-        for (uint32_t c = 0; c < NCH; ++c) {
-            const uint32_t d0 = dw(c * CW);
-            uint32_t l = 0x03020100u, h = 0x07060504u;
-#pragma unroll
-            for (uint32_t i = 0; i < 4; ++i) {
-                const uint64_t t = tab[(d0 >> (8 * i)) & 0xFFu];
-                const uint32_t tl = (uint32_t)t, th = (uint32_t)(t >> 32);
-                l = (uint32_t)__builtin_amdgcn_perm(th, tl, l);
-                h = (uint32_t)__builtin_amdgcn_perm(th, tl, h);
-            }
-            uint32_t x = l & h;             // non-rejected bytes all equal X, rejects are 0xFF
-            x &= x >> 16;
-            x &= x >> 8;
-            x &= 0xFFu;
-            st[c] = x > 7 ? 8u : x;
-            clo[c] = l;
-            chi[c] = h;
-        }
-        // one v_perm per byte builds the table index st << 8 | byte (and, depending on st, keeps
-        // the compiler from hoisting the byte extractions into live registers)
-#pragma unroll
-        for (uint32_t j = 1; j < CW; ++j) {
-#pragma unroll
-            for (uint32_t i = 0; i < 4; ++i) {
-#pragma unroll
-                for (uint32_t c = 0; c < NCH; ++c)
-                    st[c] = tab8[__builtin_amdgcn_perm(st[c], dw(c * CW + j), i | 4u << 8 | 0x0Cu << 16 | 0x0Cu << 24)];
-            }
-        }
-        uint64_t m = u8m_id();
-#pragma unroll
-        for (uint32_t c = 0; c < NCH; ++c) {
-            const uint32_t fr = (st[c] > 7 ? 0xFFu : st[c]) * 0x01010101u;
-            const uint32_t l = (uint32_t)__builtin_amdgcn_perm(fr, fr, clo[c]);   // 0..7 -> final state
-            const uint32_t h = (uint32_t)__builtin_amdgcn_perm(fr, fr, chi[c]);
-            m = c == 0 ? ((uint64_t)h << 32 | l) : u8m_then(m, (uint64_t)h << 32 | l);
-        }
-        return m;
+        return g;
     };
-    // The 16-lane rows' maps in lane order (DPP row shifts), left in lanes 0, 16, 32, 48.
-    auto row_maps = [&](uint64_t pm) -> uint64_t {
-        uint32_t mlo = (uint32_t)pm, mhi = (uint32_t)(pm >> 32);
-        u8m_row_level<1>(mlo, mhi, lane);
-        u8m_row_level<2>(mlo, mhi, lane);
-        u8m_row_level<4>(mlo, mhi, lane);
-        u8m_row_level<8>(mlo, mhi, lane);
-        return (uint64_t)mhi << 32 | mlo;
+    auto first_step = [&](const Geo& g, uint32_t len) -> uint32_t { return g.hl ? 0u : (g.tb < len ? g.tb : NONE); };
+    auto next_step = [&](const Geo& g, uint32_t len, uint32_t b0) -> uint32_t {
+        if (b0 < g.hl) return b0 + 4096 < g.hl ? b0 + 4096 : (g.tb < len ? g.tb : NONE);
+        return b0 + 4096 < len ? b0 + 4096 : NONE;
     };
-    // The map of a 4 KiB wave step (the 64 lanes' chunk maps in lane order), wave-uniform.
-    auto wave_map = [&](uint64_t pm, bool plain) -> uint64_t {
-        if (__ballot(!plain) == 0)            // ASCII (or empty) everywhere: one constant map
-            return __ballot(pm == u8m_ascii()) ? u8m_ascii() : u8m_id();
-        const uint64_t rm = row_maps(pm);
-        const uint32_t mlo = (uint32_t)rm, mhi = (uint32_t)(rm >> 32);
-        uint64_t m = u8m_id();
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            // readlane returns int: widen through uint32_t (no sign extension into the high word)
-            const uint32_t rlo = (uint32_t)__builtin_amdgcn_readlane(mlo, 16 * r);
-            const uint32_t rhi = (uint32_t)__builtin_amdgcn_readlane(mhi, 16 * r);
-            m = u8m_then(m, (uint64_t)rhi << 32 | rlo);
-        }
-        return m;
+    // the step's mask: phase 0 at item offset b0 (in place the wire is already unmasked)
+    auto mask_at = [&](const U8Item& x, uint32_t b0) -> uint32_t {
+        return a.unmasked ? 0u : rotr32(x.mask, 8u * (b0 & 3));
     };
-    // a 4 KiB step of item x at item offset b0, coalesced (bytes past the item read as 0)
-    auto fetch = [&](const U8Item& x, uint32_t b0, uint4 (&q)[4]) {
+    // a 4 KiB step of item x at item offset b0, bytes [b0, lim) (coalesced; others read as 0)
+    auto fetch = [&](const U8Item& x, uint32_t b0, uint32_t lim, u32x4 (&q)[4]) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const uint32_t o = b0 + 1024u * k + 16u * lane;
-            q[k] = o < x.len ? load16_unaligned(a.wire, (int64_t)(x.src + o), a.n_bytes) : make_uint4(0, 0, 0, 0);
+            const uint4 t = o < lim ? load16_unaligned(a.wire, (int64_t)(x.src + o), a.n_bytes) : make_uint4(0, 0, 0, 0);
+            q[k] = u32x4{t.x, t.y, t.z, t.w};
         }
     };
     auto chunk_len = [](uint32_t len, uint32_t off) -> uint32_t {
         return off < len ? (len - off >= 64 ? 64u : len - off) : 0u;
     };
+    // the failing segments' later spans, re-masked by the whole wave
+    auto remask_wave = [&](uint64_t fe, uint32_t fs) {
+        uint64_t pend = __ballot(fe != ~0ull);
+        while (pend) {
+            const uint32_t l = (uint32_t)__builtin_ctzll(pend);
+            pend &= pend - 1;
+            const uint32_t seg = (uint32_t)__builtin_amdgcn_readlane((int)fs, (int)l);
+            const uint64_t fend = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(fe >> 32), (int)l) << 32 |
+                                  (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)fe, (int)l);
+            u8_remask(a, seg, fend, lane);
+        }
+    };
     // A unit is 4 consecutive items.  Units of small items (<= 1 KiB each: 1 KiB text frames) take
     // one step: row r (16 lanes x 64 B) holds item r, and lanes 0, 16, 32, 48 publish the 4 items'
-    // maps.  Other units walk their items' 4 KiB steps in order, the next step's loads -- the next
-    // item's first step too -- issued before the current step is folded.
-    // A unit is 4 consecutive items.  Units of small items (<= 1 KiB each: 1 KiB text frames) take
-    // one step: row r (16 lanes x 64 B) holds item r, and lanes 0, 16, 32, 48 publish the 4 items'
-    // maps.  Other units walk their items' 4 KiB steps in order, the next step's loads -- the next
+    // maps.  Other units walk their items' steps in order, the next step's loads -- the next
     // item's first step too -- issued before the current step is folded.  (A ticket counter for
     // dynamic balance measured far slower: 64 k same-address atomics; a second pass striding big
     // items one by one paid a scan of every unit's lengths per wave.)
@@ -1398,48 +1314,92 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
         for (uint32_t j = 0; j < cnt; ++j) small = small && a.items[i0 + j].len <= 1024;
         if (small) {
             // piece k of the step = item k's KiB (16 B per lane, coalesced), restaged so that row r
-            // (lanes 16r..16r+15) holds item r in 64-byte chunks
+            // (lanes 16r..16r+15) holds item r in 64-byte chunks (items <= 1 KiB hold no window)
             const uint32_t r = lane >> 4;
             U8Item xr;   // (issued before the data loads: its latency overlaps theirs)
             if (r < cnt) xr = a.items[i0 + r];
             else { xr = a.items[i0]; xr.len = 0; }
-            uint4 q[4];
+            u32x4 q[4];
 #pragma unroll
             for (uint32_t k = 0; k < 4; ++k) {
                 const U8Item xk = a.items[i0 + (k < cnt ? k : 0u)];
                 const uint32_t len = k < cnt ? xk.len : 0u;
-                q[k] = 16u * lane < len ? load16_unaligned(a.wire, (int64_t)(xk.src + 16u * lane), a.n_bytes)
-                                        : make_uint4(0, 0, 0, 0);
+                const uint4 t = 16u * lane < len ? load16_unaligned(a.wire, (int64_t)(xk.src + 16u * lane), a.n_bytes)
+                                                 : make_uint4(0, 0, 0, 0);
+                q[k] = u32x4{t.x, t.y, t.z, t.w};
             }
-            restage(q);
+            u8_restage(sw, q, lane);
             const uint32_t off = (lane & 15) * 64;
             bool plain;
-            const uint64_t pm = chunk_map(q, xr.mask, chunk_len(xr.len, off), plain);
-            const uint64_t rm = row_maps(pm);
-            if ((lane & 15) == 0 && r < cnt) u8_finish(a, i0 + r, xr.seg, rm);
+            const uint64_t pm = u8_chunk_map<NCH>(T, q, mask_at(xr, 0), chunk_len(xr.len, off), plain);
+            const uint64_t rm = u8_row_maps(pm, lane);
+            uint64_t fe = ~0ull;
+            if ((lane & 15) == 0 && r < cnt) fe = u8_finish(a, i0 + r, xr.seg, rm, ovf);
+            remask_wave(fe, xr.seg);
             continue;
         }
         const U8Item x0 = a.items[i0];
-        uint4 nxt[4];
-        fetch(x0, 0, nxt);
+        u32x4 nxt[4];
+        {
+            const Geo g0 = geo(x0);
+            const uint32_t b = first_step(g0, x0.len);
+            if (b != NONE) fetch(x0, b, b < g0.hl ? g0.hl : x0.len, nxt);
+        }
         U8Item item2 = x0;   // (items re-read by index: no dynamically indexed register array)
         for (uint32_t j = 0; j < cnt; ++j) {
             const U8Item item = item2;
             if (j + 1 < cnt) item2 = a.items[i0 + j + 1];
+            const Geo g = geo(item);
+            const Geo g2 = geo(item2);
+            const uint32_t f2 = j + 1 < cnt ? first_step(g2, item2.len) : NONE;
+            // the windows between head and tail, folded by the unmask (scalar loads)
+            uint64_t mids = u8m_id();
+            for (uint32_t w = 0; w < g.nwin; ++w) mids = u8m_then(mids, a.win_map[g.w0 + w]);
             uint64_t acc = u8m_id();
-            if (item.len == 0 && j + 1 < cnt) fetch(item2, 0, nxt);
-            for (uint32_t b0 = 0; b0 < item.len; b0 += 4096) {
-                uint4 cur4[4];
+            bool mids_in = false;
+            uint32_t b0 = first_step(g, item.len);
+            if (b0 == NONE && f2 != NONE) fetch(item2, f2, f2 < g2.hl ? g2.hl : item2.len, nxt);
+            while (b0 != NONE) {
+                u32x4 cur4[4];
 #pragma unroll
                 for (int k = 0; k < 4; ++k) cur4[k] = nxt[k];
-                if (b0 + 4096 < item.len) fetch(item, b0 + 4096, nxt);
-                else if (j + 1 < cnt) fetch(item2, 0, nxt);
-                restage(cur4);
+                const uint32_t nb = next_step(g, item.len, b0);
+                if (nb != NONE) fetch(item, nb, nb < g.hl ? g.hl : item.len, nxt);
+                else if (f2 != NONE) fetch(item2, f2, f2 < g2.hl ? g2.hl : item2.len, nxt);
+                u8_restage(sw, cur4, lane);
+                const uint32_t lim = b0 < g.hl ? g.hl : item.len;
                 bool plain;
-                const uint64_t pm = chunk_map(cur4, item.mask, chunk_len(item.len, b0 + lane * 64), plain);
-                acc = u8m_then(acc, wave_map(pm, plain));
+                const uint64_t pm = u8_chunk_map<NCH>(T, cur4, mask_at(item, b0), chunk_len(lim, b0 + lane * 64), plain);
+                const uint64_t wm = u8_wave_map(pm, plain, lane);
+                if (b0 >= g.hl && !mids_in) {   // the first tail step: the windows come before it
+                    acc = u8m_then(acc, mids);
+                    mids_in = true;
+                }
+                acc = u8m_then(acc, wm);
+                b0 = nb;
             }
-            if (lane == 0) u8_finish(a, i0 + j, item.seg, acc);
+            if (!mids_in) acc = u8m_then(acc, mids);
+            uint64_t fe = ~0ull;
+            if (lane == 0) fe = u8_finish(a, i0 + j, item.seg, acc, ovf);
+            remask_wave(fe, item.seg);
+        }
+    }
+    }   // blockIdx.x * 4 < n_items
+    // the last workgroup re-arms the item count (the next walk allocates from it) and, in the
+    // staged pipeline, tells the host that this decode no longer reads the context's scratch (every
+    // scratch access before the count is complete: reads were consumed, map stores drained).  No
+    // fence per workgroup: an agent-scope release writes back the XCD's L2 (1,280 of them cost
+    // ~0.4 ms, measured)
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (__hip_atomic_fetch_add(a.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
+            __hip_atomic_store(a.count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(a.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (a.fin_host) {
+                __threadfence_system();
+                __hip_atomic_store(a.fin_host, a.fin_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __threadfence_system();
+            }
         }
     }
 }

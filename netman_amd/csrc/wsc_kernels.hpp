@@ -52,8 +52,10 @@ struct U8Item {
 };
 static_assert(sizeof(U8Item) == 32, "U8Item layout");
 struct U8Seg {          // per segment with deferred items (written by the walk)
-    uint32_t head, n, done, pending_end;   // pending_end: a text chain with a deferred part is still open
-    uint32_t sbase, nspans, fbase, pad;    // the segment's span and frame ranges (emit pass)
+    uint32_t head, n, done;
+    uint32_t pending_end;  // bit 0: a text chain with a deferred part is still open; bit 1: composite items
+    uint32_t sbase, nspans, fbase;         // the segment's span and frame ranges (emit pass)
+    uint32_t minfail;      // first failing single-piece SELF frame (ordinal), 0xFFFFFFFF = none
 };
 
 // One contiguous run of masked payload bytes to XOR: source in the wire, destination either the
@@ -106,14 +108,21 @@ struct WalkArgs {
     uint32_t u8_inline_max;      // text payloads up to this many bytes are validated in the walk
     uint32_t* sticky;            // context error bits, never re-armed by a kernel (wsc_error_flags)
     uint32_t* u8host;            // host-visible word set when any UTF-8 item is deferred (cleared by the host)
+    uint32_t* win_flag;          // per unmask window: 1 = inside a deferred text item (k_unmask folds its map)
 };
 
+// k_u8_check runs AFTER the unmask: the unmask has already folded every text window that lies
+// inside an item (win_map), so the check reads only the items' partial windows at their ends --
+// in place from the unmasked wire (mask 0), COMPACT from the still-masked wire -- composes, and
+// applies the verdicts.  Frames after a failing one were unmasked too: their spans are XORed
+// again (re-masked), so the output equals what the reference leaves (it never reads them).
 struct U8Args {
     const uint8_t* wire;
     uint64_t n_bytes;
     const uint64_t* seg_off;
     const U8Item* items;
-    const uint32_t* count;
+    uint32_t* count;             // item count: re-armed by the check's last workgroup
+    uint32_t items_cap;
     uint64_t* maps;              // per item: DFA transition map (9 x 4 bits)
     U8Seg* seg;
     wsc_frame* frames;
@@ -121,6 +130,21 @@ struct U8Args {
     wsc_seg_result* seg_out;
     wsc_conn_state* state_out;
     wsc_summary* summary;
+    const uint64_t* win_map;     // per unmask window: the map the unmask folded
+    uint32_t win_shift;
+    uint32_t unmasked;           // 1: the wire is already unmasked (in place): items are read with mask 0
+    uint8_t* out;                // where the spans' bytes went: the wire (in place) or the arena (COMPACT)
+    uint32_t* done;              // finished workgroups (self re-arming)
+    uint32_t* fin_host;          // staged pipeline: the last workgroup writes fin_seq here
+    uint32_t fin_seq;
+};
+
+// The unmask's side of the text windows (k_unmask): flag / map per window, and the item count
+// (zero = nothing deferred: the LDS tables are not even built).
+struct U8Win {
+    uint32_t* flag;
+    uint64_t* map;
+    const uint32_t* count;
 };
 
 

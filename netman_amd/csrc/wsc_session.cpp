@@ -347,6 +347,9 @@ int decode_sync_part(wsc_session* s, int set, uint32_t a, uint32_t b, uint64_t p
     const int rc = wsc_decode_host(g.ctx, wire, end, off.data(), n, s->flags, sin.data(), sout.data(), sres.data(),
                                    fr.data(), s->cfg.max_frames, compact ? res : nullptr,
                                    compact ? fd.data() : nullptr, &sm);
+    if (std::getenv("WSC_DEBUG_SPLIT"))
+        std::fprintf(stderr, "decode_sync_part a=%u b=%u prefix=%llu end=%llu rc=%d ovf=%u nf=%u ns=%u\n", a, b,
+                     (unsigned long long)prefix_limit, (unsigned long long)end, rc, sm.overflow, sm.n_frames, sm.n_spans);
     if (rc == WSC_E_CAPACITY && (sm.overflow & 1u)) {
         if (n > 1) {
             const uint32_t mid = a + n / 2;

@@ -2,8 +2,10 @@
 // the two translation units that instantiate it (wsc_unmask_inplace.hip, wsc_unmask_compact.hip)
 // so that hipcc compiles the variants in parallel.
 #pragma once
+#include <type_traits>
 #include "wsc_kernels.hpp"
 #include "wsc_dev.hpp"
+#include "wsc_u8.hpp"
 
 namespace wsc {
 
@@ -297,25 +299,90 @@ __device__ __forceinline__ bool unmask_window_lanes(uint8_t* __restrict__ dst, c
     return true;
 }
 
+// Deferred text (k_u8_check runs after this kernel): a window the walk flagged lies inside one
+// UTF-8 item, so the wave that has just unmasked it folds its DFA map from the registers (text is
+// read from HBM once) and publishes it in win_map; the check reads only the items' partial windows.
+// The workgroup's LDS tables are built by the first wave that meets a text window (binary windows
+// never touch them); the others wait on the LDS state word.
+struct U8Block {
+    U8Lds t;
+    uint4 stage[4][U8_STAGE];
+    uint32_t state;   // 0 none, 1 building, 2 ready
+};
+template <int P>
+__device__ __forceinline__ void fold_text_window(U8Block& b, const u32x4 (&v)[P], uint32_t key, U8Win u8w,
+                                                           uint64_t win, uint32_t lane) {
+    uint4* sw = b.stage[(threadIdx.x >> 6) & 3];
+    // the first 4 KiB goes to the wave's stage before anything else: the unmasked registers are
+    // dead from here on (the table build below would otherwise hold them)
+    auto stage_write = [&](int g) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t o = 1024u * k + 16u * lane;
+            const u32x4 x = v[4 * g + k] ^ key;
+            sw[(o >> 6) * 5 + ((o >> 4) & 3)] = make_uint4(x[0], x[1], x[2], x[3]);
+        }
+    };
+    stage_write(0);
+    uint32_t prev = 0;
+    if (lane == 0) prev = __hip_atomic_compare_exchange_strong(&b.state, &prev, 1u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                               __HIP_MEMORY_SCOPE_WORKGROUP) ? 0u : prev;
+    prev = (uint32_t)__builtin_amdgcn_readfirstlane((int)prev);
+    if (prev == 0) {
+#pragma unroll 1
+        for (uint32_t byte = lane; byte < 256; byte += 64) u8_tables_init(b.t, byte);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0) __hip_atomic_store(&b.state, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    } else {
+        while (__hip_atomic_load(&b.state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 2u) __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    }
+    uint64_t m = u8m_id();
+#pragma unroll
+    for (int g = 0; g < P / 4; ++g) {
+        if (g) stage_write(g);
+        __builtin_amdgcn_wave_barrier();
+        u32x4 q[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint4 t = sw[lane * 5 + k];
+            q[k] = u32x4{t.x, t.y, t.z, t.w};
+        }
+        __builtin_amdgcn_wave_barrier();
+        bool plain;
+        const uint64_t pm = u8_chunk_map<2>(b.t, q, 0u, 64u, plain);
+        m = u8m_then(m, u8_wave_map(pm, plain, lane));
+    }
+    if (lane == 0) {
+        u8w.map[win] = m;
+        u8w.flag[win] = 0u;   // consumed (flags are only ever set by the walk)
+    }
+}
+
 // NT bit 0: non-temporal loads, bit 1: non-temporal stores.  In place `src` is unused (dst is
 // both source and destination) so the two restrict pointers never alias in an access; COMPACT
 // reads `src` (the wire) and writes `dst` (the arena).  `total` = wire bytes.
-template <bool COMPACT, int P, int NT>
+template <bool COMPACT, int P, int NT, bool U8>
 __device__ __forceinline__ void unmask_all(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src,
                                            uint64_t src_bytes, uint64_t total,
                                            const Span* __restrict__ spans,
                                            const uint32_t* __restrict__ tile_first,
                                            const wsc_summary* __restrict__ summary,
-                                           uint32_t* __restrict__ lb_state, uint32_t n_walk_blocks) {
+                                           uint32_t* __restrict__ lb_state, uint32_t n_walk_blocks, U8Win u8w) {
     constexpr uint32_t WB = 1024u * P;
     static_assert(NT < 16 || !COMPACT, "buffer-instruction windows are the in-place path");
     __shared__ u32x4 pm[17];
+    // U8: the launch may meet flagged text windows (the host could not rule them out); binary
+    // batches whose walk the host has seen use the variant without the fold and its LDS
+    __shared__ std::conditional_t<U8, U8Block, uint32_t> u8b;
     if (threadIdx.x < 17) pm[threadIdx.x] = prefix_mask16(threadIdx.x);
+    if constexpr (U8) if (threadIdx.x == 0) u8b.state = 0;
     __syncthreads();
     // re-arm the walk's look-back state for the next decode (this launch is ordered after it):
-    // lb_state[0] = ticket, [1] = timeout flag, [2 ...] = per-block flags
+    // lb_state[0] = ticket, [1] = timeout flag, [3 ...] = per-block flags ([2], the UTF-8 item
+    // count, is read by k_u8_check after this launch, which re-arms it)
     for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n_walk_blocks + 2; t += gridDim.x * blockDim.x)
-        lb_state[t] = 0;
+        if (t != 2) lb_state[t] = 0;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t waves_per_block = blockDim.x >> 6;
     const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * waves_per_block + (threadIdx.x >> 6));
@@ -346,6 +413,8 @@ __device__ __forceinline__ void unmask_all(uint8_t* __restrict__ dst, const uint
         }
         // the fast-path test uses scalar loads (lgkmcnt), so it never waits behind the data loads
         const uint32_t r = tile_first[win];
+        [[maybe_unused]] uint32_t text = 0;
+        if constexpr (U8) text = u8w.flag[win];   // (beside tile_first: same scalar wait)
         Span s0 = spans[r < n_spans ? r : n_spans - 1];
         if (r >= n_spans) s0.src = ~0ull;   // no span starts before the window's end
         if (s0.src <= wbase && s0.src + s0.len >= wbase + WB) {
@@ -361,6 +430,7 @@ __device__ __forceinline__ void unmask_all(uint8_t* __restrict__ dst, const uint
 #pragma unroll
                 for (int k = 0; k < P; ++k) st16v<NT>(dst + wbase + k * 1024u + lofs, v[k] ^ s0.key);
             }
+            if constexpr (U8) if (text) fold_text_window<P>(u8b, v, s0.key, u8w, win, lane);
             continue;
         }
         // Several spans overlap the window (small frames) or it holds a frame edge: lane-parallel
@@ -381,15 +451,15 @@ __device__ __forceinline__ void unmask_all(uint8_t* __restrict__ dst, const uint
 // before counting (the next walk may run while this grid's tail drains).  Every level re-arms
 // itself for the next launch.  Vector atomics and stores only.
 constexpr uint32_t FIN_GROUPS = 256, FIN_STRIDE = 32;   // fin_ctr: (FIN_GROUPS + 1) * FIN_STRIDE words
-template <bool COMPACT, int P, int NT, int MINW = 1>
-__global__ __launch_bounds__(256, MINW) void k_unmask(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src,
+template <bool COMPACT, int P, int NT, int MINW = 1, bool U8 = false>
+__global__ __launch_bounds__(256, (P == 4 ? 4 : 2) * MINW) void k_unmask(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src,
                                                 uint64_t src_bytes, uint64_t total,
                                                 const Span* __restrict__ spans,
                                                 const uint32_t* __restrict__ tile_first,
                                                 const wsc_summary* __restrict__ summary,
                                                 uint32_t* __restrict__ lb_state, uint32_t n_walk_blocks,
-                                                uint32_t* fin_ctr, uint32_t* fin_host, uint32_t fin_seq) {
-    unmask_all<COMPACT, P, NT>(dst, src, src_bytes, total, spans, tile_first, summary, lb_state, n_walk_blocks);
+                                                uint32_t* fin_ctr, uint32_t* fin_host, uint32_t fin_seq, U8Win u8w) {
+    unmask_all<COMPACT, P, NT, U8>(dst, src, src_bytes, total, spans, tile_first, summary, lb_state, n_walk_blocks, u8w);
     if (fin_host == nullptr) return;
     __syncthreads();
     if (threadIdx.x == 0) {
