@@ -271,8 +271,8 @@ int wsc_create(int device, const wsc_config* cfg_in, wsc_ctx** out) {
     chk(hipMalloc(&c->spans, (uint64_t)cfg.max_frames * sizeof(Span)), "hipMalloc spans");
     c->tile_entries = cfg.max_batch_bytes / 1024 + 2;
     chk(hipMalloc(&c->tile, c->tile_entries * sizeof(uint32_t)), "hipMalloc tile");
-    // items are cut at U8_PIECE-aligned wire offsets: a frame is one item plus one per aligned
-    // boundary inside its payload, so frames + bytes / U8_PIECE + 1 bounds the total
+    // a frame is one item up to U8_PIECE (1 GiB), longer ones one per U8_PIECE-aligned boundary
+    // inside their payload more, so frames + bytes / U8_PIECE + 1 bounds the total
     c->u8items_cap = cfg.max_frames + (uint32_t)(cfg.max_batch_bytes / U8_PIECE) + 64;
     chk(hipMalloc(&c->u8items, (uint64_t)c->u8items_cap * sizeof(U8Item)), "hipMalloc u8items");
     chk(hipMalloc(&c->u8maps, (uint64_t)c->u8items_cap * sizeof(uint64_t)), "hipMalloc u8maps");
@@ -294,6 +294,7 @@ int wsc_create(int device, const wsc_config* cfg_in, wsc_ctx** out) {
     }
     if (const char* e = std::getenv("WSC_U8_INLINE_MAX"); e && *e)   // test knob: 0 sends all text chip-wide
         c->u8_inline_max = (uint32_t)std::strtoul(e, nullptr, 10);
+    if (c->u8_inline_max >= 4096) c->u8_inline_max = 4095;   // a payload holding a whole window is deferred
     c->enc_blocks = (cfg.max_frames + 255) / 256 + 1;
     c->enc_cap = cfg.max_batch_bytes + 16ull * cfg.max_frames;
     c->enc_tile_entries = c->enc_cap / ENC_WIN + 2;
@@ -520,7 +521,7 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
         ua.done = c->u8done;
         ua.fin_host = signal ? c->hflag + 1 : nullptr;
         ua.fin_seq = c->fin_seq + 1;
-        const dim3 ug(c->u8_grid ? c->u8_grid : (uint32_t)c->n_cu * 5);   // resident: 5 waves/SIMD (96 VGPRs)
+        const dim3 ug(c->u8_grid ? c->u8_grid : (uint32_t)c->n_cu * 4);   // resident: 4 waves/SIMD (128 VGPRs)
         if (c->u8_chains == 1) hipLaunchKernelGGL(k_u8_check<1>, ug, dim3(256), 0, st, ua);
         else if (c->u8_chains == 4) hipLaunchKernelGGL(k_u8_check<4>, ug, dim3(256), 0, st, ua);
         else hipLaunchKernelGGL(k_u8_check<2>, ug, dim3(256), 0, st, ua);

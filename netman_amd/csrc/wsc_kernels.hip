@@ -471,8 +471,11 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
                         it.len = (uint32_t)(pe - ps);
                         it.mask = rotr32(mk, 8u * (uint32_t)((ps - src) & 3));   // phase 0 at the piece
                         if (a.win_flag) {   // windows inside the piece: folded by the unmask
-                            for (uint64_t wi = (ps + W - 1) >> a.win_shift; ((wi + 1) << a.win_shift) <= pe; ++wi)
-                                a.win_flag[wi] = 1u;
+                            uint64_t wi = (ps + W - 1) >> a.win_shift;
+                            const uint64_t we = pe >> a.win_shift;
+                            for (; wi < we && (wi & 3); ++wi) a.win_flag[wi] = 1u;
+                            for (; wi + 4 <= we; wi += 4) *reinterpret_cast<uint4*>(a.win_flag + wi) = make_uint4(1, 1, 1, 1);
+                            for (; wi < we; ++wi) a.win_flag[wi] = 1u;
                         }
                         it.seg = s;
                         it.ordinal = nf;
@@ -1135,9 +1138,9 @@ __global__ __launch_bounds__(NT) void k_walk_fused(WalkArgs a) {
 // Publish one item's map; the segment's last item composes the segment's items in frame order
 // with the walk's states and applies the verdict (one lane).  Returns the wire end of the failing
 // frame when this call applied a failure verdict (the wave then re-masks the later spans), else ~0.
-__device__ __forceinline__ uint64_t u8_finish(const U8Args& a, uint32_t it, uint32_t seg, uint64_t acc, bool ovf) {
+__device__ __forceinline__ uint64_t u8_finish(const U8Args& a, uint32_t it, const U8Item& self, uint64_t acc, bool ovf) {
+    const uint32_t seg = self.seg;
     const uint32_t n = a.seg[seg].n;   // (static: loaded beside the map store, not after the count)
-    const U8Item self = a.items[it];
     // a whole TEXT message in one piece (SELF, first and last) needs no composition: its verdict
     // is its own map from state 0, folded into the segment's first failing ordinal
     if (self.kind == U8K_SELF && self.first && self.last) {
@@ -1226,7 +1229,7 @@ __device__ __forceinline__ void u8_remask(const U8Args& a, uint32_t seg, uint64_
 // per 16: PMC showed the 16-byte-piece version at 12.5 VALU per text byte, VALU-bound (77 % of
 // the chip's VALU cycles).
 template <uint32_t NCH>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_u8_check(U8Args a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_u8_check(U8Args a) {
     // (items past the capacity were dropped by the walk: only a batch whose records overflowed
     // allocates that many, and its verdicts are skipped below)
     const uint32_t n_items = *a.count < a.items_cap ? *a.count : a.items_cap;
@@ -1306,38 +1309,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
     // item's first step too -- issued before the current step is folded.  (A ticket counter for
     // dynamic balance measured far slower: 64 k same-address atomics; a second pass striding big
     // items one by one paid a scan of every unit's lengths per wave.)
-    const uint32_t n_units = (n_items + 3) / 4;
-    for (uint32_t u = gw; u < n_units; u += nw) {
-        const uint32_t i0 = 4 * u;
-        const uint32_t cnt = n_items - i0 < 4 ? n_items - i0 : 4u;
-        bool small = true;
-        for (uint32_t j = 0; j < cnt; ++j) small = small && a.items[i0 + j].len <= 1024;
-        if (small) {
-            // piece k of the step = item k's KiB (16 B per lane, coalesced), restaged so that row r
-            // (lanes 16r..16r+15) holds item r in 64-byte chunks (items <= 1 KiB hold no window)
-            const uint32_t r = lane >> 4;
-            U8Item xr;   // (issued before the data loads: its latency overlaps theirs)
-            if (r < cnt) xr = a.items[i0 + r];
-            else { xr = a.items[i0]; xr.len = 0; }
-            u32x4 q[4];
-#pragma unroll
-            for (uint32_t k = 0; k < 4; ++k) {
-                const U8Item xk = a.items[i0 + (k < cnt ? k : 0u)];
-                const uint32_t len = k < cnt ? xk.len : 0u;
-                const uint4 t = 16u * lane < len ? load16_unaligned(a.wire, (int64_t)(xk.src + 16u * lane), a.n_bytes)
-                                                 : make_uint4(0, 0, 0, 0);
-                q[k] = u32x4{t.x, t.y, t.z, t.w};
-            }
-            u8_restage(sw, q, lane);
-            const uint32_t off = (lane & 15) * 64;
-            bool plain;
-            const uint64_t pm = u8_chunk_map<NCH>(T, q, mask_at(xr, 0), chunk_len(xr.len, off), plain);
-            const uint64_t rm = u8_row_maps(pm, lane);
-            uint64_t fe = ~0ull;
-            if ((lane & 15) == 0 && r < cnt) fe = u8_finish(a, i0 + r, xr.seg, rm, ovf);
-            remask_wave(fe, xr.seg);
-            continue;
-        }
+    // Other units walk their items' steps in order, the next step's loads -- the next item's first
+    // step too -- issued before the current step is folded.
+    auto unit_large = [&](uint32_t i0, uint32_t cnt) {
         const U8Item x0 = a.items[i0];
         u32x4 nxt[4];
         {
@@ -1352,9 +1326,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
             const Geo g = geo(item);
             const Geo g2 = geo(item2);
             const uint32_t f2 = j + 1 < cnt ? first_step(g2, item2.len) : NONE;
-            // the windows between head and tail, folded by the unmask (scalar loads)
+            // the windows between head and tail, folded by the unmask: each lane composes a run
+            // of ceil(nwin / 64) of them, the wave composes the lanes in order
             uint64_t mids = u8m_id();
-            for (uint32_t w = 0; w < g.nwin; ++w) mids = u8m_then(mids, a.win_map[g.w0 + w]);
+            if (g.nwin) {
+                const uint32_t k = (g.nwin + 63) / 64;
+                uint64_t m = u8m_id();
+                for (uint32_t q = 0; q < k; ++q)
+                    if (lane * k + q < g.nwin) m = u8m_then(m, a.win_map[g.w0 + (uint64_t)lane * k + q]);
+                mids = u8_wave_map(m, false, lane);
+            }
             uint64_t acc = u8m_id();
             bool mids_in = false;
             uint32_t b0 = first_step(g, item.len);
@@ -1380,9 +1361,86 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
             }
             if (!mids_in) acc = u8m_then(acc, mids);
             uint64_t fe = ~0ull;
-            if (lane == 0) fe = u8_finish(a, i0 + j, item.seg, acc, ovf);
+            if (lane == 0) fe = u8_finish(a, i0 + j, item, acc, ovf);
             remask_wave(fe, item.seg);
         }
+    };
+    const uint32_t n_units = (n_items + 3) / 4;
+    // A small unit's 4 items as the step needs them (uniform, scalar loads); entries past the last
+    // item have len 0.
+    struct UnitS { uint64_t src[4]; uint32_t len[4], mask[4]; };
+    auto unit_items = [&](uint32_t u, UnitS& x) {
+        const uint32_t i0 = 4 * u, cnt = n_items - i0 < 4 ? n_items - i0 : 4u;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+            const U8Item it = a.items[i0 + (k < cnt ? k : 0u)];
+            x.src[k] = it.src;
+            x.len[k] = k < cnt ? it.len : 0u;
+            x.mask[k] = it.mask;
+        }
+    };
+    auto unit_small = [](const UnitS& x) -> bool {
+        return x.len[0] <= 1024 && x.len[1] <= 1024 && x.len[2] <= 1024 && x.len[3] <= 1024;
+    };
+    // piece k of a small unit's step = item k's KiB (16 B per lane, coalesced)
+    auto unit_data = [&](const UnitS& x, u32x4 (&q)[4]) {
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+            const uint4 t = 16u * lane < x.len[k] ? load16_unaligned(a.wire, (int64_t)(x.src[k] + 16u * lane), a.n_bytes)
+                                                  : make_uint4(0, 0, 0, 0);
+            q[k] = u32x4{t.x, t.y, t.z, t.w};
+        }
+    };
+    // Software pipeline over a wave's units: the next unit's items are loaded one unit ahead, and
+    // (small units) its data loads go out before this unit's verdict atomics, so the dependent
+    // round trips of consecutive units overlap (1 KiB text: 4 per unit otherwise)
+    UnitS xc, xn;
+    u32x4 qc[4] = {};
+    bool cur_small = false;
+    if (gw < n_units) {
+        unit_items(gw, xc);
+        cur_small = unit_small(xc);
+        if (cur_small) unit_data(xc, qc);
+    }
+    if (gw + nw < n_units) unit_items(gw + nw, xn);
+    for (uint32_t u = gw; u < n_units; u += nw) {
+        const uint32_t i0 = 4 * u;
+        const uint32_t cnt = n_items - i0 < 4 ? n_items - i0 : 4u;
+        const uint32_t un = u + nw;
+        bool nsmall = false;
+        u32x4 qn[4] = {};
+        if (cur_small) {
+            // restaged so that row r (lanes 16r..16r+15) holds item r in 64-byte chunks (items
+            // <= 1 KiB hold no window).  The row's full item is needed only by the verdict: its
+            // load overlaps the fold.
+            const uint32_t r = lane >> 4;
+            const U8Item xr = a.items[i0 + (r < cnt ? r : 0u)];
+            const uint32_t rlen = r == 0 ? xc.len[0] : r == 1 ? xc.len[1] : r == 2 ? xc.len[2] : xc.len[3];
+            const uint32_t rmask = r == 0 ? xc.mask[0] : r == 1 ? xc.mask[1] : r == 2 ? xc.mask[2] : xc.mask[3];
+            u8_restage(sw, qc, lane);
+            const uint32_t off = (lane & 15) * 64;
+            bool plain;
+            const uint64_t pm = u8_chunk_map<NCH>(T, qc, a.unmasked ? 0u : rmask, chunk_len(rlen, off), plain);
+            const uint64_t rm = u8_row_maps(pm, lane);
+            if (un < n_units) {
+                nsmall = unit_small(xn);
+                if (nsmall) unit_data(xn, qn);
+            }
+            uint64_t fe = ~0ull;
+            if ((lane & 15) == 0 && r < cnt) fe = u8_finish(a, i0 + r, xr, rm, ovf);
+            remask_wave(fe, xr.seg);
+        } else {
+            unit_large(i0, cnt);
+            if (un < n_units) {
+                nsmall = unit_small(xn);
+                if (nsmall) unit_data(xn, qn);
+            }
+        }
+        xc = xn;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) qc[k] = qn[k];
+        cur_small = nsmall;
+        if (un + nw < n_units) unit_items(un + nw, xn);
     }
     }   // blockIdx.x * 4 < n_items
     // the last workgroup re-arms the item count (the next walk allocates from it) and, in the

@@ -36,8 +36,9 @@ enum : uint32_t { SEGF_UTF8 = 1u, SEGF_U8DEFER = 2u, SEGF_LONG = 4u };
 // ---- chip-wide UTF-8 (k_u8_check) ------------------------------------------------------------
 // The walk validates text payloads of at most u8_inline_max bytes itself (serial DFA per lane);
 // larger ones -- and every later frame of a text chain that has a deferred part -- become items of
-// at most U8_PIECE bytes, validated by k_u8_check across the whole chip before the unmask runs.
-constexpr uint32_t U8_PIECE = 16384;   // 16 KiB: 64 KiB items left a 25 % tail (equal-sized items vs residency)
+// at most U8_PIECE bytes (one per frame below 1 GiB), validated chip-wide: the unmask folds the
+// maps of the windows inside them, k_u8_check the partial windows at their ends (after the unmask).
+constexpr uint32_t U8_PIECE = 1u << 30;
 enum : uint8_t { U8K_SELF = 0, U8K_PART = 1, U8K_CHAIN = 2 };   // close reasons are SELF items
 struct U8Item {
     uint64_t src;       // wire offset of the first (masked) byte
