@@ -19,6 +19,7 @@ template <bool COMPACT> __global__ void k_walk_count(WalkArgs);
 __global__ void k_walk_scan(WalkArgs, uint32_t);
 template <bool COMPACT> __global__ void k_walk_emit(WalkArgs);
 template <uint32_t NCH> __global__ void k_u8_check(U8Args);
+__global__ void k_u8_verdict(U8Args);
 template <bool COMPACT, int P, int NT, int MINW, bool U8>
 __global__ void k_unmask(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*,
                          const wsc_summary*, uint32_t*, uint32_t, uint32_t*, uint32_t*, uint32_t, U8Win);
@@ -519,12 +520,15 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
         ua.unmasked = compact ? 0u : 1u;
         ua.out = udst;
         ua.done = c->u8done;
+        ua.n_segs = n;
         ua.fin_host = signal ? c->hflag + 1 : nullptr;
         ua.fin_seq = c->fin_seq + 1;
         const dim3 ug(c->u8_grid ? c->u8_grid : (uint32_t)c->n_cu * 4);   // resident: 4 waves/SIMD (128 VGPRs)
         if (c->u8_chains == 1) hipLaunchKernelGGL(k_u8_check<1>, ug, dim3(256), 0, st, ua);
         else if (c->u8_chains == 4) hipLaunchKernelGGL(k_u8_check<4>, ug, dim3(256), 0, st, ua);
         else hipLaunchKernelGGL(k_u8_check<2>, ug, dim3(256), 0, st, ua);
+        HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(k_u8_verdict, dim3((n + 255) / 256), dim3(256), 0, st, ua);
         HIP_TRY(hipGetLastError());
     }
     rec(3);

@@ -619,7 +619,9 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
             a.u8info[2 * s] = u8fail;
             a.u8info[2 * s + 1] = u8dfa;
         }
-        if (u8_n) {
+        if (!u8_n) {
+            a.u8seg[s].n = 0;   // (k_u8_verdict visits every segment)
+        } else {
             U8Seg g{};
             g.head = u8_head;
             g.n = u8_n;
@@ -1125,45 +1127,42 @@ __global__ __launch_bounds__(NT) void k_walk_fused(WalkArgs a) {
 
 // ---------------------------------------------------------------------------------------------
 // Chip-wide UTF-8 (utf8.Valid, websocket_frame.go:71-73, websocket.go:170-172) for the text the
-// walk deferred.  Runs AFTER the unmask, which has folded the map of every unmask window lying
-// inside an item (win_map): this kernel reads only the items' partial windows at their ends, folds
-// them (each lane one 64-byte chunk, waves compose lanes), composes head, window maps and tail per
-// item and publishes the item's map (agent-scope store, drained, then an agent-scope counter); the
-// wave that completes a segment's last item composes the segment's items in frame order with the
-// states the walk recorded and applies the verdict: the first failing frame becomes WSC_FK_ERROR /
-// 1007, the segment stops there, and the spans of later frames -- already unmasked -- are XORed
-// again, so the bytes are left as the reference leaves them (never read).  Maps: wsc_u8.hpp.
+// walk deferred, in two launches after the unmask.  The unmask has folded the map of every unmask
+// window lying inside an item (win_map).  k_u8_check reads only the items' partial windows at
+// their ends, folds them (each lane one 64-byte chunk, waves compose lanes), composes head, window
+// maps and tail per item: a whole TEXT message (one piece, SELF) is decided on the spot (its
+// ordinal min-folded into the segment's first failure), any other item publishes its map.
+// k_u8_verdict, one lane per segment, composes the published maps in frame order with the states
+// the walk recorded and applies the verdict: the first failing frame becomes WSC_FK_ERROR / 1007,
+// the segment stops there, and the spans of later frames -- already unmasked -- are XORed again,
+// so the bytes are left as the reference leaves them (never read).  Maps: wsc_u8.hpp.
 // ---------------------------------------------------------------------------------------------
 
-// Publish one item's map; the segment's last item composes the segment's items in frame order
-// with the walk's states and applies the verdict (one lane).  Returns the wire end of the failing
-// frame when this call applied a failure verdict (the wave then re-masks the later spans), else ~0.
-__device__ __forceinline__ uint64_t u8_finish(const U8Args& a, uint32_t it, const U8Item& self, uint64_t acc, bool ovf) {
-    const uint32_t seg = self.seg;
-    const uint32_t n = a.seg[seg].n;   // (static: loaded beside the map store, not after the count)
-    // a whole TEXT message in one piece (SELF, first and last) needs no composition: its verdict
-    // is its own map from state 0, folded into the segment's first failing ordinal
+// One item's result: no waiting, no counter (the verdict kernel runs after this launch).
+__device__ __forceinline__ void u8_publish(const U8Args& a, uint32_t it, const U8Item& self, uint64_t acc) {
     if (self.kind == U8K_SELF && self.first && self.last) {
         if (u8m_get(acc, 0) != 0)
-            __hip_atomic_fetch_min(&a.seg[seg].minfail, self.ordinal, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_min(&a.seg[self.seg].minfail, self.ordinal, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
-        __hip_atomic_store(a.maps + it, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        a.maps[it] = acc;
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const uint32_t done = __hip_atomic_fetch_add(&a.seg[seg].done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
-    if (done != n) return ~0ull;
-    const U8Seg g = a.seg[seg];
+}
+
+// A segment's verdict (one lane): the first failing frame -- the single-piece SELF items' minimum
+// or the first failing composition -- and, if any, its results.  Returns the failing frame's wire
+// end (the wave then re-masks the later spans), else ~0.
+__device__ __forceinline__ uint64_t u8_verdict(const U8Args& a, uint32_t s, const U8Seg& g) {
     uint32_t cur = 0, start = 0;   // states 0..7, 0xFF = reject
-    uint32_t fail = __hip_atomic_fetch_add(&a.seg[seg].minfail, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // the segment's last item: compose its composite items in frame order with the walk's states
-    // (single-piece SELF items were decided above; a chain never has one inside it)
+    uint32_t fail = g.minfail;
+    // compose the composite items in frame order with the walk's states (a chain never has a
+    // single-piece SELF item inside it)
     uint64_t fm = u8m_id();
     uint32_t j = (g.pending_end & 2u) ? g.head : 0xFFFFFFFFu;
     for (uint32_t c = 0; c < g.n && j != 0xFFFFFFFFu; ++c) {
         const U8Item x = a.items[j];
         if (x.ordinal >= fail) break;   // a single-piece SELF frame failed first
         if (x.kind == U8K_SELF && x.first && x.last) { j = x.next; continue; }
-        const uint64_t m = __hip_atomic_fetch_add(a.maps + j, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t m = a.maps[j];
         if (x.first) {
             start = x.kind == U8K_SELF ? 0u : (x.s_in != 0xFF ? (x.s_in > 7 ? 0xFFu : (uint32_t)x.s_in) : cur);
             fm = u8m_id();
@@ -1180,8 +1179,6 @@ __device__ __forceinline__ uint64_t u8_finish(const U8Args& a, uint32_t it, cons
         }
         j = x.next;
     }
-    const uint32_t s = seg;
-    if (ovf) return ~0ull;
     if (fail == 0xFFFFFFFFu) {
         if ((g.pending_end & 1u) && a.state_out[s].cont_len) a.state_out[s].cont_utf8 = (uint8_t)(cur > 7 ? 8u : cur);
         return ~0ull;
@@ -1233,13 +1230,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
     // (items past the capacity were dropped by the walk: only a batch whose records overflowed
     // allocates that many, and its verdicts are skipped below)
     const uint32_t n_items = *a.count < a.items_cap ? *a.count : a.items_cap;
-    // a batch whose records overflowed is invalid as a whole (the caller re-decodes it): its
-    // verdicts are not applied -- the failing frame or its later spans may lie past the capacity
-    const bool ovf = a.summary->overflow != 0;
     __shared__ U8Lds T;
     __shared__ uint4 stage[4][U8_STAGE];
     const uint32_t lane = threadIdx.x & 63;
-    if (blockIdx.x * 4 < n_items) {   // (nothing deferred: the workgroup only counts itself done)
+    if (blockIdx.x * 4 >= n_items) return;   // nothing deferred (or fewer units than waves)
+    {
     u8_tables_init(T, threadIdx.x);
     __syncthreads();
     const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
@@ -1290,18 +1285,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
     };
     auto chunk_len = [](uint32_t len, uint32_t off) -> uint32_t {
         return off < len ? (len - off >= 64 ? 64u : len - off) : 0u;
-    };
-    // the failing segments' later spans, re-masked by the whole wave
-    auto remask_wave = [&](uint64_t fe, uint32_t fs) {
-        uint64_t pend = __ballot(fe != ~0ull);
-        while (pend) {
-            const uint32_t l = (uint32_t)__builtin_ctzll(pend);
-            pend &= pend - 1;
-            const uint32_t seg = (uint32_t)__builtin_amdgcn_readlane((int)fs, (int)l);
-            const uint64_t fend = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(fe >> 32), (int)l) << 32 |
-                                  (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)fe, (int)l);
-            u8_remask(a, seg, fend, lane);
-        }
     };
     // A unit is 4 consecutive items.  Units of small items (<= 1 KiB each: 1 KiB text frames) take
     // one step: row r (16 lanes x 64 B) holds item r, and lanes 0, 16, 32, 48 publish the 4 items'
@@ -1360,9 +1343,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
                 b0 = nb;
             }
             if (!mids_in) acc = u8m_then(acc, mids);
-            uint64_t fe = ~0ull;
-            if (lane == 0) fe = u8_finish(a, i0 + j, item, acc, ovf);
-            remask_wave(fe, item.seg);
+            if (lane == 0) u8_publish(a, i0 + j, item, acc);
         }
     };
     const uint32_t n_units = (n_items + 3) / 4;
@@ -1426,9 +1407,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
                 nsmall = unit_small(xn);
                 if (nsmall) unit_data(xn, qn);
             }
-            uint64_t fe = ~0ull;
-            if ((lane & 15) == 0 && r < cnt) fe = u8_finish(a, i0 + r, xr, rm, ovf);
-            remask_wave(fe, xr.seg);
+            if ((lane & 15) == 0 && r < cnt) u8_publish(a, i0 + r, xr, rm);
         } else {
             unit_large(i0, cnt);
             if (un < n_units) {
@@ -1442,12 +1421,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
         cur_small = nsmall;
         if (un + nw < n_units) unit_items(un + nw, xn);
     }
-    }   // blockIdx.x * 4 < n_items
-    // the last workgroup re-arms the item count (the next walk allocates from it) and, in the
-    // staged pipeline, tells the host that this decode no longer reads the context's scratch (every
-    // scratch access before the count is complete: reads were consumed, map stores drained).  No
-    // fence per workgroup: an agent-scope release writes back the XCD's L2 (1,280 of them cost
-    // ~0.4 ms, measured)
+    }
+}
+
+// One lane per segment (segments without deferred items have n == 0).  The last workgroup
+// re-arms the item count (the next walk allocates from it) and, in the staged pipeline, tells the
+// host that this decode no longer reads the context's scratch (every scratch access before the
+// count is complete: reads were consumed).  No fence per workgroup: an agent-scope release writes
+// back the XCD's L2 (1,280 of them cost ~0.4 ms, measured).
+__global__ __launch_bounds__(256) void k_u8_verdict(U8Args a) {
+    // a batch whose records overflowed is invalid as a whole (the caller re-decodes it): its
+    // verdicts are not applied -- the failing frame or its later spans may lie past the capacity
+    const bool ovf = a.summary->overflow != 0;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    uint64_t fe = ~0ull;
+    if (s < a.n_segs && !ovf) {
+        const U8Seg g = a.seg[s];
+        if (g.n) fe = u8_verdict(a, s, g);
+    }
+    // failing segments: their later spans re-masked by the whole wave
+    uint64_t pend = __ballot(fe != ~0ull);
+    while (pend) {
+        const uint32_t l = (uint32_t)__builtin_ctzll(pend);
+        pend &= pend - 1;
+        const uint32_t seg = (uint32_t)__builtin_amdgcn_readlane((int)s, (int)l);
+        const uint64_t fend = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(fe >> 32), (int)l) << 32 |
+                              (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)fe, (int)l);
+        u8_remask(a, seg, fend, lane);
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
         if (__hip_atomic_fetch_add(a.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {

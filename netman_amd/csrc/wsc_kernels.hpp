@@ -135,7 +135,8 @@ struct U8Args {
     uint32_t win_shift;
     uint32_t unmasked;           // 1: the wire is already unmasked (in place): items are read with mask 0
     uint8_t* out;                // where the spans' bytes went: the wire (in place) or the arena (COMPACT)
-    uint32_t* done;              // finished workgroups (self re-arming)
+    uint32_t n_segs;
+    uint32_t* done;              // k_u8_verdict's finished workgroups (self re-arming)
     uint32_t* fin_host;          // staged pipeline: the last workgroup writes fin_seq here
     uint32_t fin_seq;
 };
