@@ -1,6 +1,7 @@
 """Back-to-back decodes of one device batch on one stream (one batch in flight), for kernel-trace
 gap analysis:  python tools/single_loop.py <config> [iters]
-config: head (16384 x 64 KiB, 4/seg) | c1 (1M x 1 KiB, 16/seg) | c2 (256k mixed, 16/seg)"""
+config: head (16384 x 64 KiB, 4/seg) | c1 (1M x 1 KiB, 16/seg) | c2 (256k mixed, 16/seg) |
+t64 / t1 (TEXT 16384 x 64 KiB / 262144 x 1 KiB; wire restored before each decode, wall time includes the copy)"""
 import os
 import sys
 import time
@@ -31,12 +32,22 @@ def main():
              fr=torch.zeros((cfg["n_frames"] + 16) * 32, dtype=torch.uint8, device=dev), sm=torch.zeros(32, dtype=torch.uint8, device=dev))
     b = c.make_batch(t["wire"], t["seg_off"], None, t["st"], t["so"], t["fr"], t["sm"])
     st = torch.cuda.Stream(device=dev)
-    for _ in range(3):
+    # TEXT batches are decoded from the pristine masked wire every time (an in-place decode leaves
+    # the payload unmasked; decoding it again would validate garbage); the copy is its own kernel
+    pristine = t["wire"].clone() if which.startswith("t") else None
+
+    def one():
+        if pristine is not None:
+            with torch.cuda.stream(st):
+                t["wire"].copy_(pristine)
         c.decode(b, st.cuda_stream)
+
+    for _ in range(3):
+        one()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(iters):
-        c.decode(b, st.cuda_stream)
+        one()
     torch.cuda.synchronize()
     el = (time.perf_counter() - t0) / iters * 1e3
     print(f"{which}: {el:.4f} ms per decode, {cfg['payload_bytes'] / (el * 1e-3) / 2**30:.1f} GiB/s, errors {c.error_flags()}")
