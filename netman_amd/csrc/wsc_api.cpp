@@ -3,6 +3,7 @@
 // missing device is an error, WSC_E_NODEVICE).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -85,7 +86,8 @@ struct wsc_ctx {
     U8Seg* u8seg = nullptr;
     uint32_t* win_flag = nullptr;       // per unmask window: inside a deferred text item (walk sets, unmask clears)
     uint64_t* win_map = nullptr;        // per unmask window: the DFA map the unmask folded
-    uint32_t* u8done = nullptr;         // k_u8_check finished workgroups (self re-arming)
+    uint32_t* u8done = nullptr;         // [0] k_u8_verdict finished workgroups, [32] listed segments (self re-arming)
+    uint32_t* u8seglist = nullptr;      // segments with deferred UTF-8 items
     uint32_t u8_inline_max = 256;
     uint32_t u8_grid = 0;               // WSC_U8_GRID: k_u8_check workgroups (A/B experiments; 0 = 5 per CU)
     int walk_mode = 0;                  // WSC_WALK_MODE: 64, 256 or 3 pins the walk geometry (A/B, tests); 0 = auto
@@ -280,10 +282,11 @@ int wsc_create(int device, const wsc_config* cfg_in, wsc_ctx** out) {
     chk(hipMalloc(&c->u8seg, (uint64_t)cfg.max_segs * sizeof(U8Seg)), "hipMalloc u8seg");
     chk(hipMalloc(&c->win_flag, c->tile_entries * sizeof(uint32_t)), "hipMalloc win_flag");
     chk(hipMalloc(&c->win_map, c->tile_entries * sizeof(uint64_t)), "hipMalloc win_map");
-    chk(hipMalloc(&c->u8done, sizeof(uint32_t)), "hipMalloc u8done");
+    chk(hipMalloc(&c->u8done, 64 * sizeof(uint32_t)), "hipMalloc u8done");
+    chk(hipMalloc(&c->u8seglist, (uint64_t)cfg.max_segs * sizeof(uint32_t)), "hipMalloc u8seglist");
     if (rc == WSC_OK) {
         chk(hipMemsetAsync(c->win_flag, 0, c->tile_entries * sizeof(uint32_t), c->stream), "hipMemset win_flag");
-        chk(hipMemsetAsync(c->u8done, 0, sizeof(uint32_t), c->stream), "hipMemset u8done");
+        chk(hipMemsetAsync(c->u8done, 0, 64 * sizeof(uint32_t), c->stream), "hipMemset u8done");
         chk(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
     }
     if (const char* e = std::getenv("WSC_UNMASK_BUF"); e && *e) c->unmask_buf = std::atoi(e);
@@ -324,7 +327,7 @@ int wsc_destroy(wsc_ctx* c) {
                     c->d_seg_off, c->d_state_in, c->d_state_out, c->d_seg_out, c->d_frames,
                     c->d_frame_dst, c->d_summary, c->enc_lb_state, c->enc_lb_agg, c->enc_lb_incl, c->enc_tile,
                     c->d_enc_msgs, c->d_enc_src, c->d_enc_out, c->d_enc_off, c->u8items, c->u8maps, c->u8seg,
-                    c->win_flag, c->win_map, c->u8done};
+                    c->win_flag, c->win_map, c->u8done, c->u8seglist};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -408,6 +411,8 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     wa.sticky = c->sticky;
     wa.u8host = c->hflag;
     wa.win_flag = c->win_flag;
+    wa.u8seglist = c->u8seglist;
+    wa.u8segcnt = c->u8done + 32;
 
     // walk geometry: the fused walk with blocks that fill the CUs once (64 lanes for up to 64
     // segments per CU, else 256), or -- for more segments than the chip holds lanes at once -- the
@@ -521,6 +526,8 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
         ua.out = udst;
         ua.done = c->u8done;
         ua.n_segs = n;
+        ua.seglist = c->u8seglist;
+        ua.segcnt = c->u8done + 32;
         ua.fin_host = signal ? c->hflag + 1 : nullptr;
         ua.fin_seq = c->fin_seq + 1;
         const dim3 ug(c->u8_grid ? c->u8_grid : (uint32_t)c->n_cu * 4);   // resident: 4 waves/SIMD (128 VGPRs)
@@ -528,7 +535,7 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
         else if (c->u8_chains == 4) hipLaunchKernelGGL(k_u8_check<4>, ug, dim3(256), 0, st, ua);
         else hipLaunchKernelGGL(k_u8_check<2>, ug, dim3(256), 0, st, ua);
         HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL(k_u8_verdict, dim3((n + 255) / 256), dim3(256), 0, st, ua);
+        hipLaunchKernelGGL(k_u8_verdict, dim3(std::min<uint32_t>((n + 255) / 256, (uint32_t)c->n_cu * 2)), dim3(256), 0, st, ua);
         HIP_TRY(hipGetLastError());
     }
     rec(3);

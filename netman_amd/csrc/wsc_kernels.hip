@@ -619,9 +619,20 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
             a.u8info[2 * s] = u8fail;
             a.u8info[2 * s + 1] = u8dfa;
         }
-        if (!u8_n) {
-            a.u8seg[s].n = 0;   // (k_u8_verdict visits every segment)
-        } else {
+        // segments with deferred items are listed for k_u8_verdict (one atomic per wave, at the
+        // segment's end: off the header chain, and never for binary batches)
+        const uint64_t has = __ballot(u8_n != 0);
+        if (has) {
+            const uint32_t leader = (uint32_t)__builtin_ctzll(has);
+            uint32_t base = 0;
+            if (lane_id() == leader)
+                base = __hip_atomic_fetch_add(a.u8segcnt, (uint32_t)__builtin_popcountll(has), __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+            base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)leader);
+            if (u8_n)
+                a.u8seglist[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(has >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)has, 0u))] = s;
+        }
+        if (u8_n) {
             U8Seg g{};
             g.head = u8_head;
             g.n = u8_n;
@@ -1424,7 +1435,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
     }
 }
 
-// One lane per segment (segments without deferred items have n == 0).  The last workgroup
+// One lane per listed segment (the walk lists those with deferred items).  The last workgroup
 // re-arms the item count (the next walk allocates from it) and, in the staged pipeline, tells the
 // host that this decode no longer reads the context's scratch (every scratch access before the
 // count is complete: reads were consumed).  No fence per workgroup: an agent-scope release writes
@@ -1434,26 +1445,32 @@ __global__ __launch_bounds__(256) void k_u8_verdict(U8Args a) {
     // verdicts are not applied -- the failing frame or its later spans may lie past the capacity
     const bool ovf = a.summary->overflow != 0;
     const uint32_t lane = threadIdx.x & 63;
-    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    uint64_t fe = ~0ull;
-    if (s < a.n_segs && !ovf) {
-        const U8Seg g = a.seg[s];
-        if (g.n) fe = u8_verdict(a, s, g);
-    }
-    // failing segments: their later spans re-masked by the whole wave
-    uint64_t pend = __ballot(fe != ~0ull);
-    while (pend) {
-        const uint32_t l = (uint32_t)__builtin_ctzll(pend);
-        pend &= pend - 1;
-        const uint32_t seg = (uint32_t)__builtin_amdgcn_readlane((int)s, (int)l);
-        const uint64_t fend = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(fe >> 32), (int)l) << 32 |
-                              (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)fe, (int)l);
-        u8_remask(a, seg, fend, lane);
+    const uint32_t nseg = *a.segcnt < a.n_segs ? *a.segcnt : a.n_segs;   // segments with deferred items
+    // grid-stride over the list, whole waves per step (the re-mask below is wave-cooperative)
+    for (uint32_t b = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); b < nseg && !ovf; b += gridDim.x * blockDim.x) {
+        const uint32_t i = b + lane;
+        uint32_t s = 0;
+        uint64_t fe = ~0ull;
+        if (i < nseg) {
+            s = a.seglist[i];
+            fe = u8_verdict(a, s, a.seg[s]);
+        }
+        // failing segments: their later spans re-masked by the whole wave
+        uint64_t pend = __ballot(fe != ~0ull);
+        while (pend) {
+            const uint32_t l = (uint32_t)__builtin_ctzll(pend);
+            pend &= pend - 1;
+            const uint32_t seg = (uint32_t)__builtin_amdgcn_readlane((int)s, (int)l);
+            const uint64_t fend = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(fe >> 32), (int)l) << 32 |
+                                  (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)fe, (int)l);
+            u8_remask(a, seg, fend, lane);
+        }
     }
     __syncthreads();
     if (threadIdx.x == 0) {
         if (__hip_atomic_fetch_add(a.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
             __hip_atomic_store(a.count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(a.segcnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(a.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (a.fin_host) {
                 __threadfence_system();

@@ -110,6 +110,8 @@ struct WalkArgs {
     uint32_t* sticky;            // context error bits, never re-armed by a kernel (wsc_error_flags)
     uint32_t* u8host;            // host-visible word set when any UTF-8 item is deferred (cleared by the host)
     uint32_t* win_flag;          // per unmask window: 1 = inside a deferred text item (k_unmask folds its map)
+    uint32_t* u8seglist;         // segments with deferred items (for k_u8_verdict)
+    uint32_t* u8segcnt;          // ... their count (re-armed by k_u8_verdict)
 };
 
 // k_u8_check runs AFTER the unmask: the unmask has already folded every text window that lies
@@ -136,6 +138,8 @@ struct U8Args {
     uint32_t unmasked;           // 1: the wire is already unmasked (in place): items are read with mask 0
     uint8_t* out;                // where the spans' bytes went: the wire (in place) or the arena (COMPACT)
     uint32_t n_segs;
+    const uint32_t* seglist;     // segments with deferred items (the walk's list)
+    uint32_t* segcnt;            // ... their count (re-armed with the item count)
     uint32_t* done;              // k_u8_verdict's finished workgroups (self re-arming)
     uint32_t* fin_host;          // staged pipeline: the last workgroup writes fin_seq here
     uint32_t fin_seq;
