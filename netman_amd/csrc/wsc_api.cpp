@@ -65,7 +65,8 @@ struct wsc_ctx {
     bool fin_pending = false;         // a staged unmask was enqueued without ev_done
     hipStream_t fin_stream = nullptr; // ... on this stream
     bool walk_waited = false;         // wsc_walk_wait saw the last walk complete
-    int u8_chains = 2;                // WSC_U8_CHAINS: independent byte chains per 64-byte lane chunk (1, 2, 4)
+    int u8_chains = 4;                // WSC_U8_CHAINS: independent byte chains per 64-byte lane chunk (1, 2, 4);
+                                      // 4: 1 KiB TEXT 0.241 -> 0.238 ms (A/B, one box), 64 KiB TEXT unchanged
     int unmask_buf = 3;               // WSC_UNMASK_BUF: in-place windows through buffer ops (1 nt, 2 nt sc1, 3 sc0 nt sc1
                                       // stores; 0 = 64-bit global addresses).  3: headline 2,890-2,898 -> 2,911-2,918
                                       // GiB/s (A/B on one box, profiles/r02_unmask_policy.log)
@@ -276,7 +277,8 @@ int wsc_create(int device, const wsc_config* cfg_in, wsc_ctx** out) {
     chk(hipMalloc(&c->tile, c->tile_entries * sizeof(uint32_t)), "hipMalloc tile");
     // a frame is one item up to U8_PIECE (1 GiB), longer ones one per U8_PIECE-aligned boundary
     // inside their payload more, so frames + bytes / U8_PIECE + 1 bounds the total
-    c->u8items_cap = cfg.max_frames + (uint32_t)(cfg.max_batch_bytes / U8_PIECE) + 64;
+    // (+ up to 3 unused pool slots per segment and per > 1 GiB frame: the walk's item pools)
+    c->u8items_cap = cfg.max_frames + 4 * cfg.max_segs + 4 * (uint32_t)(cfg.max_batch_bytes / U8_PIECE) + 64;
     chk(hipMalloc(&c->u8items, (uint64_t)c->u8items_cap * sizeof(U8Item)), "hipMalloc u8items");
     chk(hipMalloc(&c->u8maps, (uint64_t)c->u8items_cap * sizeof(uint64_t)), "hipMalloc u8maps");
     chk(hipMalloc(&c->u8seg, (uint64_t)cfg.max_segs * sizeof(U8Seg)), "hipMalloc u8seg");

@@ -241,6 +241,16 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
     bool u8_pending = false;                      // a text chain has a deferred (chip-wide) part
     uint32_t u8_head = 0xFFFFFFFFu, u8_last = 0xFFFFFFFFu, u8_n = 0;
     bool u8_comp = false;                         // an item whose verdict needs the segment's composition
+    uint32_t pool_next = 0, pool_end = 0;         // the segment's unused item slots
+    auto dead_fill = [&](uint32_t i, uint32_t e) {
+        for (; i < e; ++i)
+            if (i < a.u8items_cap) {
+                U8Item d{};
+                d.seg = U8_DEAD;
+                d.next = 0xFFFFFFFFu;
+                a.u8items[i] = d;
+            }
+    };
     if constexpr (EMIT) {
         u8fail = a.u8info[2 * s];
         u8dfa = a.u8info[2 * s + 1];
@@ -431,33 +441,44 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
                     // inside a text payload lies inside one item (its map is folded by the unmask
                     // that has just unmasked it, win_flag / win_map)
                     const uint32_t pieces = n <= U8_PIECE ? 1u : (uint32_t)((src + n - 1) / U8_PIECE - src / U8_PIECE + 1);
-                    // wave-aggregated allocation when every active lane takes one item (text frames
-                    // <= 16 KiB): one atomic per wave instead of one per frame (262 k same-address
-                    // atomics: the 1 KiB TEXT walk 97 -> 74.5 us with aggregation)
-                    // (the rank counts the lanes below plus those of them that take two pieces)
-                    uint32_t b0;
-                    {
+                    // Item slots come from a per-segment pool: a same-address atomic per frame sat on
+                    // the header chain (1 KiB TEXT: 16 of them per lane, ~3 us each), so a refill
+                    // takes up to 4 slots (the frames of this size the segment still holds),
+                    // wave-aggregated (rank = the slots of the refilling lanes below).  Unused slots
+                    // become dead items at the segment's end (k_u8_check skips them).
+                    if (pool_end - pool_next < pieces) {
+                        dead_fill(pool_next, pool_end);   // (only > 1 GiB frames leave slots here)
+                        const uint64_t more = (seg_end - (src + n)) / (fr.hdr_len + n + 1);
+                        const uint32_t want = pieces + (uint32_t)(more < 3 ? more : 3);
+                        const uint32_t rq = pieces > 4 ? pieces : (want < 4 ? want : 4u);
+                        uint32_t base;
                         const uint64_t act = __ballot(true);
-                        if (__ballot(pieces > 2) == 0) {
-                            const uint64_t two = __ballot(pieces == 2);
+                        if (__ballot(rq > 4) == 0) {
+                            const uint64_t m0 = __ballot(rq & 1), m1 = __ballot(rq & 2), m2 = __ballot(rq & 4);
+                            auto below = [](uint64_t m) {
+                                return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                            };
                             const uint32_t leader = (uint32_t)__builtin_ctzll(act);
-                            const uint32_t rank =
-                                __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u)) +
-                                __builtin_amdgcn_mbcnt_hi((uint32_t)(two >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)two, 0u));
-                            uint32_t base = 0;
+                            uint32_t b = 0;
                             if (lane_id() == leader)
-                                base = __hip_atomic_fetch_add(a.u8count,
-                                                              (uint32_t)(__builtin_popcountll(act) + __builtin_popcountll(two)),
-                                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                            b0 = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)leader) + rank;
+                                b = __hip_atomic_fetch_add(a.u8count,
+                                                           (uint32_t)(__builtin_popcountll(m0) + 2 * __builtin_popcountll(m1) +
+                                                                      4 * __builtin_popcountll(m2)),
+                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            base = (uint32_t)__builtin_amdgcn_readlane((int)b, (int)leader) + below(m0) + 2 * below(m1) +
+                                   4 * below(m2);
                         } else {
-                            b0 = __hip_atomic_fetch_add(a.u8count, pieces, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            base = __hip_atomic_fetch_add(a.u8count, rq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         }
+                        if (base == 0 && a.u8host) {   // the first deferral tells the host the check has work
+                            __hip_atomic_store(a.u8host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                            __threadfence_system();
+                        }
+                        pool_next = base;
+                        pool_end = base + rq;
                     }
-                    if (b0 == 0 && a.u8host) {   // the first deferral tells the host the check has work
-                        __hip_atomic_store(a.u8host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                        __threadfence_system();
-                    }
+                    const uint32_t b0 = pool_next;
+                    pool_next += pieces;
                     // capacity: frames + wire bytes / U8_PIECE + 1 (each aligned boundary inside a
                     // payload adds one piece)
                     const uint64_t W = 1ull << a.win_shift;
@@ -608,6 +629,7 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
         }
     }
 
+    if constexpr (!EMIT) dead_fill(pool_next, pool_end);
     SegCount c;
     bool replay = false;
     c.frames = nf; c.spans0 = ns0; c.spans1 = ns1; c.flags = sflags;
@@ -1151,6 +1173,7 @@ __global__ __launch_bounds__(NT) void k_walk_fused(WalkArgs a) {
 
 // One item's result: no waiting, no counter (the verdict kernel runs after this launch).
 __device__ __forceinline__ void u8_publish(const U8Args& a, uint32_t it, const U8Item& self, uint64_t acc) {
+    if (self.seg == U8_DEAD) return;   // an unused slot of a walk pool
     if (self.kind == U8K_SELF && self.first && self.last) {
         if (u8m_get(acc, 0) != 0)
             __hip_atomic_fetch_min(&a.seg[self.seg].minfail, self.ordinal, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

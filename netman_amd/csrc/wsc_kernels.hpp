@@ -40,6 +40,7 @@ enum : uint32_t { SEGF_UTF8 = 1u, SEGF_U8DEFER = 2u, SEGF_LONG = 4u };
 // maps of the windows inside them, k_u8_check the partial windows at their ends (after the unmask).
 constexpr uint32_t U8_PIECE = 1u << 30;
 enum : uint8_t { U8K_SELF = 0, U8K_PART = 1, U8K_CHAIN = 2 };   // close reasons are SELF items
+constexpr uint32_t U8_DEAD = 0xFFFFFFFFu;   // U8Item.seg of an unused walk-pool slot
 struct U8Item {
     uint64_t src;       // wire offset of the first (masked) byte
     uint32_t len;
