@@ -95,10 +95,13 @@ def _unmask(cfg, i):
     return p, L, mb
 
 
-def test_text_64k_frames_valid_and_invalid(codec_lib):
-    """1,024 connections x 4 x 64 KiB TEXT frames (chip-wide path by default); a 0xFF byte is
-    injected into ~6 % of the frames: each connection must stop at its first bad frame with 1007,
-    leave later frames masked, and match the oracle record for record, byte for byte."""
+@pytest.mark.parametrize("compact", [False, True])
+def test_text_64k_frames_valid_and_invalid(codec_lib, compact):
+    """1,024 connections x 4 x 64 KiB TEXT frames (chip-wide path by default: most bytes are folded
+    by the unmask, the rest by k_u8_check); a 0xFF byte is injected into ~6 % of the frames: each
+    connection must stop at its first bad frame with 1007, leave later frames masked (re-masked
+    after the unmask, in place and in the COMPACT arena), and match the oracle record for record,
+    byte for byte."""
     cfg = synth.text_batch(4096, 65536, 4, seed=synth.SEED_BASE + 31)
     rng = np.random.default_rng(5)
     bad = set(int(x) for x in rng.choice(4096, 256, replace=False))
@@ -108,12 +111,13 @@ def test_text_64k_frames_valid_and_invalid(codec_lib):
         cfg["wire"][p + q] = 0xFF ^ mb[q & 3]
     c = K.Codec(0, max_batch_bytes=len(cfg["wire"]) + 4096, max_segs=2048, max_frames=8192)
     wire = cfg["wire"].copy()
-    res = c.decode_host(wire, cfg["seg_off"])
+    res = c.decode_host(wire, cfg["seg_off"], compact=compact)
     assert int(res.summary["overflow"]) == 0
     n_seg = len(cfg["seg_off"]) - 1
     for s in range(n_seg):
         a, b = int(cfg["seg_off"][s]), int(cfg["seg_off"][s + 1])
-        compare_segment(s, bytes(cfg["wire"][a:b]), a, res, O.run(bytes(cfg["wire"][a:b])), wire_after=wire)
+        compare_segment(s, bytes(cfg["wire"][a:b]), a, res, O.run(bytes(cfg["wire"][a:b])), wire_after=wire,
+                        compact=compact)
     n_err = int((res.seg["status"] == K.SEG_ERROR).sum())
     assert n_err == len({i // 4 for i in bad}) and n_err > 0
     assert int(res.summary["n_frames"]) >= int(res.seg["frame_count"].sum())
@@ -121,8 +125,9 @@ def test_text_64k_frames_valid_and_invalid(codec_lib):
 
 
 def test_text_large_frames_cross_piece_characters(codec_lib):
-    """frames larger than one item (U8_PIECE = 16 KiB) with multi-byte characters across item edges,
-    plus a TEXT chain of big fragments where a 4-byte character straddles two fragments"""
+    """frames larger than several unmask windows with multi-byte characters across window edges
+    (folded by the unmask, partial windows by k_u8_check), plus a TEXT chain of big fragments where
+    a 4-byte character straddles two fragments"""
     e = "😀".encode()                                        # 4 bytes
     body = ("ab" + "é" * 40000 + "x").encode()               # 80003 bytes, 2-byte chars across 65536
     body2 = b"a" * 65535 + e + b"z" * 100                    # emoji straddles a piece edge (65536)
