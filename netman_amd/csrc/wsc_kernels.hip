@@ -6,8 +6,10 @@
 //                         records, payload spans and the window->span index, in one launch.
 //   k_unmask<COMPACT,P,NT> the hot loop (websocket_frame.go:35-39): XOR-unmask every payload span,
 //                         byte-tile decomposed, 16 B per lane access, 1 KiB per wave instruction.
-//   utf8.Valid (websocket_frame.go:71-73, websocket.go:170-172) runs inside the walk's counting
-//   pass on the still-masked wire, so a connection whose text is invalid stops at that frame.
+//   utf8.Valid (websocket_frame.go:71-73, websocket.go:170-172): payloads up to u8_inline_max run
+//   inside the walk's counting pass on the still-masked wire, so a connection whose text is invalid
+//   stops at that frame.  Larger ones are deferred: the unmask folds the windows it unmasks
+//   (wsc_unmask.inl), k_u8_check the partial windows, k_u8_verdict applies 1007 (below).
 #include "wsc_kernels.hpp"
 #include "wsc_dev.hpp"
 #include "wsc_u8.hpp"
@@ -479,8 +481,7 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
                     }
                     const uint32_t b0 = pool_next;
                     pool_next += pieces;
-                    // capacity: frames + wire bytes / U8_PIECE + 1 (each aligned boundary inside a
-                    // payload adds one piece)
+                    // capacity (wsc_create): frames + 4 x segments (pool slots) + 4 x bytes / U8_PIECE
                     const uint64_t W = 1ull << a.win_shift;
                     for (uint32_t p = 0; p < pieces; ++p) {
                         const uint32_t idx = b0 + p;
