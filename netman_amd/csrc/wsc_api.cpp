@@ -538,7 +538,8 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
         else if (c->u8_chains == 4) hipLaunchKernelGGL(k_u8_check<4>, ug, dim3(256), 0, st, ua);
         else hipLaunchKernelGGL(k_u8_check<2>, ug, dim3(256), 0, st, ua);
         HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL(k_u8_verdict, dim3(std::min<uint32_t>((n + 255) / 256, (uint32_t)c->n_cu * 2)), dim3(256), 0, st, ua);
+        // (grid-stride over the listed segments; a small grid: an empty launch costs ~2 us)
+        hipLaunchKernelGGL(k_u8_verdict, dim3(std::min<uint32_t>((n + 255) / 256, (uint32_t)c->n_cu / 2)), dim3(256), 0, st, ua);
         HIP_TRY(hipGetLastError());
     }
     rec(3);

@@ -1469,7 +1469,11 @@ __global__ __launch_bounds__(256) void k_u8_verdict(U8Args a) {
     // verdicts are not applied -- the failing frame or its later spans may lie past the capacity
     const bool ovf = a.summary->overflow != 0;
     const uint32_t lane = threadIdx.x & 63;
-    const uint32_t nseg = *a.segcnt < a.n_segs ? *a.segcnt : a.n_segs;   // segments with deferred items
+    const uint32_t listed = *a.segcnt;
+    // nothing deferred (a binary batch through wsc_decode): nothing to decide, nothing to re-arm,
+    // nobody to signal -- every workgroup sees the same words and leaves without the counter
+    if (listed == 0 && *a.count == 0 && a.fin_host == nullptr) return;
+    const uint32_t nseg = listed < a.n_segs ? listed : a.n_segs;   // segments with deferred items
     // grid-stride over the list, whole waves per step (the re-mask below is wave-cooperative)
     for (uint32_t b = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); b < nseg && !ovf; b += gridDim.x * blockDim.x) {
         const uint32_t i = b + lane;
