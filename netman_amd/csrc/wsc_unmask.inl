@@ -309,13 +309,38 @@ struct U8Block {
     uint4 stage[4][U8_STAGE];
     uint32_t state;   // 0 none, 1 building, 2 ready
 };
+// (namespace scope: allocated only in the kernels that reach it, the U8 instantiations)
+__shared__ U8Block g_u8b;
+
+// The fold of a window whose first 4 KiB the caller has written to the wave's stage: tables (built
+// once per workgroup), then the map of every 4 KiB group.  COMPACT calls it out of line: its window
+// loop keeps more registers live, and the fold inlined there pushed it past 128 VGPRs (spill)
 template <int P>
-__device__ __forceinline__ void fold_text_window(U8Block& b, const u32x4 (&v)[P], uint32_t key, U8Win u8w,
-                                                           uint64_t win, uint32_t lane) {
-    uint4* sw = b.stage[(threadIdx.x >> 6) & 3];
+__device__ __forceinline__ void fold_staged(const u32x4* v, uint32_t key, U8Win u8w, uint64_t win, uint32_t lane);
+static __device__ __attribute__((noinline)) void fold_staged4(U8Win u8w, uint64_t win, uint32_t lane);
+template <bool OUTLINE, int P>
+__device__ __forceinline__ void fold_text_window(const u32x4 (&v)[P], uint32_t key, U8Win u8w, uint64_t win,
+                                                 uint32_t lane) {
+    uint4* sw = g_u8b.stage[(threadIdx.x >> 6) & 3];
     // the first 4 KiB goes to the wave's stage before anything else: the unmasked registers are
-    // dead from here on (the table build below would otherwise hold them)
-    auto stage_write = [&](int g) {
+    // dead from here on (the table build would otherwise hold them)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t o = 1024u * k + 16u * lane;
+        const u32x4 x = v[k] ^ key;
+        sw[(o >> 6) * 5 + ((o >> 4) & 3)] = make_uint4(x[0], x[1], x[2], x[3]);
+    }
+    if constexpr (OUTLINE && P == 4) {
+        fold_staged4(u8w, win, lane);
+    } else {
+        fold_staged<P>(v, key, u8w, win, lane);
+    }
+}
+template <int P>
+__device__ __forceinline__ void fold_staged(const u32x4* v, uint32_t key, U8Win u8w, uint64_t win, uint32_t lane) {
+    U8Block& b = g_u8b;
+    uint4* sw = b.stage[(threadIdx.x >> 6) & 3];
+    auto stage_write = [&](int g) {   // groups after the first (P = 8)
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const uint32_t o = 1024u * k + 16u * lane;
@@ -323,7 +348,6 @@ __device__ __forceinline__ void fold_text_window(U8Block& b, const u32x4 (&v)[P]
             sw[(o >> 6) * 5 + ((o >> 4) & 3)] = make_uint4(x[0], x[1], x[2], x[3]);
         }
     };
-    stage_write(0);
     uint32_t prev = 0;
     if (lane == 0) prev = __hip_atomic_compare_exchange_strong(&b.state, &prev, 1u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                                __HIP_MEMORY_SCOPE_WORKGROUP) ? 0u : prev;
@@ -359,6 +383,10 @@ __device__ __forceinline__ void fold_text_window(U8Block& b, const u32x4 (&v)[P]
     }
 }
 
+static __device__ __attribute__((noinline)) void fold_staged4(U8Win u8w, uint64_t win, uint32_t lane) {
+    fold_staged<4>(nullptr, 0u, u8w, win, lane);
+}
+
 // NT bit 0: non-temporal loads, bit 1: non-temporal stores.  In place `src` is unused (dst is
 // both source and destination) so the two restrict pointers never alias in an access; COMPACT
 // reads `src` (the wire) and writes `dst` (the arena).  `total` = wire bytes.
@@ -373,10 +401,9 @@ __device__ __forceinline__ void unmask_all(uint8_t* __restrict__ dst, const uint
     static_assert(NT < 16 || !COMPACT, "buffer-instruction windows are the in-place path");
     __shared__ u32x4 pm[17];
     // U8: the launch may meet flagged text windows (the host could not rule them out); binary
-    // batches whose walk the host has seen use the variant without the fold and its LDS
-    __shared__ std::conditional_t<U8, U8Block, uint32_t> u8b;
+    // batches whose walk the host has seen use the variant without the fold and its LDS (g_u8b)
     if (threadIdx.x < 17) pm[threadIdx.x] = prefix_mask16(threadIdx.x);
-    if constexpr (U8) if (threadIdx.x == 0) u8b.state = 0;
+    if constexpr (U8) if (threadIdx.x == 0) g_u8b.state = 0;
     __syncthreads();
     // re-arm the walk's look-back state for the next decode (this launch is ordered after it):
     // lb_state[0] = ticket, [1] = timeout flag, [3 ...] = per-block flags ([2], the UTF-8 item
@@ -430,7 +457,7 @@ __device__ __forceinline__ void unmask_all(uint8_t* __restrict__ dst, const uint
 #pragma unroll
                 for (int k = 0; k < P; ++k) st16v<NT>(dst + wbase + k * 1024u + lofs, v[k] ^ s0.key);
             }
-            if constexpr (U8) if (text) fold_text_window<P>(u8b, v, s0.key, u8w, win, lane);
+            if constexpr (U8) if (text) fold_text_window<COMPACT, P>(v, s0.key, u8w, win, lane);
             continue;
         }
         // Several spans overlap the window (small frames) or it holds a frame edge: lane-parallel
