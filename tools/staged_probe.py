@@ -34,8 +34,16 @@ def main():
         pair.append((c, c.make_batch(t["wire"], t["seg_off"], None, t["st"], t["so"], t["fr"], t["sm"]), t))
     torch.cuda.synchronize()
     c0 = pair[0][0]
-    ws = c0.stream_create(K.cu_mask(range(wcus), n_cu))
-    us = c0.stream_create(K.cu_mask(range(wcus, n_cu), n_cu) if rest else None)
+    # PATTERN=stride: the walk's CUs are spread over the CU index space (i % 8 < wcus * 8 / n_cu)
+    # instead of the first wcus indices (A/B for the XCD layout of the CU mask)
+    if os.environ.get("PATTERN") == "stride":
+        k8 = max(1, wcus * 8 // n_cu)
+        wl = [i for i in range(n_cu) if i % 8 < k8]
+    else:
+        wl = list(range(wcus))
+    rl = [i for i in range(n_cu) if i not in set(wl)]
+    ws = c0.stream_create(K.cu_mask(wl, n_cu))
+    us = c0.stream_create(K.cu_mask(rl, n_cu) if rest else None)
 
     def run(k):
         for i in range(k):
