@@ -49,7 +49,7 @@ def parse():
                          "header walk of batch k+1 overlaps the unmask of batch k")
     ap.add_argument("--walk-cus", type=int, default=16,
                     help="split pipeline (wsc_decode_split): the header walk runs on a stream masked to this "
-                         "many CUs, the UTF-8 check + unmask on --unmask-streams streams over every CU "
+                         "many CUs, the unmask (+ UTF-8 check when text was deferred) on --unmask-streams streams over every CU "
                          "(0 = every stage of a batch in order on its own stream)")
     ap.add_argument("--unmask-streams", type=int, default=1)
     ap.add_argument("--staged", type=int, default=1,
@@ -282,7 +282,7 @@ def main():
                    "frames_per_gpu": a.frames, "frame_bytes": a.frame_bytes,
                    "segments_per_gpu": n_segs, "parallelism": f"shard{world}",
                    "batches_in_flight": P,
-                   "pipeline": (f"split: walk on a stream masked to {a.walk_cus} CUs, UTF-8 check + unmask on "
+                   "pipeline": (f"split: walk on a stream masked to {a.walk_cus} CUs, unmask (+ UTF-8 check when text was deferred) on "
                                 f"{len(unmask_st)} stream(s) over "
                                 f"{'the other ' + str(n_cu - a.walk_cus) if a.unmask_rest else 'all ' + str(n_cu)} CUs") if split
                                else "each batch in order on its own stream"},
