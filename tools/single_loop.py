@@ -20,6 +20,7 @@ def main():
     iters = int(sys.argv[2]) if len(sys.argv) > 2 else 30
     cfg = {"head": lambda: synth.uniform_batch(16384, 65536, 4, seed=synth.SEED_BASE + 1),
            "c1": lambda: synth.uniform_batch(1 << 20, 1024, 16, seed=synth.SEED_BASE + 1),
+           "c11": lambda: synth.uniform_batch(1 << 20, 1024, 1, seed=synth.SEED_BASE + 1),
            "c2": lambda: synth.mixed_batch(),
            "t64": lambda: synth.text_batch(16384, 65536, 4, seed=synth.SEED_BASE + 7),
            "t1": lambda: synth.text_batch(262144, 1024, 16, seed=synth.SEED_BASE + 8)}[which]()
