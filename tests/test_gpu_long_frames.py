@@ -126,3 +126,79 @@ def test_length_2_40_and_more_is_too_large(codec_lib):
 def test_max_frame_len_limit(codec_lib):
     with pytest.raises(K.WscError):
         K.Codec(0, max_batch_bytes=1 << 20, max_segs=4, max_frames=64, max_frame_len=1 << 40)
+
+
+@pytest.mark.parametrize("compact,bad", [(False, False), (False, True), (True, True)])
+def test_text_frame_over_1gib(codec_lib, compact, bad):
+    """a TEXT frame of 2 GiB + 4100 B: three UTF-8 items cut at 1 GiB-aligned wire offsets with
+    2-byte characters straddling every cut, most of it folded window by window inside the unmask,
+    the item ends in k_u8_check, the three items composed by k_u8_verdict.  With one 0xFF byte at
+    1.5 GiB the connection must stop at that frame with 1007 (websocket_frame.go:71-73,
+    epoll.go:126-127) and the TEXT frame after it must be left masked (re-masked after the unmask);
+    valid, the frame after it is a Message.  The payload is built and checked on the device."""
+    torch = pytest.importorskip("torch")
+    dev = torch.device("cuda:0")
+    big = (2 << 30) + 4100
+    mask_big = 0x5EC0DE11
+    pre = synth.frame(1, "pré".encode(), mask=0x01020304)
+    post = synth.frame(1, "après".encode(), mask=0x0BADF00D)
+    hb = _hdr64(1, big, mask_big)
+    n_bytes = len(pre) + len(hb) + big + len(post)
+    c = K.Codec(0, max_batch_bytes=n_bytes + 4096, max_segs=4, max_frames=64, max_frame_len=(1 << 40) - 1)
+    wire = torch.empty(n_bytes + 64, dtype=torch.uint8, device=dev)
+    head = np.frombuffer(pre + hb, dtype=np.uint8)
+    wire[:len(head)] = torch.from_numpy(head.copy()).to(dev)
+    p0 = len(head)
+    bad_at = (3 << 29) + 1
+
+    def text(o, n):   # "é" = C3 A9 repeated (payload offset o is even at every chunk start)
+        i = torch.arange(o, o + n, dtype=torch.int64, device=dev)
+        t = torch.where((i & 1) == 0, torch.tensor(0xC3, dtype=torch.uint8, device=dev),
+                        torch.tensor(0xA9, dtype=torch.uint8, device=dev))
+        if bad and o <= bad_at < o + n:
+            t[bad_at - o] = 0xFF
+        return t
+
+    for o in range(0, big, CHUNK):
+        n = min(CHUNK, big - o)
+        wire[p0 + o:p0 + o + n] = text(o, n) ^ _mask_tile(torch, dev, mask_big, n)
+    tail = np.frombuffer(post, dtype=np.uint8)
+    wire[p0 + big:p0 + big + len(tail)] = torch.from_numpy(tail.copy()).to(dev)
+    seg_off = torch.tensor([0, n_bytes], dtype=torch.int64, device=dev)
+    st_out = torch.zeros(16, dtype=torch.uint8, device=dev)
+    seg_out = torch.zeros(32, dtype=torch.uint8, device=dev)
+    frames = torch.zeros(64 * 32, dtype=torch.uint8, device=dev)
+    summ = torch.zeros(32, dtype=torch.uint8, device=dev)
+    arena = torch.zeros(n_bytes + 64, dtype=torch.uint8, device=dev) if compact else None
+    frame_dst = torch.zeros(64, dtype=torch.int64, device=dev) if compact else None
+    b = c.make_batch(wire, seg_off, None, st_out, seg_out, frames, summ, compact=compact, arena=arena,
+                     frame_dst=frame_dst, n_bytes=n_bytes)
+    c.decode(b)
+    c.sync()
+    sm = summ.cpu().numpy().copy().view(K.SUMMARY_DTYPE)[0]
+    assert K.Codec.summary_status(sm) == K.WSC_OK and int(sm["n_frames"]) == 3
+    seg = seg_out.cpu().numpy().copy().view(K.SEG_RESULT_DTYPE)[0]
+    fr = frames.cpu().numpy().copy().view(K.FRAME_DTYPE)[:3]
+    assert K.frame_len(fr[1]) == big and int(fr[1]["opcode"]) == 1
+    fd = frame_dst.cpu().numpy().copy().view(np.uint64)[:3] if compact else None
+    out = arena if compact else wire
+    base = int(fd[1]) if compact else p0
+    for o in range(0, big, CHUNK):   # the big payload is unmasked either way (nextFrame unmasks first)
+        n = min(CHUNK, big - o)
+        assert torch.equal(out[base + o:base + o + n], text(o, n)), f"big payload at {o}"
+    if bad:
+        assert int(seg["status"]) == K.SEG_ERROR and int(seg["close_code"]) == 1007
+        assert int(seg["frame_count"]) == 2 and int(fr[1]["kind"]) == K.FK_ERROR
+        assert int(seg["consumed"]) == p0 + big
+        # the frame after the failing one is never read by the reference: its payload stays masked
+        pl = len("après".encode())
+        masked = wire[n_bytes - pl:n_bytes].cpu().numpy().tobytes()
+        assert masked == post[-pl:], "payload after the failing frame must stay masked (in place)"
+        if compact:   # in the arena the later payload is copied masked, as the key-0 span did
+            assert arena[int(fd[2]):int(fd[2]) + pl].cpu().numpy().tobytes() == post[-pl:]
+    else:
+        assert int(seg["status"]) == K.SEG_OPEN and int(seg["frame_count"]) == 3
+        assert [int(x) for x in fr["kind"]] == [K.FK_MESSAGE] * 3
+        pl = len("après".encode())
+        assert wire[n_bytes - pl:n_bytes].cpu().numpy().tobytes() == "après".encode()
+    c.close()
