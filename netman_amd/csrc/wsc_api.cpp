@@ -414,6 +414,7 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     wa.u8host = c->hflag;
     wa.win_flag = c->win_flag;
     wa.u8seglist = c->u8seglist;
+    wa.compact = compact ? 1u : 0u;
     wa.u8segcnt = c->u8done + 32;
 
     // walk geometry: the fused walk with blocks that fill the CUs once (64 lanes for up to 64

@@ -785,7 +785,7 @@ __global__ __launch_bounds__(256) void k_walk_count(WalkArgs a) {
 
 // one block: thread t owns the SCAN_PER consecutive block totals starting at t * SCAN_PER (all its
 // loads in flight at once), scans them in registers, then one block-wide scan of the threads' sums
-constexpr uint32_t SCAN_PER = 8;
+constexpr uint32_t SCAN_PER = 16;
 __global__ __launch_bounds__(256) void k_walk_scan(WalkArgs a, uint32_t n_blocks) {
     __shared__ SegCount sh_wave[4];
     __shared__ SegCount sh_carry;
@@ -814,8 +814,9 @@ __global__ __launch_bounds__(256) void k_walk_scan(WalkArgs a, uint32_t n_blocks
     if (threadIdx.x == 0) {
         const SegCount tt = sh_carry;
         wsc_summary sm;
-        sm.data_bytes = tt.bytes0;
-        sm.ctrl_bytes = tt.bytes1;
+        const bool compact = a.compact != 0;   // (as the fused walk reports: arena bytes, COMPACT only)
+        sm.data_bytes = compact ? tt.bytes0 : 0;
+        sm.ctrl_bytes = compact ? tt.bytes1 : 0;
         sm.n_frames = tt.frames;
         // spans past the capacity were never written: the unmask must not read them (an overflowed
         // batch unmasks the spans that fit; n_spans = spans unmasked)

@@ -113,6 +113,7 @@ struct WalkArgs {
     uint32_t* win_flag;          // per unmask window: 1 = inside a deferred text item (k_unmask folds its map)
     uint32_t* u8seglist;         // segments with deferred items (for k_u8_verdict)
     uint32_t* u8segcnt;          // ... their count (re-armed by k_u8_verdict)
+    uint32_t compact;            // WSC_F_COMPACT (k_walk_scan: the other kernels are templated on it)
 };
 
 // k_u8_check runs AFTER the unmask: the unmask has already folded every text window that lies
