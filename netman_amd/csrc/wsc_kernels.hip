@@ -603,6 +603,9 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
     uint64_t stride = 0;
     bool go = status == WSC_SEG_OPEN;
     while (go) {
+        // fewer than 2 bytes left: `step` would stop on them anyway -- no round trip for a header
+        // that cannot be there (every segment's walk used to end with one)
+        if (seg_end - pos < 2) break;
         // one memory round trip: the next header + SPEC_D-1 speculative ones
         uint4 hc[SPEC_D];
         uint64_t hp[SPEC_D];
