@@ -317,7 +317,7 @@ __shared__ U8Block g_u8b;
 // loop keeps more registers live, and the fold inlined there pushed it past 128 VGPRs (spill)
 template <int P>
 __device__ __forceinline__ void fold_staged(const u32x4* v, uint32_t key, U8Win u8w, uint64_t win, uint32_t lane);
-static __device__ __attribute__((noinline)) void fold_staged4(U8Win u8w, uint64_t win, uint32_t lane);
+static inline __device__ __attribute__((noinline)) void fold_staged4(U8Win u8w, uint64_t win, uint32_t lane);
 template <bool OUTLINE, int P>
 __device__ __forceinline__ void fold_text_window(const u32x4 (&v)[P], uint32_t key, U8Win u8w, uint64_t win,
                                                  uint32_t lane) {
@@ -383,7 +383,7 @@ __device__ __forceinline__ void fold_staged(const u32x4* v, uint32_t key, U8Win 
     }
 }
 
-static __device__ __attribute__((noinline)) void fold_staged4(U8Win u8w, uint64_t win, uint32_t lane) {
+static inline __device__ __attribute__((noinline)) void fold_staged4(U8Win u8w, uint64_t win, uint32_t lane) {
     fold_staged<4>(nullptr, 0u, u8w, win, lane);
 }
 
