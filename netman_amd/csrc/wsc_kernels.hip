@@ -1334,20 +1334,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
     // Other units walk their items' steps in order, the next step's loads -- the next item's first
     // step too -- issued before the current step is folded.
     auto unit_large = [&](uint32_t i0, uint32_t cnt) {
-        const U8Item x0 = a.items[i0];
-        u32x4 nxt[4];
-        {
-            const Geo g0 = geo(x0);
-            const uint32_t b = first_step(g0, x0.len);
-            if (b != NONE) fetch(x0, b, b < g0.hl ? g0.hl : x0.len, nxt);
-        }
-        U8Item item2 = x0;   // (items re-read by index: no dynamically indexed register array)
+        // (prefetch within an item only: carrying the next item's geometry and first step across
+        // the fold held ~15 more VGPRs, past 128)
         for (uint32_t j = 0; j < cnt; ++j) {
-            const U8Item item = item2;
-            if (j + 1 < cnt) item2 = a.items[i0 + j + 1];
+            const U8Item item = a.items[i0 + j];
             const Geo g = geo(item);
-            const Geo g2 = geo(item2);
-            const uint32_t f2 = j + 1 < cnt ? first_step(g2, item2.len) : NONE;
+            uint32_t b0 = first_step(g, item.len);
+            u32x4 nxt[4];
+            if (b0 != NONE) fetch(item, b0, b0 < g.hl ? g.hl : item.len, nxt);
             // the windows between head and tail, folded by the unmask: each lane composes a run
             // of ceil(nwin / 64) of them, the wave composes the lanes in order
             uint64_t mids = u8m_id();
@@ -1360,15 +1354,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
             }
             uint64_t acc = u8m_id();
             bool mids_in = false;
-            uint32_t b0 = first_step(g, item.len);
-            if (b0 == NONE && f2 != NONE) fetch(item2, f2, f2 < g2.hl ? g2.hl : item2.len, nxt);
             while (b0 != NONE) {
                 u32x4 cur4[4];
 #pragma unroll
                 for (int k = 0; k < 4; ++k) cur4[k] = nxt[k];
                 const uint32_t nb = next_step(g, item.len, b0);
                 if (nb != NONE) fetch(item, nb, nb < g.hl ? g.hl : item.len, nxt);
-                else if (f2 != NONE) fetch(item2, f2, f2 < g2.hl ? g2.hl : item2.len, nxt);
                 u8_restage(sw, cur4, lane);
                 const uint32_t lim = b0 < g.hl ? g.hl : item.len;
                 bool plain;
