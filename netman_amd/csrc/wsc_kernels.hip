@@ -274,6 +274,94 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
         if (have_span) pend = fr.hdr_off + fr.hdr_len + plen;
     };
 
+    // A text payload validated chip-wide (after the unmask): item slots from the segment's pool,
+    // window flags for the unmask's fold, the segment's item list.  Counting pass only.
+    auto defer = [&](uint64_t src, uint64_t n, uint32_t mk, bool part, bool chain, uint32_t hl) {
+        // large text (or a chain already deferred): validated chip-wide by k_u8_check,
+        // which also applies the verdict; the walk goes on as if it were valid
+        const uint8_t kind = part ? U8K_PART : (chain ? U8K_CHAIN : U8K_SELF);
+        const uint8_t s_in = (part || chain) ? (u8_pending ? 0xFF : (uint8_t)u8dfa) : 0;
+        // a payload up to U8_PIECE is one piece; longer ones are cut at absolute
+        // U8_PIECE-aligned wire offsets.  Either way every unmask window that lies
+        // inside a text payload lies inside one item (its map is folded by the unmask
+        // that has just unmasked it, win_flag / win_map)
+        const uint32_t pieces = n <= U8_PIECE ? 1u : (uint32_t)((src + n - 1) / U8_PIECE - src / U8_PIECE + 1);
+        // Item slots come from a per-segment pool: a same-address atomic per frame sat on
+        // the header chain (1 KiB TEXT: 16 of them per lane, ~3 us each), so a refill
+        // takes up to 4 slots (the frames of this size the segment still holds),
+        // wave-aggregated (rank = the slots of the refilling lanes below).  Unused slots
+        // become dead items at the segment's end (k_u8_check skips them).
+        if (pool_end - pool_next < pieces) {
+            dead_fill(pool_next, pool_end);   // (only > 1 GiB frames leave slots here)
+            const uint64_t more = (seg_end - (src + n)) / (hl + n + 1);
+            const uint32_t want = pieces + (uint32_t)(more < 3 ? more : 3);
+            const uint32_t rq = pieces > 4 ? pieces : (want < 4 ? want : 4u);
+            uint32_t base;
+            const uint64_t act = __ballot(true);
+            if (__ballot(rq > 4) == 0) {
+                const uint64_t m0 = __ballot(rq & 1), m1 = __ballot(rq & 2), m2 = __ballot(rq & 4);
+                auto below = [](uint64_t m) {
+                    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                };
+                const uint32_t leader = (uint32_t)__builtin_ctzll(act);
+                uint32_t b = 0;
+                if (lane_id() == leader)
+                    b = __hip_atomic_fetch_add(a.u8count,
+                                               (uint32_t)(__builtin_popcountll(m0) + 2 * __builtin_popcountll(m1) +
+                                                          4 * __builtin_popcountll(m2)),
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                base = (uint32_t)__builtin_amdgcn_readlane((int)b, (int)leader) + below(m0) + 2 * below(m1) +
+                       4 * below(m2);
+            } else {
+                base = __hip_atomic_fetch_add(a.u8count, rq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if (base == 0 && a.u8host) {   // the first deferral tells the host the check has work
+                __hip_atomic_store(a.u8host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __threadfence_system();
+            }
+            pool_next = base;
+            pool_end = base + rq;
+        }
+        const uint32_t b0 = pool_next;
+        pool_next += pieces;
+        // capacity (wsc_create): frames + 4 x segments (pool slots) + 4 x bytes / U8_PIECE
+        const uint64_t W = 1ull << a.win_shift;
+        for (uint32_t p = 0; p < pieces; ++p) {
+            const uint32_t idx = b0 + p;
+            U8Item it;
+            const uint64_t ps = p == 0 ? src : (src / U8_PIECE + p) * U8_PIECE;
+            const uint64_t pe0 = pieces == 1 ? src + n : (src / U8_PIECE + p + 1) * U8_PIECE;
+            const uint64_t pe = pe0 < src + n ? pe0 : src + n;
+            it.src = ps;
+            it.len = (uint32_t)(pe - ps);
+            it.mask = rotr32(mk, 8u * (uint32_t)((ps - src) & 3));   // phase 0 at the piece
+            if (a.win_flag) {   // windows inside the piece: folded by the unmask
+                uint64_t wi = (ps + W - 1) >> a.win_shift;
+                const uint64_t we = pe >> a.win_shift;
+                for (; wi < we && (wi & 3); ++wi) a.win_flag[wi] = 1u;
+                for (; wi + 4 <= we; wi += 4) *reinterpret_cast<uint4*>(a.win_flag + wi) = make_uint4(1, 1, 1, 1);
+                for (; wi < we; ++wi) a.win_flag[wi] = 1u;
+            }
+            it.seg = s;
+            it.ordinal = nf;
+            it.next = 0xFFFFFFFFu;
+            it.kind = kind;
+            it.s_in = s_in;
+            it.first = p == 0;
+            it.last = p + 1 == pieces;
+            if (idx < a.u8items_cap) {
+                a.u8items[idx] = it;
+                if (u8_last != 0xFFFFFFFFu) a.u8items[u8_last].next = idx;
+                else u8_head = idx;
+                u8_last = idx;
+                u8_n += 1;
+            }
+        }
+        if (part || chain || pieces != 1) u8_comp = true;
+        if (part) u8_pending = true;
+        if (chain) u8_pending = false;   // the message completes here
+    };
+
     // One frame at `pos` from its 32-byte header window; returns false when the walk stops
     // (terminal status, or the frame is incomplete and is carried to the next batch).
     auto step = [&](const uint4& hd) -> bool {
@@ -434,89 +522,7 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
                     const bool skip = fr.mode == 1 && u8_run_masked(0, w, src, n, mk) != 0;
                     if (!skip && u8_run_masked(0, w, src + 2, n - 2, rotr32(mk, 16)) != 0) u8fail = nf;
                 } else if (n > a.u8_inline_max || ((part || chain) && u8_pending)) {
-                    // large text (or a chain already deferred): validated chip-wide by k_u8_check,
-                    // which also applies the verdict; the walk goes on as if it were valid
-                    const uint8_t kind = part ? U8K_PART : (chain ? U8K_CHAIN : U8K_SELF);
-                    const uint8_t s_in = (part || chain) ? (u8_pending ? 0xFF : (uint8_t)u8dfa) : 0;
-                    // a payload up to U8_PIECE is one piece; longer ones are cut at absolute
-                    // U8_PIECE-aligned wire offsets.  Either way every unmask window that lies
-                    // inside a text payload lies inside one item (its map is folded by the unmask
-                    // that has just unmasked it, win_flag / win_map)
-                    const uint32_t pieces = n <= U8_PIECE ? 1u : (uint32_t)((src + n - 1) / U8_PIECE - src / U8_PIECE + 1);
-                    // Item slots come from a per-segment pool: a same-address atomic per frame sat on
-                    // the header chain (1 KiB TEXT: 16 of them per lane, ~3 us each), so a refill
-                    // takes up to 4 slots (the frames of this size the segment still holds),
-                    // wave-aggregated (rank = the slots of the refilling lanes below).  Unused slots
-                    // become dead items at the segment's end (k_u8_check skips them).
-                    if (pool_end - pool_next < pieces) {
-                        dead_fill(pool_next, pool_end);   // (only > 1 GiB frames leave slots here)
-                        const uint64_t more = (seg_end - (src + n)) / (fr.hdr_len + n + 1);
-                        const uint32_t want = pieces + (uint32_t)(more < 3 ? more : 3);
-                        const uint32_t rq = pieces > 4 ? pieces : (want < 4 ? want : 4u);
-                        uint32_t base;
-                        const uint64_t act = __ballot(true);
-                        if (__ballot(rq > 4) == 0) {
-                            const uint64_t m0 = __ballot(rq & 1), m1 = __ballot(rq & 2), m2 = __ballot(rq & 4);
-                            auto below = [](uint64_t m) {
-                                return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                            };
-                            const uint32_t leader = (uint32_t)__builtin_ctzll(act);
-                            uint32_t b = 0;
-                            if (lane_id() == leader)
-                                b = __hip_atomic_fetch_add(a.u8count,
-                                                           (uint32_t)(__builtin_popcountll(m0) + 2 * __builtin_popcountll(m1) +
-                                                                      4 * __builtin_popcountll(m2)),
-                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                            base = (uint32_t)__builtin_amdgcn_readlane((int)b, (int)leader) + below(m0) + 2 * below(m1) +
-                                   4 * below(m2);
-                        } else {
-                            base = __hip_atomic_fetch_add(a.u8count, rq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        }
-                        if (base == 0 && a.u8host) {   // the first deferral tells the host the check has work
-                            __hip_atomic_store(a.u8host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                            __threadfence_system();
-                        }
-                        pool_next = base;
-                        pool_end = base + rq;
-                    }
-                    const uint32_t b0 = pool_next;
-                    pool_next += pieces;
-                    // capacity (wsc_create): frames + 4 x segments (pool slots) + 4 x bytes / U8_PIECE
-                    const uint64_t W = 1ull << a.win_shift;
-                    for (uint32_t p = 0; p < pieces; ++p) {
-                        const uint32_t idx = b0 + p;
-                        U8Item it;
-                        const uint64_t ps = p == 0 ? src : (src / U8_PIECE + p) * U8_PIECE;
-                        const uint64_t pe0 = pieces == 1 ? src + n : (src / U8_PIECE + p + 1) * U8_PIECE;
-                        const uint64_t pe = pe0 < src + n ? pe0 : src + n;
-                        it.src = ps;
-                        it.len = (uint32_t)(pe - ps);
-                        it.mask = rotr32(mk, 8u * (uint32_t)((ps - src) & 3));   // phase 0 at the piece
-                        if (a.win_flag) {   // windows inside the piece: folded by the unmask
-                            uint64_t wi = (ps + W - 1) >> a.win_shift;
-                            const uint64_t we = pe >> a.win_shift;
-                            for (; wi < we && (wi & 3); ++wi) a.win_flag[wi] = 1u;
-                            for (; wi + 4 <= we; wi += 4) *reinterpret_cast<uint4*>(a.win_flag + wi) = make_uint4(1, 1, 1, 1);
-                            for (; wi < we; ++wi) a.win_flag[wi] = 1u;
-                        }
-                        it.seg = s;
-                        it.ordinal = nf;
-                        it.next = 0xFFFFFFFFu;
-                        it.kind = kind;
-                        it.s_in = s_in;
-                        it.first = p == 0;
-                        it.last = p + 1 == pieces;
-                        if (idx < a.u8items_cap) {
-                            a.u8items[idx] = it;
-                            if (u8_last != 0xFFFFFFFFu) a.u8items[u8_last].next = idx;
-                            else u8_head = idx;
-                            u8_last = idx;
-                            u8_n += 1;
-                        }
-                    }
-                    if (part || chain || pieces != 1) u8_comp = true;
-                    if (part) u8_pending = true;
-                    if (chain) u8_pending = false;   // the message completes here
+                    defer(src, n, mk, part, chain, fr.hdr_len);
                 } else {
                     bool ok = true;
                     if (part) u8dfa = u8_run_masked(u8dfa, w, src, n, mk);
@@ -552,10 +558,13 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
     // Fast path (both passes): a complete, masked FIN BIN frame (0x82) while no fragmented
     // message is open (cont == 0) is always Message{MsgID: msg, Opcode: 2} (websocket.go:142-146,
     // websocket_frame.go:52-91; messageMode 2 -> 0, msgID + 1): its record is written without the
-    // general state machine.  Everything else goes through `step`.
+    // general state machine.  So is a FIN TEXT frame (0x81) whose payload is validated chip-wide
+    // (above u8_inline_max, one item): Opcode 1, its UTF-8 verdict applied later.  Everything else
+    // goes through `step`.
     auto fast = [&](const uint4& hd) -> bool {
         const uint32_t b0 = hd.x & 0xFFu, b1 = (hd.x >> 8) & 0xFFu;
-        if (b0 != 0x82u || !(b1 & 0x80u) || cont != 0) return false;
+        if ((b0 != 0x82u && b0 != 0x81u) || !(b1 & 0x80u) || cont != 0) return false;
+        const bool text = b0 == 0x81u;
         const uint32_t len7 = b1 & 0x7Fu;
         uint64_t plen;
         uint32_t mask, hl;
@@ -575,6 +584,9 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
             hl = 14;
         }
         if (plen > a.max_frame_len || seg_end - pos < hl + plen) return false;
+        // TEXT: only a whole message that is validated chip-wide (one item); small ones are
+        // checked inline by `step`
+        if (text && (plen <= a.u8_inline_max || plen > U8_PIECE)) return false;
         wsc_frame fr;
         fr.hdr_off = pos;
         fr.payload_len = (uint32_t)plen;
@@ -582,13 +594,17 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
         fr.mask = mask;
         fr.seg = s;
         fr.msg_id = msg;
-        fr.opcode = 2;
+        fr.opcode = text ? 1 : 2;
         fr.fin = 1;
         fr.kind = WSC_FK_MESSAGE;
-        fr.mode = 2;
+        fr.mode = text ? 1 : 2;
         fr.err = 0;
         fr.hdr_len = (uint8_t)hl;
-        fr.flags = WSC_FF_UNMASKED;
+        fr.flags = text ? (WSC_FF_UNMASKED | WSC_FF_U8_SELF) : WSC_FF_UNMASKED;
+        if (text) {
+            sflags |= SEGF_UTF8;
+            if constexpr (!EMIT) defer(pos + hl, plen, mask, false, false, hl);
+        }
         const bool have_span = plen > 0;
         if constexpr (EMIT) emit_frame<COMPACT>(a, e, fr, plen, have_span, 0);
         else record(fr, have_span, 0, true, plen);
