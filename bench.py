@@ -62,7 +62,24 @@ def parse():
                     help="skip the BASELINE configs[3] line (1 M x 4 KiB frames per GPU dealt round-robin)")
     ap.add_argument("--no-other-configs", action="store_true",
                     help="skip the device-time lines for BASELINE.json configs[1], [2], [4]")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="control path only (rank launch, process group, barriers, max-over-ranks timing, the "
+                         "JSON line) with a CPU stand-in step and no device work: the CPU test of --gpus N")
     return ap.parse_args()
+
+
+def launch_ranks(n):
+    """`--gpus N` without a launcher: start N ranks (one process per GPU) under
+    torch.distributed.run as a CHILD process -- before this process has touched a GPU -- and
+    return its exit code.  Rank r binds device r (LOCAL_RANK)."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
 
 
 def cpu_model():
@@ -107,16 +124,31 @@ def cpu_baseline(cfg, seconds, threads):
 
 def main():
     a = parse()
+    # --gpus N is authoritative: without a launcher, start N ranks (nothing has touched a GPU
+    # yet); under a launcher, its world size must be N
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(launch_ranks(a.gpus))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != a.gpus:
+        print(f"bench.py: --gpus {a.gpus} but the launcher started WORLD_SIZE={world} ranks", file=sys.stderr)
+        sys.exit(2)
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # one process per GPU; WSC_BENCH_BACKEND=gloo + a shared device is only for rehearsing the
-    # N>1 control path on a 1-GPU box (the driver's N>1 runs use RCCL, one GPU per rank)
-    backend = os.environ.get("WSC_BENCH_BACKEND", "nccl")
-    local = local % max(1, torch.cuda.device_count())
+    # one process per GPU, rank r on device LOCAL_RANK; WSC_BENCH_BACKEND=gloo + a shared device is
+    # only for rehearsing the N>1 control path on a 1-GPU box (the driver's N>1 runs use RCCL)
+    backend = "gloo" if a.dry_run else os.environ.get("WSC_BENCH_BACKEND", "nccl")
+    if a.dry_run:
+        if world > 1:
+            dist.init_process_group("gloo")
+        return dry_run(a, dist, world, rank)
+    n_dev = torch.cuda.device_count()
+    if backend == "nccl" and local >= n_dev:
+        print(f"bench.py: rank {rank} wants device {local} but {n_dev} are visible", file=sys.stderr)
+        sys.exit(2)
+    local = local % max(1, n_dev)
     if world > 1:
         torch.cuda.set_device(local)
         if backend == "nccl":
@@ -144,7 +176,7 @@ def main():
         c = K.Codec(local, **over)
         t = dict(wire=torch.from_numpy(cfg["wire"]).to(dev),
                  seg_off=torch.from_numpy(cfg["seg_off"].view(np.int64)).to(dev),
-                 st_out=torch.zeros(n_segs * 16, dtype=torch.uint8, device=dev),
+                 st_out=torch.zeros(n_segs * K.STATE_BYTES, dtype=torch.uint8, device=dev),
                  seg_out=torch.zeros(n_segs * 32, dtype=torch.uint8, device=dev),
                  frames=torch.zeros((a.frames + 16) * 32, dtype=torch.uint8, device=dev),
                  summ=torch.zeros(32, dtype=torch.uint8, device=dev))
@@ -330,6 +362,41 @@ def main():
         dist.destroy_process_group()
 
 
+def dry_run(a, dist, world, rank):
+    """The control path of a --gpus N run with a CPU stand-in step (XOR of a 1 MiB buffer): the
+    barriers, the max-over-ranks wall time and the JSON line, n_gpus = world.  No device work."""
+    import torch
+    buf = np.frombuffer(np.random.default_rng(rank).bytes(1 << 20), np.uint8).copy()
+
+    def step():
+        np.bitwise_xor(buf, np.uint8(0x5A), out=buf)
+
+    for _ in range(a.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+        ranks = torch.tensor([rank], dtype=torch.int64)
+        dist.all_reduce(ranks, op=dist.ReduceOp.SUM)
+        rank_sum = int(ranks.item())
+    else:
+        rank_sum = 0
+    if rank == 0:
+        print(json.dumps({"metric": "dry run (control path only, no device work)", "value": None,
+                          "unit": "GiB/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+                          "ms_per_step": round(el / max(1, a.steps) * 1e3, 4), "rank_sum": rank_sum,
+                          "data": "dry run"}))
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def config3_dealt(a, torch, dist, K, synth, world, rank, dev, cdev):
     """BASELINE.json configs[3] at N GPUs: ONE global batch of N x 1 M masked 4 KiB BIN frames
     (16 frames per connection segment; 8 M frames = 32 GiB at N = 8) whose segments are dealt
@@ -347,7 +414,7 @@ def config3_dealt(a, torch, dist, K, synth, world, rank, dev, cdev):
         c = K.Codec(dev.index, max_batch_bytes=n_bytes + 4096, max_segs=n_segs, max_frames=nf + 16)
         t = dict(wire=torch.from_numpy(cfg["wire"]).to(dev),
                  seg_off=torch.from_numpy(cfg["seg_off"].view(np.int64)).to(dev),
-                 st=torch.zeros(n_segs * 16, dtype=torch.uint8, device=dev),
+                 st=torch.zeros(n_segs * K.STATE_BYTES, dtype=torch.uint8, device=dev),
                  so=torch.zeros(n_segs * 32, dtype=torch.uint8, device=dev),
                  fr=torch.zeros((nf + 16) * 32, dtype=torch.uint8, device=dev),
                  sm=torch.zeros(32, dtype=torch.uint8, device=dev))
@@ -442,7 +509,7 @@ def other_configs(torch, K, synth, only=None):
             c = K.Codec(dev.index, max_batch_bytes=len(cfg["wire"]) + 4096, max_segs=n, max_frames=cfg["n_frames"] + 16)
             t = dict(wire=torch.from_numpy(cfg["wire"]).to(dev),
                      seg_off=torch.from_numpy(cfg["seg_off"].view(np.int64)).to(dev),
-                     st=torch.zeros(n * 16, dtype=torch.uint8, device=dev), so=torch.zeros(n * 32, dtype=torch.uint8, device=dev),
+                     st=torch.zeros(n * K.STATE_BYTES, dtype=torch.uint8, device=dev), so=torch.zeros(n * 32, dtype=torch.uint8, device=dev),
                      fr=torch.zeros((cfg["n_frames"] + 16) * 32, dtype=torch.uint8, device=dev),
                      sm=torch.zeros(32, dtype=torch.uint8, device=dev))
             if compact:
@@ -693,7 +760,7 @@ def host_inclusive_pipelined(torch, codecs, streams, cfg, K, chunks=16, iters=3)
     for j in range(P):
         bufs.append(dict(wire=torch.empty(max_bytes + 16, dtype=torch.uint8, device=dev),
                          seg_off=torch.empty(max_segs + 1, dtype=torch.int64, device=dev),
-                         st=torch.empty(max_segs * 16, dtype=torch.uint8, device=dev),
+                         st=torch.empty(max_segs * K.STATE_BYTES, dtype=torch.uint8, device=dev),
                          so=torch.empty(max_segs * 32, dtype=torch.uint8, device=dev),
                          fr=torch.empty(max_frames * 32, dtype=torch.uint8, device=dev),
                          sm=torch.empty(32, dtype=torch.uint8, device=dev)))
@@ -773,7 +840,7 @@ def host_inclusive_zero_copy(torch, codecs, streams, cfg, K, chunks=16, iters=3)
         for j in range(P):
             bufs.append(dict(wire=torch.empty(max_bytes + 16, dtype=torch.uint8, device=dev),
                              seg_off=torch.empty(max_segs + 1, dtype=torch.int64, device=dev),
-                             st=torch.empty(max_segs * 16, dtype=torch.uint8, device=dev),
+                             st=torch.empty(max_segs * K.STATE_BYTES, dtype=torch.uint8, device=dev),
                              so=torch.empty(max_segs * 32, dtype=torch.uint8, device=dev),
                              fr=torch.empty(max_frames * 32, dtype=torch.uint8, device=dev),
                              fd=torch.empty(max_frames, dtype=torch.int64, device=dev),

@@ -28,7 +28,8 @@
 extern "C" {
 #endif
 
-#define WSC_ABI_VERSION 2   /* 2: wsc_frame.payload_len_hi (40-bit payload lengths), staged split */
+#define WSC_ABI_VERSION 3   /* 2: wsc_frame.payload_len_hi (40-bit payload lengths), staged split;
+                               3: payloads streamed across batches (wsc_conn_state.frame_*, WSC_FK_PIECE) */
 
 /* ---- return codes --------------------------------------------------------------------------- */
 #define WSC_OK 0
@@ -62,6 +63,20 @@ extern "C" {
 #define WSC_FK_PONG_EMPTY 5  /* PONG without payload: Close() (websocket.go:198-201)             */
 #define WSC_FK_ERROR 6       /* sentinel `err` at this frame: CloseCode(1002|1007)               */
 #define WSC_FK_STALL 7       /* unmasked client frame: reference returns EAGAIN forever (Q3)     */
+#define WSC_FK_PIECE 8       /* the payload bytes of a data frame that is not complete at the end of
+                                its segment (nextFrame's partial read into rBuffer,
+                                websocket_frame.go:16-31): unmasked, nothing delivered yet.  The
+                                frame continues in the connection's next segment (state_out.frame_*);
+                                its last piece carries the frame's real kind (MESSAGE or FRAG) */
+
+/* Streaming (ABI 3).  A data frame (opcode 0/1/2) whose header is complete is consumed as its
+ * payload arrives: each batch unmasks the bytes it holds and records them (WSC_FK_PIECE, then the
+ * final kind on the piece that completes the frame), and the connection carries only
+ * {frame_rem, frame_mask, frame_hdr, frame_len} -- never the payload -- to its next segment, which
+ * starts with the rest of that payload.  A record whose header lay in an earlier batch has
+ * WSC_FF_HEAD_PREV, hdr_len 0 and hdr_off = its first payload byte; its `mask` is phased to that
+ * byte.  The frame's data is the concatenation of its pieces' payloads, in order.  Control frames
+ * (<= 125 B) and incomplete headers are still carried whole (seg_result.consumed stops before them). */
 
 /* wsc_frame.flags */
 #define WSC_FF_UNMASKED 0x01  /* payload went through nextFrame and was XOR-unmasked             */
@@ -71,6 +86,7 @@ extern "C" {
 #define WSC_FF_U8_CHAIN 0x10  /* internal: continueBuffer || payload must be valid utf8          */
 #define WSC_FF_U8_REASON 0x20 /* internal: CLOSE reason payload[2:] must be valid utf8          */
 #define WSC_FF_CTRL_ARENA 0x40 /* COMPACT: payload placed in the control region of the arena    */
+#define WSC_FF_HEAD_PREV 0x80  /* the frame's header was in an earlier batch (hdr_len 0)          */
 
 /* ---- per-connection terminal status ---------------------------------------------------------- */
 #define WSC_SEG_OPEN 0      /* connection continues; bytes [consumed, len) are carried over        */
@@ -89,10 +105,16 @@ typedef struct wsc_conn_state {
     uint64_t cont_len;     /* continueBuffer length (bytes of an unfinished fragmented message)  */
     uint32_t msg_id;       /* msgID: next Message.MsgID                                          */
     uint8_t message_mode;  /* messageMode: 0, 1 (text) or 2 (binary)                             */
-    uint8_t cont_utf8;     /* utf8 DFA state after continueBuffer (0 = complete characters)      */
+    uint8_t cont_utf8;     /* utf8 DFA state after continueBuffer and the in-progress frame's
+                              bytes so far (0 = complete characters)                              */
     uint8_t status;        /* WSC_SEG_*; a connection that is not OPEN decodes nothing           */
-    uint8_t pad;
-} wsc_conn_state;          /* 16 B */
+    uint8_t frame_hdr;     /* in-progress frame (frame_rem != 0): FIN << 7 | opcode              */
+    uint64_t frame_rem;    /* payload bytes of the in-progress frame still to come; 0 = the next
+                              byte starts a header (websocket_frame.go:16 rLen)                   */
+    uint64_t frame_len;    /* its whole payload length (fragmentLength)                          */
+    uint32_t frame_mask;   /* its mask, phased so that the next payload byte takes wire byte 0   */
+    uint32_t pad;
+} wsc_conn_state;          /* 40 B */
 
 /* One record per frame whose header was parsed and acted on, in stream order.                  */
 typedef struct wsc_frame {
@@ -157,7 +179,10 @@ typedef struct wsc_config {
     uint64_t max_batch_bytes;  /* largest n_bytes a batch may have                               */
     uint32_t max_segs;         /* largest n_segs                                                 */
     uint32_t max_frames;       /* largest number of frames in one batch                          */
-    uint64_t max_frame_len;    /* payloads above this -> WSC_ERR_TOO_LARGE (<= 2^40 - 1)         */
+    uint64_t max_frame_len;    /* payloads above this -> WSC_ERR_TOO_LARGE (<= 2^40 - 1, the
+                                  default: the record width; the reference has no limit until
+                                  make() fails, Q4).  Independent of max_batch_bytes: payloads
+                                  stream across batches                                          */
     uint32_t unmask_window;    /* bytes per wave-window in the unmask kernel: 4096 / 8192 (0 = 4096) */
     uint32_t unmask_waves_per_cu; /* unmask grid sizing (0 = default)                            */
     uint32_t unmask_nt;        /* in place: bit0 non-temporal payload loads, bit1 non-temporal    */
@@ -181,7 +206,11 @@ int wsc_host_free(void* p);
 
 /* Enqueue the decode of one device-resident batch on `hip_stream` (a hipStream_t; NULL = the
  * default stream, as everywhere in HIP).  Asynchronous: results are valid once the stream is
- * synchronised (wsc_sync with the same stream).  Inputs must be ready on that stream. */
+ * synchronised (wsc_sync with the same stream).  Inputs must be ready on that stream.
+ * A batch whose summary has overflow bit 0 set (records beyond frames_cap) is INVALID as a whole:
+ * besides the dropped records, its chip-wide UTF-8 verdicts were not applied (a TEXT frame that
+ * should have closed with 1007 may read as a MESSAGE) -- re-decode it in smaller parts, as
+ * wsc_session does.  Check with wsc_summary_status() or wsc_error_flags(). */
 int wsc_decode(wsc_ctx* ctx, const wsc_batch* batch, void* hip_stream);
 int wsc_sync(wsc_ctx* ctx, void* hip_stream);
 
@@ -284,10 +313,18 @@ int wsc_debug_stamps(wsc_ctx* ctx, uint64_t* out, uint32_t max_blocks);
  * the single thread that owns the session.  Handles carry a generation: a stale handle of a
  * removed connection never touches a newer connection in the same slot.
  *
- * Capacity is per connection: max_frame_len is clamped to max_batch_bytes - 14 at create (a
- * longer frame could never fit one batch: it closes ITS connection with WSC_ERR_TOO_LARGE / 1002,
- * Q4); a connection with more bytes than a batch holds is decoded from a prefix and continues in
- * the next batch; a batch with more frame records than max_frames is re-decoded in halves.
+ * Capacity is per connection: frames of any size up to max_frame_len stream through batches of
+ * any size (each batch unmasks the payload bytes it holds; the session appends them to the
+ * connection's rBuffer and delivers the message when its last byte has been decoded, as
+ * websocket_frame.go:16-31 does), so every wire byte crosses PCIe once except an incomplete header
+ * or control frame at a segment's end (<= 139 B, sent again with the next bytes); a connection
+ * with more bytes than a batch holds is decoded from a prefix and continues in the next batch; a
+ * batch with more frame records than max_frames is re-decoded in halves.
+ *
+ * Ordering: reads (reserve/commit, feed) are accepted at any time, including while a submitted
+ * batch is in flight; a connection whose previous bytes are in that batch gets its new bytes
+ * staged behind the batch's undecoded tail, which complete() establishes -- they are placed in a
+ * batch only after it.
  *
  * Device failure (WSC_E_DEVICE / WSC_E_INTERNAL from decode/complete): the connections of the
  * failed batch get WSC_EV_CLOSE with close_code 1011 and err WSC_ERR_DEVICE, keep their carried
@@ -336,6 +373,11 @@ int wsc_session_decode(wsc_session* s);    /* submit + complete until everything
 int wsc_session_pending(wsc_session* s, uint64_t* bytes);
 int wsc_session_next(wsc_session* s, uint32_t conn, wsc_event* ev);  /* DecodePacket() */
 int wsc_session_state(wsc_session* s, uint32_t conn, wsc_conn_state* st, uint64_t* carry_bytes);
+/* Byte accounting since create: out[0] bytes read (committed / fed), out[1] bytes sent to the
+ * device (H2D of batch wires), out[2] of those, bytes sent again (carried incomplete headers and
+ * control frames), out[3] batches, out[4] bytes of streamed payload pieces delivered into
+ * messages.  n = how many of these to write (<= 5).                                            */
+int wsc_session_stats(wsc_session* s, uint64_t* out, uint32_t n);
 
 #ifdef __cplusplus
 }

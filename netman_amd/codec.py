@@ -31,8 +31,8 @@ ERR_NONE, ERR_OPCODE_FAIL, ERR_RSV_FAIL, ERR_PING_PAYLOAD_OVERSIZE = 0, 1, 2, 3
 ERR_CTRL_FRAGMENTED, ERR_MUST_UTF8, ERR_PROTOCOL_ERROR, ERR_TOO_LARGE = 4, 5, 6, 7
 ERR_DEVICE = 8   # session: the connection's batch hit a device error -> CloseCode(1011)
 
-FK_FRAG, FK_MESSAGE, FK_PING, FK_PONG, FK_CLOSE, FK_PONG_EMPTY, FK_ERROR, FK_STALL = range(8)
-FF_UNMASKED, FF_CONT_MSG, FF_CTRL_ARENA = 0x01, 0x02, 0x40
+FK_FRAG, FK_MESSAGE, FK_PING, FK_PONG, FK_CLOSE, FK_PONG_EMPTY, FK_ERROR, FK_STALL, FK_PIECE = range(9)
+FF_UNMASKED, FF_CONT_MSG, FF_CTRL_ARENA, FF_HEAD_PREV = 0x01, 0x02, 0x40, 0x80
 
 SEG_OPEN, SEG_CLOSED, SEG_ERROR, SEG_STALLED = 0, 1, 2, 3
 F_COMPACT = 0x1
@@ -41,7 +41,8 @@ EV_NONE, EV_MESSAGE, EV_PONG, EV_CLOSE, EV_STALL = 0, 1, 2, 3, 4
 
 # ---- numpy views of the ABI records ------------------------------------------------------------
 CONN_STATE_DTYPE = np.dtype([("cont_len", "<u8"), ("msg_id", "<u4"), ("message_mode", "u1"),
-                             ("cont_utf8", "u1"), ("status", "u1"), ("pad", "u1")])
+                             ("cont_utf8", "u1"), ("status", "u1"), ("frame_hdr", "u1"),
+                             ("frame_rem", "<u8"), ("frame_len", "<u8"), ("frame_mask", "<u4"), ("pad", "<u4")])
 FRAME_DTYPE = np.dtype([("hdr_off", "<u8"), ("payload_len", "<u4"), ("mask", "<u4"), ("seg", "<u4"),
                         ("msg_id", "<u4"), ("opcode", "u1"), ("fin", "u1"), ("kind", "u1"),
                         ("mode", "u1"), ("err", "u1"), ("hdr_len", "u1"), ("flags", "u1"),
@@ -50,7 +51,8 @@ SEG_RESULT_DTYPE = np.dtype([("consumed", "<u8"), ("frame_begin", "<u4"), ("fram
                              ("status", "<u4"), ("close_code", "<u4"), ("err", "<u4"), ("pad", "<u4")])
 SUMMARY_DTYPE = np.dtype([("data_bytes", "<u8"), ("ctrl_bytes", "<u8"), ("n_frames", "<u4"),
                           ("n_spans", "<u4"), ("overflow", "<u4"), ("pad", "<u4")])
-assert CONN_STATE_DTYPE.itemsize == 16 and FRAME_DTYPE.itemsize == 32
+STATE_BYTES = 40   # sizeof(wsc_conn_state)
+assert CONN_STATE_DTYPE.itemsize == STATE_BYTES and FRAME_DTYPE.itemsize == 32
 
 
 def frame_len(rec) -> int:
@@ -84,7 +86,9 @@ class WscEvent(C.Structure):
 
 class WscConnState(C.Structure):
     _fields_ = [("cont_len", C.c_uint64), ("msg_id", C.c_uint32), ("message_mode", C.c_uint8),
-                ("cont_utf8", C.c_uint8), ("status", C.c_uint8), ("pad", C.c_uint8)]
+                ("cont_utf8", C.c_uint8), ("status", C.c_uint8), ("frame_hdr", C.c_uint8),
+                ("frame_rem", C.c_uint64), ("frame_len", C.c_uint64), ("frame_mask", C.c_uint32),
+                ("pad", C.c_uint32)]
 
 
 # every function include/wscodec.h declares, with its ctypes signature
@@ -127,10 +131,11 @@ SIGNATURES = {
     "wsc_session_pending": (_I, [_P, C.POINTER(_U64)]),
     "wsc_session_next": (_I, [_P, _U32, C.POINTER(WscEvent)]),
     "wsc_session_state": (_I, [_P, _U32, C.POINTER(WscConnState), C.POINTER(_U64)]),
+    "wsc_session_stats": (_I, [_P, C.POINTER(_U64), _U32]),
 }
 
 _lib = None
-ABI_VERSION = 2   # include/wscodec.h WSC_ABI_VERSION: the record layouts above
+ABI_VERSION = 3   # include/wscodec.h WSC_ABI_VERSION: the record layouts above
 
 
 def load_library(path: str = LIB_PATH):
@@ -527,6 +532,13 @@ class Session:
         if e.type == EV_PONG:
             return None, None
         return None, EAGAIN
+
+    def stats(self) -> dict:
+        """wsc_session_stats: bytes read, sent to the device, sent again (carried), batches,
+        streamed payload bytes collected into messages"""
+        v = (C.c_uint64 * 5)()
+        _check(self.lib.wsc_session_stats(self.h, v, 5), "wsc_session_stats")
+        return dict(zip(("read", "h2d", "resent", "batches", "pieces"), list(v)))
 
     def state(self, conn: int):
         st = WscConnState()

@@ -37,6 +37,14 @@ int fail(int code, const std::string& msg) {
     g_err = msg;
     return code;
 }
+}  // namespace
+
+namespace wsc {
+// wsc_last_error() text for the session layer (wsc_session.cpp), same thread-local slot
+int set_last_error(int code, const std::string& msg) { return fail(code, msg); }
+}  // namespace wsc
+
+namespace {
 #define HIP_TRY(expr)                                                                    \
     do {                                                                                 \
         hipError_t e_ = (expr);                                                          \
@@ -92,6 +100,8 @@ struct wsc_ctx {
     uint32_t u8_inline_max = 256;
     uint32_t u8_grid = 0;               // WSC_U8_GRID: k_u8_check workgroups (A/B experiments; 0 = 5 per CU)
     int walk_mode = 0;                  // WSC_WALK_MODE: 64, 256 or 3 pins the walk geometry (A/B, tests); 0 = auto
+    uint32_t walk_used = 0;             // geometry (64 / 256 / 3) and block count of the last walk launched:
+    uint32_t walk_blocks = 0;           // the staged unmask re-arms exactly that walk's look-back flags
     SegCount* counts = nullptr;         // three-launch walk: per-segment counts
     uint64_t tile_entries = 0;
     // host-staged path buffers (lazily allocated)
@@ -186,7 +196,7 @@ int wsc_config_default(wsc_config* cfg) {
     cfg->max_batch_bytes = 64ull << 20;
     cfg->max_segs = 1u << 16;
     cfg->max_frames = 1u << 20;
-    cfg->max_frame_len = 0x7FFFFFFFull;
+    cfg->max_frame_len = 0xFFFFFFFFFFull;   // 2^40 - 1: the record width (Q4)
     cfg->unmask_window = 4096;       // tools/tune_unmask.py, profiles/r01_tune_*.log
     cfg->unmask_waves_per_cu = 0;    // 0: one window per wave (grid = windows)
     cfg->unmask_nt = 3 | 2 << 2;     // in place: non-temporal loads and stores; COMPACT (bits 2-3): NT stores
@@ -420,9 +430,17 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     // walk geometry: the fused walk with blocks that fill the CUs once (64 lanes for up to 64
     // segments per CU, else 256), or -- for more segments than the chip holds lanes at once -- the
     // three-launch walk, which never waits on another block
-    const uint32_t mode = walk_mode(c, n, stream_cus(c, split ? sw : st));
+    // (phase 2 -- the staged unmask -- re-arms the look-back state of the walk phase 1 launched,
+    // whose geometry followed ITS stream's CUs: recomputing it here from another stream could pick
+    // fewer flags and leave stale inclusive prefixes for the next walk)
+    const uint32_t mode = phase == 2 && c->walk_used ? c->walk_used : walk_mode(c, n, stream_cus(c, split ? sw : st));
     const uint32_t wnt = mode == 64 ? 64u : 256u;
     const dim3 wblk(wnt), wgrid((n + wnt - 1) / wnt);
+    if (phase != 2) {
+        c->walk_used = mode;
+        c->walk_blocks = wgrid.x;
+    }
+    const uint32_t rearm = mode == 3 ? 1u : (phase == 2 ? c->walk_blocks : wgrid.x) + 1;
     auto rec = [&](int i) {
         if (ev) (void)hipEventRecord(ev[i], st);
     };
@@ -504,7 +522,7 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     }
     hipLaunchKernelGGL(kern, ugrid, ublk, 0, st, udst, (const uint8_t*)b->wire, b->n_bytes, b->n_bytes,
                        (const Span*)c->spans, (const uint32_t*)c->tile, (const wsc_summary*)b->summary,
-                       c->lb_state, mode == 3 ? 1u : wgrid.x + 1,   // re-arms ticket, timeout, flags
+                       c->lb_state, rearm,   // re-arms ticket, timeout, flags
                        sig_unmask ? c->fin_ctr : nullptr, sig_unmask ? c->hflag + 1 : nullptr, c->fin_seq + 1, uw);
     HIP_TRY(hipGetLastError());
     rec(2);

@@ -167,9 +167,27 @@ __device__ __forceinline__ void emit_frame(const WalkArgs& a, EmitCtx& e, const 
 struct WalkEnd {
     uint64_t pos, cont;
     uint64_t last_dend;      // wire end of the segment's last payload span (seg_start if none)
+    uint64_t frem, flen;     // the in-progress (streamed) data frame: payload still to come, length
+    uint32_t fmask, fhdr;    // ... its mask phased to the next payload byte, FIN << 7 | opcode
     uint32_t msg, mode, status, close_code, err, u8dfa;
     bool replay;             // counting pass: the LDS records hold the whole segment
 };
+
+// the carried state a walk leaves (websocket.go:38-56 subset + the streamed frame)
+__device__ __forceinline__ wsc_conn_state end_state(const WalkEnd& w) {
+    wsc_conn_state o;
+    o.cont_len = w.cont;
+    o.msg_id = w.msg;
+    o.message_mode = (uint8_t)w.mode;
+    o.cont_utf8 = (w.cont || w.frem) ? (uint8_t)w.u8dfa : 0;
+    o.status = (uint8_t)w.status;
+    o.frame_hdr = w.frem ? (uint8_t)w.fhdr : 0;
+    o.frame_rem = w.frem;
+    o.frame_len = w.frem ? w.flen : 0;
+    o.frame_mask = w.frem ? w.fmask : 0;
+    o.pad = 0;
+    return o;
+}
 
 template <bool COMPACT>
 __device__ __forceinline__ void emit_end(const WalkArgs& a, EmitCtx& e, const WalkEnd& w) {
@@ -185,23 +203,18 @@ __device__ __forceinline__ void emit_end(const WalkArgs& a, EmitCtx& e, const Wa
     r.err = w.err;
     r.pad = 0;
     a.seg_out[e.s] = r;
-    wsc_conn_state o;
-    o.cont_len = w.cont;
-    o.msg_id = w.msg;
-    o.message_mode = (uint8_t)w.mode;
-    o.cont_utf8 = w.cont ? (uint8_t)w.u8dfa : 0;
-    o.status = (uint8_t)w.status;
-    o.pad = 0;
-    a.state_out[e.s] = o;
+    a.state_out[e.s] = end_state(w);
 }
 
 
+// LDS record of the counting pass: header offset in the segment, payload length, mask, and the
+// frame's fields packed into one word -- opcode 0-3, fin 4, kind 5-8, mode 9-10, err 11-13,
+// hdr_len 14-17, flags 18-25, region 26, have_span 27, the lane's segment (tag) 28-31
 __device__ __forceinline__ uint4 rec_pack(const wsc_frame& fr, uint64_t seg_start, bool have_span,
-                                          uint32_t region, bool msg_inc) {
+                                          uint32_t region) {
     const uint32_t bits = (uint32_t)fr.opcode | (uint32_t)fr.fin << 4 | (uint32_t)fr.kind << 5 |
-                          (uint32_t)fr.mode << 8 | (uint32_t)fr.err << 10 | (uint32_t)fr.hdr_len << 13 |
-                          (uint32_t)fr.flags << 17 | region << 24 | (uint32_t)have_span << 25 |
-                          (uint32_t)msg_inc << 26;
+                          (uint32_t)fr.mode << 9 | (uint32_t)fr.err << 11 | (uint32_t)fr.hdr_len << 14 |
+                          (uint32_t)fr.flags << 18 | region << 26 | (uint32_t)have_span << 27;
     return make_uint4((uint32_t)(fr.hdr_off - seg_start), fr.payload_len, fr.mask, bits);
 }
 
@@ -229,6 +242,10 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
     uint32_t msg = st.msg_id;
     uint32_t mode = st.message_mode;
     uint32_t status = st.status;
+    // a data frame whose payload is still arriving (its header was in an earlier batch):
+    // websocket_frame.go:16-31 -- nextFrame reads what is there into rBuffer, completes later
+    uint64_t frem = st.frame_rem, flen = st.frame_len;
+    uint32_t fmask = st.frame_mask, fhdr = st.frame_hdr;
     uint32_t close_code = 0, err_out = 0;
     uint32_t nf = 0, ns0 = 0, ns1 = 0, sflags = 0;
     uint64_t nb0 = 0, nb1 = 0;
@@ -237,9 +254,9 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
 
     // UTF-8 verdicts are decided by the counting pass (payload read on the still-masked wire) and
     // replayed by the emitting pass: u8fail = ordinal of the first frame that fails, u8dfa = DFA
-    // state after the continueBuffer (carried to the next batch).
+    // state after the continueBuffer and the in-progress frame's bytes (carried to the next batch).
     uint32_t u8fail = 0xFFFFFFFFu;
-    uint32_t u8dfa = cont ? st.cont_utf8 : 0u;
+    uint32_t u8dfa = (cont || frem) ? st.cont_utf8 : 0u;
     bool u8_pending = false;                      // a text chain has a deferred (chip-wide) part
     uint32_t u8_head = 0xFFFFFFFFu, u8_last = 0xFFFFFFFFu, u8_n = 0;
     bool u8_comp = false;                         // an item whose verdict needs the segment's composition
@@ -263,10 +280,10 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
 
     // LDS records of the counting pass for the emit: rec_pack + the frame's position among the
     // segment's outputs (MsgID, span ordinal, arena offset in its region, previous span end)
-    auto record = [&](const wsc_frame& fr, bool have_span, uint32_t region, bool inc, uint64_t plen) {
+    auto record = [&](const wsc_frame& fr, bool have_span, uint32_t region, uint64_t plen) {
         if (lrec && nf < cap) {
-            uint4 r = rec_pack(fr, seg_start, have_span, region, inc);
-            r.w |= tag << 27;   // the lane's segment the frame belongs to
+            uint4 r = rec_pack(fr, seg_start, have_span, region);
+            r.w |= tag << 28;   // the lane's segment the frame belongs to
             lrec[nf * LS] = r;
             lrec2[nf * LS] = make_uint4(fr.msg_id, ns0 + ns1, (uint32_t)(COMPACT && region ? nb1 : nb0),
                                         (uint32_t)(pend - seg_start));
@@ -362,6 +379,97 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
         if (chain) u8_pending = false;   // the message completes here
     };
 
+    // The end of every frame record: utf8.Valid (TEXT messages, websocket_frame.go:71-73, across
+    // fragments, pieces and batches; control payloads inside a TEXT message, Q6; close reasons,
+    // websocket.go:170-172), then the record and the segment's counts.  `plen` = the payload
+    // bytes this record covers (a streamed frame's piece).
+    auto finish = [&](wsc_frame& fr, uint64_t plen, bool have_span, uint32_t region) {
+        if (fr.flags & (WSC_FF_U8_PART | WSC_FF_U8_SELF | WSC_FF_U8_CHAIN | WSC_FF_U8_REASON)) {
+            sflags |= SEGF_UTF8;
+            if constexpr (!EMIT) {
+                const bool part = (fr.flags & WSC_FF_U8_PART) != 0, chain = (fr.flags & WSC_FF_U8_CHAIN) != 0;
+                const uint64_t src = fr.hdr_off + fr.hdr_len, n = plen;
+                const uint32_t mk = fr.mask;
+                if (fr.flags & WSC_FF_U8_REASON) {
+                    // CLOSE reason, websocket.go:153-172 (<= 125 B: always checked here).  Under
+                    // messageMode == TEXT nextFrame first runs utf8.Valid over the whole payload
+                    // (websocket_frame.go:71-73); if that fails the error is swallowed (:156) and
+                    // the stand-in reason has DataLen = fragmentLength, already zeroed by reset()
+                    // (frame.go:49), so payload[2:] is NOT checked -- only the code is.
+                    const bool skip = fr.mode == 1 && u8_run_masked(0, w, src, n, mk) != 0;
+                    if (!skip && u8_run_masked(0, w, src + 2, n - 2, rotr32(mk, 16)) != 0) u8fail = nf;
+                } else if (n > a.u8_inline_max || ((part || chain) && u8_pending)) {
+                    defer(src, n, mk, part, chain, fr.hdr_len);
+                } else {
+                    bool ok = true;
+                    if (part) u8dfa = u8_run_masked(u8dfa, w, src, n, mk);
+                    else if (chain) ok = u8_run_masked(u8dfa, w, src, n, mk) == 0;
+                    else ok = u8_run_masked(0, w, src, n, mk) == 0;
+                    if (!ok) u8fail = nf;
+                }
+            }
+            if (nf == u8fail) {   // -> CloseCode(1007) (epoll.go:126-127); nothing after it is read
+                fr.kind = WSC_FK_ERROR;
+                fr.err = WSC_ERR_MUST_UTF8;
+                status = WSC_SEG_ERROR; close_code = 1007; err_out = WSC_ERR_MUST_UTF8;
+            }
+        }
+        // continueBuffer (and a streamed frame's bytes) consumed by the message
+        if constexpr (!EMIT) if (fr.flags & (WSC_FF_CONT_MSG | WSC_FF_U8_CHAIN)) u8dfa = 0;
+        if constexpr (COMPACT) if (region) fr.flags |= WSC_FF_CTRL_ARENA;
+        if (plen > 0xFFFFFFFFull) sflags |= SEGF_LONG;
+
+        if constexpr (EMIT) emit_frame<COMPACT>(a, e, fr, plen, have_span, region);
+        else record(fr, have_span, region, plen);
+        nf += 1;
+        if (have_span) {
+            if (COMPACT && region) { ns1 += 1; nb1 += plen; }   // control payloads: <= 125 B
+            else { ns0 += span_chunks(plen); nb0 += plen; }
+        }
+    };
+
+    // The segment starts with the rest of a streamed data frame's payload: consume what is here
+    // as one piece.  The piece that completes the frame takes the frame's kind -- FIN=1: the
+    // message (continueBuffer || earlier pieces || this one, websocket_frame.go:52-91); FIN=0: a
+    // fragment appended to continueBuffer (:92-99) -- earlier ones are WSC_FK_PIECE.
+    auto resume = [&]() {
+        const uint64_t have = seg_end - pos;
+        const uint64_t take = have < frem ? have : frem;
+        const uint32_t op = fhdr & 0xFu, fin = fhdr >> 7;
+        wsc_frame fr;
+        fr.hdr_off = pos;
+        fr.payload_len = (uint32_t)take;
+        fr.payload_len_hi = (uint8_t)(take >> 32);
+        fr.mask = fmask;
+        fr.seg = s;
+        fr.msg_id = msg;
+        fr.opcode = (uint8_t)op;
+        fr.fin = (uint8_t)fin;
+        fr.mode = (uint8_t)mode;
+        fr.err = 0;
+        fr.hdr_len = 0;
+        fr.flags = WSC_FF_UNMASKED | WSC_FF_HEAD_PREV;
+        const bool text = mode == 1;
+        if (take < frem) {
+            fr.kind = WSC_FK_PIECE;
+            if (text) fr.flags |= WSC_FF_U8_PART;
+        } else if (fin) {
+            fr.kind = WSC_FK_MESSAGE;
+            if (op == 0 && cont >= 1) { fr.flags |= WSC_FF_CONT_MSG; cont = 0; }
+            if (text) fr.flags |= WSC_FF_U8_CHAIN;   // from the state after continueBuffer + pieces
+            mode = 0;
+            msg += 1;
+        } else {
+            fr.kind = WSC_FK_FRAG;
+            if (text) fr.flags |= WSC_FF_U8_PART;
+            cont += flen;
+        }
+        frem -= take;
+        fmask = rotr32(fmask, 8u * (uint32_t)(take & 3));
+        finish(fr, take, take > 0, 0);
+        pos += take;
+    };
+
     // One frame at `pos` from its 32-byte header window; returns false when the walk stops
     // (terminal status, or the frame is incomplete and is carried to the next batch).
     auto step = [&](const uint4& hd) -> bool {
@@ -393,7 +501,7 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
         uint64_t next = pos;
         bool have_span = false;
         uint32_t region = 0;
-        uint64_t plen = 0;
+        uint64_t plen = 0, take = 0;   // take: payload bytes this record covers
 
         if (rsv) {  // websocket.go:229-231, checked as soon as the 2 bytes are in
             fr.err = WSC_ERR_RSV_FAIL;
@@ -456,15 +564,38 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
                 } else {
                     err = WSC_ERR_OPCODE_FAIL;
                 }
+                bool piece = false;   // the payload is still arriving: stream it (data frames)
                 if (payload && !err) {
                     if (plen > a.max_frame_len) err = WSC_ERR_TOO_LARGE;        // Q4
-                    else if (avail < hl + plen) return false;                    // wait for payload
+                    else if (avail < hl + plen) {
+                        if (op > 2) return false;   // a control frame (<= 125 B) waits whole
+                        piece = true;               // websocket_frame.go:16-31 partial read
+                    }
                 }
-                next = pstart + (payload && !err ? plen : 0);
+                if (piece) {
+                    take = avail - hl;
+                    fr.payload_len = (uint32_t)take;
+                    fr.payload_len_hi = (uint8_t)(take >> 32);
+                } else {
+                    take = plen;
+                }
+                next = pstart + (payload && !err ? take : 0);
                 if (err) {
                     fr.err = (uint8_t)err;
                     status = WSC_SEG_ERROR; close_code = 1002; err_out = err;
                     next = pstart;
+                } else if (piece) {
+                    // the header is consumed (messageMode set, websocket.go:234-236); the rest of
+                    // the payload is carried as state, never as bytes
+                    fr.kind = WSC_FK_PIECE;
+                    fr.flags |= WSC_FF_UNMASKED;
+                    if (mode_h == 1) fr.flags |= WSC_FF_U8_PART;
+                    mode = mode_h;
+                    frem = plen - take;
+                    flen = plen;
+                    fmask = rotr32(mask, 8u * (uint32_t)(take & 3));
+                    fhdr = fin << 7 | op;
+                    have_span = take > 0;
                 } else {
                     fr.kind = (uint8_t)kind;
                     if (payload) fr.flags |= WSC_FF_UNMASKED;
@@ -505,52 +636,7 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
             }
         }
 
-        // utf8.Valid: TEXT messages (websocket_frame.go:71-73; across fragments and batches),
-        // control payloads inside a TEXT message (Q6), close reasons (websocket.go:170-172)
-        if (fr.flags & (WSC_FF_U8_PART | WSC_FF_U8_SELF | WSC_FF_U8_CHAIN | WSC_FF_U8_REASON)) {
-            sflags |= SEGF_UTF8;
-            if constexpr (!EMIT) {
-                const bool part = (fr.flags & WSC_FF_U8_PART) != 0, chain = (fr.flags & WSC_FF_U8_CHAIN) != 0;
-                const uint64_t src = pos + fr.hdr_len, n = plen;
-                const uint32_t mk = fr.mask;
-                if (fr.flags & WSC_FF_U8_REASON) {
-                    // CLOSE reason, websocket.go:153-172 (<= 125 B: always checked here).  Under
-                    // messageMode == TEXT nextFrame first runs utf8.Valid over the whole payload
-                    // (websocket_frame.go:71-73); if that fails the error is swallowed (:156) and
-                    // the stand-in reason has DataLen = fragmentLength, already zeroed by reset()
-                    // (frame.go:49), so payload[2:] is NOT checked -- only the code is.
-                    const bool skip = fr.mode == 1 && u8_run_masked(0, w, src, n, mk) != 0;
-                    if (!skip && u8_run_masked(0, w, src + 2, n - 2, rotr32(mk, 16)) != 0) u8fail = nf;
-                } else if (n > a.u8_inline_max || ((part || chain) && u8_pending)) {
-                    defer(src, n, mk, part, chain, fr.hdr_len);
-                } else {
-                    bool ok = true;
-                    if (part) u8dfa = u8_run_masked(u8dfa, w, src, n, mk);
-                    else if (chain) ok = u8_run_masked(u8dfa, w, src, n, mk) == 0;
-                    else ok = u8_run_masked(0, w, src, n, mk) == 0;
-                    if (!ok) u8fail = nf;
-                }
-            }
-            if (nf == u8fail) {   // -> CloseCode(1007) (epoll.go:126-127); nothing after it is read
-                fr.kind = WSC_FK_ERROR;
-                fr.err = WSC_ERR_MUST_UTF8;
-                status = WSC_SEG_ERROR; close_code = 1007; err_out = WSC_ERR_MUST_UTF8;
-            }
-        }
-        if constexpr (!EMIT) if (fr.flags & WSC_FF_CONT_MSG) u8dfa = 0;   // continueBuffer consumed
-        if constexpr (COMPACT) if (region) fr.flags |= WSC_FF_CTRL_ARENA;
-
-        if constexpr (EMIT) {
-            emit_frame<COMPACT>(a, e, fr, plen, have_span, region);
-        } else {
-            record(fr, have_span, region,
-                   fr.kind == WSC_FK_MESSAGE || fr.kind == WSC_FK_PING || fr.kind == WSC_FK_PONG, plen);
-        }
-        nf += 1;
-        if (have_span) {
-            if (COMPACT && region) { ns1 += 1; nb1 += plen; }   // control payloads: <= 125 B
-            else { ns0 += span_chunks(plen); nb0 += plen; }
-        }
+        finish(fr, take, have_span, region);
         pos = next;
         return status == WSC_SEG_OPEN;
     };
@@ -607,7 +693,7 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
         }
         const bool have_span = plen > 0;
         if constexpr (EMIT) emit_frame<COMPACT>(a, e, fr, plen, have_span, 0);
-        else record(fr, have_span, 0, true, plen);
+        else record(fr, have_span, 0, plen);
         msg += 1;
         mode = 0;
         nf += 1;
@@ -618,6 +704,8 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
 
     uint64_t stride = 0;
     bool go = status == WSC_SEG_OPEN;
+    if (go && frem && seg_end > pos) resume();   // (a rest longer than the segment: nothing else)
+    go = go && status == WSC_SEG_OPEN && frem == 0;
     while (go) {
         // fewer than 2 bytes left: `step` would stop on them anyway -- no round trip for a header
         // that cannot be there (every segment's walk used to end with one)
@@ -688,6 +776,8 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
     WalkEnd we;
     we.pos = pos; we.cont = cont; we.msg = msg; we.mode = mode; we.status = status;
     we.close_code = close_code; we.err = err_out; we.u8dfa = u8dfa;
+    we.frem = status == WSC_SEG_OPEN ? frem : 0;
+    we.flen = flen; we.fmask = fmask; we.fhdr = fhdr;
     we.last_dend = pend;
     we.replay = replay;
     if (wend) *wend = we;
@@ -932,14 +1022,7 @@ __global__ __launch_bounds__(NT) void k_walk_fused(WalkArgs a) {
             sh_abase[q] = c.bytes0 + c.bytes1;
             sh_ob0[q] = c.bytes0;
         }
-        wsc_conn_state o;   // the connection's carried state (websocket.go:38-56 subset)
-        o.cont_len = we.cont;
-        o.msg_id = we.msg;
-        o.message_mode = (uint8_t)we.mode;
-        o.cont_utf8 = we.cont ? (uint8_t)we.u8dfa : 0;
-        o.status = (uint8_t)we.status;
-        o.pad = 0;
-        a.state_out[s] = o;
+        a.state_out[s] = end_state(we);   // the connection's carried state
         tot = sc_add(tot, c);
     }
     // ---- block scan of the lanes' totals (64-lane shuffles, then across the waves) ----
@@ -1069,11 +1152,11 @@ __global__ __launch_bounds__(NT) void k_walk_fused(WalkArgs a) {
         const uint32_t k = f - sh_rpre[o];
         const uint4 r = sh_rec[k * NT + o];
         const uint4 q = sh_rec2[k * NT + o];
-        const uint32_t j = r.w >> 27;
+        const uint32_t j = r.w >> 28;
         const uint32_t qi = j * NT + o;
         const uint64_t ss = sh_sstart[qi];
-        const uint32_t hl = (r.w >> 13) & 15, fl = (r.w >> 17) & 0x7F, region = (r.w >> 24) & 1;
-        const bool have_span = (r.w >> 25) & 1;
+        const uint32_t hl = (r.w >> 14) & 15, fl = (r.w >> 18) & 0xFF, region = (r.w >> 26) & 1;
+        const bool have_span = (r.w >> 27) & 1;
         const uint64_t hdr_off = ss + r.x;
         uint64_t dst = ~0ull;
         if constexpr (COMPACT)
@@ -1082,9 +1165,9 @@ __global__ __launch_bounds__(NT) void k_walk_fused(WalkArgs a) {
         if (fidx < a.frames_cap) {
             const uint4 r0 = make_uint4((uint32_t)hdr_off, (uint32_t)(hdr_off >> 32), r.y, r.z);
             const uint4 r1 = make_uint4((bid * NT + o) * G + j, q.x,
-                                        (r.w & 0xF) | ((r.w >> 4) & 1) << 8 | ((r.w >> 5) & 7) << 16 |
-                                            ((r.w >> 8) & 3) << 24,
-                                        ((r.w >> 10) & 7) | hl << 8 | fl << 16);
+                                        (r.w & 0xF) | ((r.w >> 4) & 1) << 8 | ((r.w >> 5) & 15) << 16 |
+                                            ((r.w >> 9) & 3) << 24,
+                                        ((r.w >> 11) & 7) | hl << 8 | fl << 16);
             reinterpret_cast<uint4*>(a.frames + fidx)[0] = r0;
             reinterpret_cast<uint4*>(a.frames + fidx)[1] = r1;
             if constexpr (COMPACT) a.frame_dst[fidx] = dst;
@@ -1235,7 +1318,9 @@ __device__ __forceinline__ uint64_t u8_verdict(const U8Args& a, uint32_t s, cons
         j = x.next;
     }
     if (fail == 0xFFFFFFFFu) {
-        if ((g.pending_end & 1u) && a.state_out[s].cont_len) a.state_out[s].cont_utf8 = (uint8_t)(cur > 7 ? 8u : cur);
+        // an open text chain (continueBuffer and/or a streamed frame's pieces) carries its state
+        if ((g.pending_end & 1u) && (a.state_out[s].cont_len || a.state_out[s].frame_rem))
+            a.state_out[s].cont_utf8 = (uint8_t)(cur > 7 ? 8u : cur);
         return ~0ull;
     }
     // frame `fail` fails: CloseCode(1007) there (epoll.go:126-127), nothing after it is read

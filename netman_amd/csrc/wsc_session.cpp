@@ -21,10 +21,13 @@
 // its next bytes.
 //
 // Capacity is handled per connection, never per session (one connection cannot stall the others):
-//   * frames longer than max_batch_bytes - 14 cannot ever fit a batch: max_frame_len is clamped to
-//     that at create, so such a frame closes ITS connection with WSC_ERR_TOO_LARGE -> 1002 (Q4);
+//   * payloads stream: a data frame whose header is in a batch is unmasked piece by piece as its
+//     bytes arrive (WSC_FK_PIECE records, the connection's device state carries the rest of the
+//     frame, never its bytes); the pieces collect in Conn::rbuf -- nextFrame's rBuffer,
+//     websocket_frame.go:16-31 -- and the message is delivered when its last piece decodes, so a
+//     frame of any size up to max_frame_len passes through batches of any size;
 //   * a connection whose bytes do not fit the batch is decoded from a prefix (it always leads a
-//     batch then, so its first frame fits) and the rest follows in the next batch;
+//     batch then) and the rest follows in the next batch;
 //   * a batch whose frame records exceed max_frames is re-decoded in halves (one connection: a
 //     prefix ending at a frame boundary the device reported).
 // Device failure policy (the reference drops a poller's connections when epoll_wait
@@ -50,6 +53,10 @@
 
 #include "../../include/wscodec.h"
 
+namespace wsc {
+int set_last_error(int code, const std::string& msg);   // wsc_api.cpp: the wsc_last_error() text
+}
+
 namespace {
 
 constexpr uint32_t SLOT_BITS = 22;                  // handle = slot | generation << 22
@@ -73,6 +80,7 @@ struct Conn {
     std::vector<uint8_t> carry;   // undecoded tail of earlier reads (starts at a frame header), masked
     std::vector<uint8_t> spill;   // bytes fed while they did not fit the staging being filled
     std::vector<uint8_t> cont;    // continueBuffer (unmasked fragments so far)
+    std::vector<uint8_t> rbuf;    // rBuffer: the unmasked pieces of the frame still arriving
     std::deque<Event> pending;
     Event current;                // storage for the event last returned by next()
     uint64_t fill_epoch = ~0ull;  // == session fill_epoch while placed in the staging being filled
@@ -80,6 +88,8 @@ struct Conn {
     uint64_t reserved = 0;        // bytes handed out by the last reserve (0 = none)
     bool reserved_spill = false;
     bool failed = false;          // its batch hit a device error (WSC_ERR_DEVICE)
+    bool in_flight = false;       // has a segment in the submitted batch: new bytes wait in the
+                                  // spill until complete() has set the carry they must follow
 };
 
 struct Stage {                    // one staging set: pinned host buffers, device buffers, context
@@ -144,6 +154,9 @@ struct wsc_session {
     bool timing = false;
     double t_pack = 0, t_device = 0, t_harvest = 0;
     uint64_t n_batches = 0, n_bytes = 0;
+    // wsc_session_stats: bytes read, sent to the device, of those sent again (carried), batches,
+    // streamed payload bytes collected into messages
+    uint64_t st_read = 0, st_h2d = 0, st_resent = 0, st_batches = 0, st_pieces = 0;
 };
 
 namespace {
@@ -214,6 +227,7 @@ bool place(wsc_session* s, Conn& c, uint32_t handle, uint64_t extra) {
     uint64_t k = 0;
     const uint64_t kc = c.carry.size() < n ? c.carry.size() : n;
     if (kc) std::memcpy(f.h_wire + f.bytes, c.carry.data(), kc);
+    s->st_resent += kc;   // an incomplete header / control frame goes over PCIe again
     k = kc;
     if (k < n) {
         const uint64_t ks = n - k;
@@ -246,12 +260,25 @@ void harvest(wsc_session* s, int set, Conn& c, uint32_t slot, const uint8_t* in_
         Event e;
         std::memset(&e.ev, 0, sizeof(e.ev));
         switch (f.kind) {
+        case WSC_FK_PIECE:                                    // websocket_frame.go:16-31 (rBuffer)
+            c.rbuf.insert(c.rbuf.end(), p, p + flen);
+            s->st_pieces += flen;
+            continue;
         case WSC_FK_FRAG:                                     // websocket_frame.go:95-98
+            if (!c.rbuf.empty()) {                            // a streamed fragment's earlier pieces
+                c.cont.insert(c.cont.end(), c.rbuf.begin(), c.rbuf.end());
+                c.rbuf.clear();
+            }
             c.cont.insert(c.cont.end(), p, p + flen);
             continue;
         case WSC_FK_MESSAGE:                                  // websocket_frame.go:62-91
             if (f.flags & WSC_FF_CONT_MSG) {
                 e.data.swap(c.cont);
+                e.data.insert(e.data.end(), c.rbuf.begin(), c.rbuf.end());
+                c.rbuf.clear();
+                e.data.insert(e.data.end(), p, p + flen);
+            } else if (!c.rbuf.empty()) {                     // a streamed message: rBuffer || last piece
+                e.data.swap(c.rbuf);
                 e.data.insert(e.data.end(), p, p + flen);
             } else {
                 e.view = p;
@@ -297,6 +324,7 @@ void harvest(wsc_session* s, int set, Conn& c, uint32_t slot, const uint8_t* in_
         c.carry.clear();
         c.spill.clear();
         c.cont.clear();
+        c.rbuf.clear();
     }
 }
 
@@ -344,6 +372,7 @@ int decode_sync_part(wsc_session* s, int set, uint32_t a, uint32_t b, uint64_t p
         wire_copy.assign(g.h_wire + base, g.h_wire + base + end);
         wire = wire_copy.data();
     }
+    s->st_h2d += end;   // (a re-decode sends the part again)
     const int rc = wsc_decode_host(g.ctx, wire, end, off.data(), n, s->flags, sin.data(), sout.data(), sres.data(),
                                    fr.data(), s->cfg.max_frames, compact ? res : nullptr,
                                    compact ? fd.data() : nullptr, &sm);
@@ -385,11 +414,19 @@ int decode_range(wsc_session* s, int set, uint32_t a, uint32_t b, uint64_t prefi
     return decode_sync_part(s, set, a, b, prefix_limit);
 }
 
+// a failed HIP call of the session: WSC_E_DEVICE with wsc_last_error() naming the call and the
+// runtime's error text (never a stale message of an earlier error)
+int hip_fail(const char* what, hipError_t e) {
+    return wsc::set_last_error(WSC_E_DEVICE, std::string("wsc_session: ") + what + ": " + hipGetErrorString(e));
+}
+
 int launch_stage(wsc_session* s, Stage& g) {
     const bool compact = (s->flags & WSC_F_COMPACT) != 0;
     const uint32_t n = (uint32_t)g.seg_conn.size();
     hipStream_t st = g.stream;
-#define HT(x) do { if ((x) != hipSuccess) return WSC_E_DEVICE; } while (0)
+    s->st_h2d += g.bytes;
+    s->st_batches += 1;
+#define HT(x) do { const hipError_t e_ = (x); if (e_ != hipSuccess) return hip_fail(#x, e_); } while (0)
     HT(hipMemcpyAsync(g.d_wire, g.h_wire, g.bytes, hipMemcpyHostToDevice, st));
     HT(hipMemcpyAsync(g.d_seg_off, g.h_seg_off, (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, st));
     HT(hipMemcpyAsync(g.d_state_in, g.h_state_in, n * sizeof(wsc_conn_state), hipMemcpyHostToDevice, st));
@@ -438,17 +475,16 @@ int wsc_session_create(int device, const wsc_config* cfg, uint32_t flags, wsc_se
     if (cfg) s->cfg = *cfg; else wsc_config_default(&s->cfg);
     wsc_config& g = s->cfg;
     if (g.max_frames < 2 || g.max_segs < 2 || g.max_batch_bytes < 64) { delete s; return WSC_E_INVAL; }
-    // a frame that can never fit one batch closes its connection (WSC_ERR_TOO_LARGE) instead of
-    // holding every other connection of the session back
-    if (g.max_frame_len > g.max_batch_bytes - 14) g.max_frame_len = g.max_batch_bytes - 14;
+    // (no clamp of max_frame_len to the batch: payloads stream across batches)
     s->flags = flags & WSC_F_COMPACT;
     s->device = device;
     int rc = WSC_OK;
     for (Stage& t : s->st) {
         if (rc == WSC_OK) rc = wsc_create(device, &g, &t.ctx);
         if (rc) break;
-        if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&t.stream, hipStreamNonBlocking) != hipSuccess) {
-            rc = WSC_E_DEVICE;
+        if (const hipError_t e = hipSetDevice(device); e != hipSuccess) { rc = hip_fail("hipSetDevice", e); break; }
+        if (const hipError_t e = hipStreamCreateWithFlags(&t.stream, hipStreamNonBlocking); e != hipSuccess) {
+            rc = hip_fail("hipStreamCreateWithFlags", e);
             break;
         }
         auto H = [&](uint64_t bytes) -> void* {
@@ -556,7 +592,7 @@ int wsc_session_reserve(wsc_session* s, uint32_t conn, uint64_t max_bytes, uint8
     const uint64_t cap = s->cfg.max_batch_bytes;
     // straight into the staging being filled, right behind the connection's segment there (its
     // carried bytes first); bytes already waiting in its spill keep the order, so they go first
-    if (c->spill.empty()) {
+    if (c->spill.empty() && !c->in_flight) {
         if (c->fill_epoch == s->fill_epoch && c->seg + 1 != f.seg_conn.size()) {
             // read twice in one round and no longer the last segment: the old region becomes a dead
             // segment and the bytes move to the end
@@ -592,6 +628,7 @@ int wsc_session_commit(wsc_session* s, uint32_t conn, uint64_t n) {
     Conn* c = lookup(s, conn);
     if (!c) return WSC_E_STATE;
     if (n > c->reserved) return WSC_E_INVAL;
+    s->st_read += n;
     if (c->reserved_spill) {
         c->spill.resize(c->spill.size() - (c->reserved - n));
     } else if (c->reserved) {
@@ -657,9 +694,14 @@ int wsc_session_submit(wsc_session* s) {
         f.h_state_in[q] = st;
     }
     f.h_seg_off[n] = f.bytes;
+    for (uint32_t q = 0; q < n; ++q)
+        if (Conn* c = f.seg_conn[q] == DEAD_SEG ? nullptr : lookup(s, f.seg_conn[q])) c->in_flight = true;
     const double t1 = s->timing ? now_s() : 0;
     s->n_submits += 1;
-    f.launch_rc = (s->fault_at && s->n_submits == s->fault_at) ? WSC_E_DEVICE : launch_stage(s, f);
+    if (s->fault_at && s->n_submits == s->fault_at)   // test knob: as a failed launch would
+        f.launch_rc = wsc::set_last_error(WSC_E_DEVICE, "wsc_session: injected device failure (WSC_SESSION_FAULT)");
+    else
+        f.launch_rc = launch_stage(s, f);
     f.in_flight = true;
     s->fill ^= 1;
     s->fill_epoch += 1;
@@ -684,9 +726,13 @@ int wsc_session_complete(wsc_session* s) {
     const bool compact = (s->flags & WSC_F_COMPACT) != 0;
     const double t0 = s->timing ? now_s() : 0;
     int rc = g.launch_rc;
-    if (rc == WSC_OK && hipStreamSynchronize(g.stream) != hipSuccess) rc = WSC_E_DEVICE;
-    if (rc == WSC_OK && (g.h_summary->overflow & 2u)) rc = WSC_E_INTERNAL;
+    if (rc == WSC_OK)
+        if (const hipError_t e = hipStreamSynchronize(g.stream); e != hipSuccess) rc = hip_fail("hipStreamSynchronize", e);
+    if (rc == WSC_OK && (g.h_summary->overflow & 2u))
+        rc = wsc::set_last_error(WSC_E_INTERNAL, "wsc_session: device look-back timeout: batch results are invalid");
     const uint32_t n = (uint32_t)g.seg_conn.size();
+    for (uint32_t q = 0; q < n; ++q)
+        if (Conn* c = g.seg_conn[q] == DEAD_SEG ? nullptr : lookup(s, g.seg_conn[q])) c->in_flight = false;
     g.done.assign(n, 0);
     bool split = false;
     if (rc == WSC_OK && (g.h_summary->overflow & 1u)) split = true;
@@ -694,17 +740,20 @@ int wsc_session_complete(wsc_session* s) {
     if (rc == WSC_OK && !split) {
         nf = g.h_summary->n_frames;
         hipStream_t st = g.stream;
-        bool ok = true;
-        if (nf) ok = ok && hipMemcpyAsync(g.h_frames, g.d_frames, (uint64_t)nf * sizeof(wsc_frame), hipMemcpyDeviceToHost, st) == hipSuccess;
+        hipError_t e = hipSuccess;
+        const char* what = "";
+        auto D2H = [&](void* dst, const void* src, uint64_t bytes, const char* w) {
+            if (e == hipSuccess && bytes && (e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st)) != hipSuccess) what = w;
+        };
+        D2H(g.h_frames, g.d_frames, (uint64_t)nf * sizeof(wsc_frame), "hipMemcpyAsync frames");
         if (compact) {
-            const uint64_t ab = g.h_summary->data_bytes + g.h_summary->ctrl_bytes;
-            if (ab) ok = ok && hipMemcpyAsync(g.h_res, g.d_arena, ab, hipMemcpyDeviceToHost, st) == hipSuccess;
-            if (nf) ok = ok && hipMemcpyAsync(g.h_frame_dst, g.d_frame_dst, (uint64_t)nf * sizeof(uint64_t), hipMemcpyDeviceToHost, st) == hipSuccess;
-        } else if (g.bytes) {
-            ok = ok && hipMemcpyAsync(g.h_res, g.d_wire, g.bytes, hipMemcpyDeviceToHost, st) == hipSuccess;
+            D2H(g.h_res, g.d_arena, g.h_summary->data_bytes + g.h_summary->ctrl_bytes, "hipMemcpyAsync arena");
+            D2H(g.h_frame_dst, g.d_frame_dst, (uint64_t)nf * sizeof(uint64_t), "hipMemcpyAsync frame_dst");
+        } else {
+            D2H(g.h_res, g.d_wire, g.bytes, "hipMemcpyAsync wire");
         }
-        ok = ok && hipStreamSynchronize(st) == hipSuccess;
-        if (!ok) rc = WSC_E_DEVICE;
+        if (e == hipSuccess && (e = hipStreamSynchronize(st)) != hipSuccess) what = "hipStreamSynchronize";
+        if (e != hipSuccess) rc = hip_fail(what, e);
     }
     const double t1 = s->timing ? now_s() : 0;
     materialize_views(s, set ^ 1);   // the other set is filled next: its views must not dangle
@@ -791,6 +840,13 @@ int wsc_session_next(wsc_session* s, uint32_t conn, wsc_event* ev) {
         ev->data = c->current.data.empty() ? nullptr : c->current.data.data();
         ev->len = c->current.data.size();
     }
+    return WSC_OK;
+}
+
+int wsc_session_stats(wsc_session* s, uint64_t* out, uint32_t n) {
+    if (!s || (n && !out)) return WSC_E_INVAL;
+    const uint64_t v[5] = {s->st_read, s->st_h2d, s->st_resent, s->st_batches, s->st_pieces};
+    for (uint32_t i = 0; i < n && i < 5; ++i) out[i] = v[i];
     return WSC_OK;
 }
 

@@ -16,12 +16,47 @@ def pack_streams(streams):
     return wire, off
 
 
+def header_len(stream, off):
+    """(header bytes, payload length) of the masked frame header at stream[off:]"""
+    b1 = stream[off + 1] & 0x7F
+    if b1 == 126:
+        return 8, int.from_bytes(stream[off + 2:off + 4], "big")
+    if b1 == 127:
+        return 14, int.from_bytes(stream[off + 2:off + 10], "big")
+    return 6, b1
+
+
+def xor_phased(buf, lo, hi, mask):
+    """XOR buf[lo:hi] with the 4 mask bytes phased to lo (byte i takes mask byte i & 3)"""
+    if hi <= lo:
+        return buf
+    k = np.frombuffer(int(mask).to_bytes(4, "little"), dtype=np.uint8)
+    buf[lo:hi] ^= np.resize(k, hi - lo)
+    return buf
+
+
 def compare_segment(si, stream, seg_start, res: K.DecodeResult, ora: O.OracleOut, wire_after=None,
                     compact=False, check_state=True):
     sr = res.seg[si]
     fb, fc = int(sr["frame_begin"]), int(sr["frame_count"])
     fr = res.frames[fb:fb + fc]
     of = ora.frames
+    # A data frame whose payload is still arriving at the segment's end is streamed (ABI 3): its
+    # record is a WSC_FK_PIECE holding the bytes that are here, unmasked; the oracle logs a frame
+    # only once nextFrame completes it (websocket_frame.go:31), so the piece is checked on its own
+    piece = None
+    if fc and int(fr[fc - 1]["kind"]) == K.FK_PIECE:
+        piece = fr[fc - 1]
+        fr, fc = fr[:fc - 1], fc - 1
+        p_off = int(piece["hdr_off"]) - seg_start
+        hl, plen = header_len(stream, p_off)
+        assert int(piece["hdr_len"]) == hl and int(piece["flags"]) & K.FF_UNMASKED, f"seg {si} piece {piece}"
+        assert p_off + hl + K.frame_len(piece) == len(stream), f"seg {si}: the piece must end the segment"
+        assert int(piece["mask"]) == int.from_bytes(stream[p_off + hl - 4:p_off + hl], "little")
+        assert int(sr["consumed"]) == len(stream) and int(sr["status"]) == K.SEG_OPEN
+        st = res.state[si]
+        assert int(st["frame_rem"]) == plen - K.frame_len(piece) and int(st["frame_len"]) == plen, f"seg {si} {st}"
+        assert int(st["frame_hdr"]) == (stream[p_off] & 0x8F), f"seg {si} {st}"
     assert fc == len(of), f"seg {si}: {fc} device frames vs {len(of)} oracle frames\n{fr}\n{of}"
     for i in range(fc):
         d, o = fr[i], of[i]
@@ -51,6 +86,12 @@ def compare_segment(si, stream, seg_start, res: K.DecodeResult, ora: O.OracleOut
             assert int(st["cont_len"]) == r["cont_len"], f"seg {si} {st} vs {r}"
     # payload bytes
     ref = np.frombuffer(ora.inplace, dtype=np.uint8)
+    if piece is not None:   # the streamed piece is unmasked with the frame's mask from its payload start
+        lo = int(piece["hdr_off"]) + int(piece["hdr_len"]) - seg_start
+        ref = xor_phased(ref.copy(), lo, lo + K.frame_len(piece), int(piece["mask"]))
+        if compact:
+            fr = res.frames[fb:fb + fc + 1]
+            fc += 1
     if not compact:
         got = wire_after[seg_start:seg_start + len(stream)]
         if not np.array_equal(got, ref):

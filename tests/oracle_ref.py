@@ -83,13 +83,18 @@ class OracleOut:
     res: dict = field(default_factory=dict)
 
 
-def run(stream: bytes, chunk_ends=None, max_frame_len=0x7FFFFFFF) -> OracleOut:
+MAX_FRAME_LEN = (1 << 40) - 1   # wsc_config_default's max_frame_len (the 40-bit record, Q4)
+
+
+def run(stream: bytes, chunk_ends=None, max_frame_len=MAX_FRAME_LEN, cap=None) -> OracleOut:
+    """cap: room for that many events / frame log lines (default: enough for any stream of
+    this length -- n / 2; pass a bound for streams of a few large frames)"""
     L = lib()
     s = np.frombuffer(stream, dtype=np.uint8) if stream else np.zeros(1, np.uint8)
     n = len(stream)
     inplace = np.zeros(max(n, 1), np.uint8)
-    ev_cap = n // 2 + 16
-    fr_cap = n // 2 + 16
+    ev_cap = (n // 2 + 16) if cap is None else int(cap)
+    fr_cap = ev_cap
     ev = (WsoEvent * ev_cap)()
     fr = np.zeros(fr_cap, FRAME_DTYPE)
     arena = np.zeros(n + 16, np.uint8)

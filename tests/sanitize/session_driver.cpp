@@ -17,7 +17,7 @@
 #include "../../include/wscodec.h"
 
 namespace {
-std::mt19937_64 rng(12345);
+thread_local std::mt19937_64 rng(12345);
 uint64_t rnd(uint64_t n) { return n ? rng() % n : 0; }
 
 void put_frame(std::vector<uint8_t>& out, uint8_t b0, const uint8_t* p, size_t n) {
@@ -59,7 +59,7 @@ Conn make_conn(size_t n_msgs, size_t max_len) {
     return c;
 }
 
-int fails = 0;
+std::atomic<int> fails{0};
 #define CHECK(x) do { if (!(x)) { std::fprintf(stderr, "CHECK failed %s:%d: %s\n", __FILE__, __LINE__, #x); ++fails; } } while (0)
 
 void drain(wsc_session* s, Conn& c) {
@@ -75,7 +75,9 @@ void drain(wsc_session* s, Conn& c) {
 }
 
 // one phase: conns streams fed in random chunks; mode 0 = feed + decode, 1 = reserve/commit +
-// decode, 2 = reserve/commit + submit / drain previous / complete
+// decode, 2 = reserve/commit + submit / drain previous / complete, 3 = submit, then this round's
+// reads WHILE the batch is in flight (its connections' new bytes must wait behind the batch's
+// undecoded tails), complete, drain
 void phase(uint64_t batch_bytes, uint32_t max_frames, int mode, size_t n_conns, size_t n_msgs, size_t max_len,
            bool remover) {
     wsc_config cfg;
@@ -106,6 +108,7 @@ void phase(uint64_t batch_bytes, uint32_t max_frames, int mode, size_t n_conns, 
         if (round == 3) go = true;
         bool any = false;
         std::vector<size_t> fed;
+        if (mode == 3) CHECK(wsc_session_submit(s) == WSC_OK);
         for (size_t i = 0; i < cs.size(); ++i) {
             Conn& c = cs[i];
             if (c.fed >= c.wire.size() || rnd(4) == 0) continue;
@@ -132,7 +135,10 @@ void phase(uint64_t batch_bytes, uint32_t max_frames, int mode, size_t n_conns, 
             fed.push_back(i);
             any = true;
         }
-        if (mode == 2) {
+        if (mode == 3) {
+            CHECK(wsc_session_complete(s) == WSC_OK);
+            for (size_t i = 0; i < cs.size(); ++i) drain(s, cs[i]);
+        } else if (mode == 2) {
             CHECK(wsc_session_submit(s) == WSC_OK);
             for (size_t i : prev) drain(s, cs[i]);
             CHECK(wsc_session_complete(s) == WSC_OK);
@@ -145,7 +151,8 @@ void phase(uint64_t batch_bytes, uint32_t max_frames, int mode, size_t n_conns, 
         for (const Conn& c : cs) left = left || c.fed < c.wire.size();
         uint64_t pend = 0;
         CHECK(wsc_session_pending(s, &pend) == WSC_OK);
-        if (!left && mode != 2) { CHECK(pend == 0); break; }
+        if (!left && mode < 2) { CHECK(pend == 0); break; }
+        if (!left && mode == 3 && pend == 0) break;
         if (!left && !any && pend == 0) {   // pipelined: nothing fed, nothing waiting
             for (size_t i = 0; i < cs.size(); ++i) drain(s, cs[i]);
             break;
@@ -205,12 +212,21 @@ void fault_phase() {
 
 int main(int argc, char** argv) {
     const bool threads = argc > 1 && std::strcmp(argv[1], "--threads") == 0;
-    for (int mode = 0; mode < 3; ++mode) {
+    for (int mode = 0; mode < 4; ++mode) {
         phase(1 << 20, 1 << 12, mode, 24, 40, 3000, false);    // ordinary
         phase(1 << 14, 64, mode, 12, 30, 9000, false);        // tiny batches: prefixes, spills, record splits
         phase(1 << 16, 1 << 12, mode, 40, 20, 200, threads);  // many small frames (+ a remover thread)
+        phase(1 << 13, 256, mode, 6, 8, 70000, false);        // frames up to 8x a batch: streamed payloads
     }
+    // one session per poller thread (eventloop/event.go:33-37): 4 threads, 4 sessions at once
+    std::vector<std::thread> pollers;
+    for (int t = 0; t < 4; ++t)
+        pollers.emplace_back([t] {
+            rng.seed(1000 + t);
+            phase(1 << 16, 1 << 10, t % 4, 16, 20, 6000, false);
+        });
+    for (auto& t : pollers) t.join();
     fault_phase();
-    std::printf("session_driver: %s, %d failed checks\n", threads ? "with remover thread" : "single thread", fails);
-    return fails ? 1 : 0;
+    std::printf("session_driver: %s, %d failed checks\n", threads ? "with remover thread" : "single thread", fails.load());
+    return fails.load() ? 1 : 0;
 }

@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <string>
 
 #include "../../include/wscodec.h"
 
@@ -17,17 +18,17 @@ struct wsc_ctx {
     wsc_config cfg;
 };
 
-static thread_local const char* g_err = "";
+static thread_local std::string g_err;
 static std::mutex g_alloc_mu;
 
 extern "C" {
-const char* wsc_last_error(void) { return g_err; }
+const char* wsc_last_error(void) { return g_err.c_str(); }
 int wsc_config_default(wsc_config* c) {
     std::memset(c, 0, sizeof(*c));
     c->max_batch_bytes = 64ull << 20;
     c->max_segs = 1u << 16;
     c->max_frames = 1u << 20;
-    c->max_frame_len = 0x7FFFFFFFull;
+    c->max_frame_len = 0xFFFFFFFFFFull;
     return WSC_OK;
 }
 int wsc_create(int, const wsc_config* cfg, wsc_ctx** out) {
@@ -57,12 +58,51 @@ int wsc_host_free(void* p) {
 }
 
 // ---- the stand-in walk: one segment ----
+static uint32_t rotr(uint32_t x, uint32_t r) { r &= 31; return r ? (x >> r) | (x << (32 - r)) : x; }
+// unmask n bytes at p with the mask word phased to p (byte i takes mask byte i & 3)
+static void xor_run(uint8_t* p, uint64_t n, uint32_t mask) {
+    for (uint64_t i = 0; i < n; ++i) p[i] ^= (uint8_t)(mask >> (8 * (i & 3)));
+}
 static void walk(const wsc_ctx* c, uint8_t* w, uint64_t a, uint64_t b, uint32_t s, const wsc_conn_state* in,
                  wsc_conn_state* out, wsc_seg_result* r, wsc_frame* fr, uint32_t cap, uint32_t& nf) {
     wsc_conn_state st = in ? *in : wsc_conn_state{};
     uint64_t pos = a;
     uint32_t status = st.status, code = 0, err = 0, k0 = nf;
-    while (status == WSC_SEG_OPEN && b - pos >= 2) {
+    // a streamed data frame's rest (ABI 3): one piece, the last one takes the frame's kind
+    if (status == WSC_SEG_OPEN && st.frame_rem && b > pos) {
+        const uint64_t take = b - pos < st.frame_rem ? b - pos : st.frame_rem;
+        const uint32_t op = st.frame_hdr & 15, fin = st.frame_hdr >> 7;
+        wsc_frame f{};
+        f.hdr_off = pos;
+        f.seg = s;
+        f.msg_id = st.msg_id;
+        f.opcode = (uint8_t)op;
+        f.fin = (uint8_t)fin;
+        f.mode = st.message_mode;
+        f.payload_len = (uint32_t)take;
+        f.payload_len_hi = (uint8_t)(take >> 32);
+        f.mask = st.frame_mask;
+        f.flags = WSC_FF_UNMASKED | WSC_FF_HEAD_PREV;
+        xor_run(w + pos, take, st.frame_mask);
+        if (take < st.frame_rem) {
+            f.kind = WSC_FK_PIECE;
+        } else if (fin) {
+            f.kind = WSC_FK_MESSAGE;
+            if (op == 0 && st.cont_len) f.flags |= WSC_FF_CONT_MSG;
+            st.cont_len = 0;
+            st.message_mode = 0;
+            st.msg_id += 1;
+        } else {
+            f.kind = WSC_FK_FRAG;
+            st.cont_len += st.frame_len;
+        }
+        st.frame_rem -= take;
+        st.frame_mask = rotr(st.frame_mask, 8 * (uint32_t)(take & 3));
+        if (nf < cap) fr[nf] = f;
+        ++nf;
+        pos += take;
+    }
+    while (status == WSC_SEG_OPEN && st.frame_rem == 0 && b - pos >= 2) {
         const uint8_t b0 = w[pos], b1 = w[pos + 1];
         const uint32_t op = b0 & 15, fin = b0 >> 7, len7 = b1 & 127;
         const uint32_t ext = len7 == 126 ? 2 : (len7 == 127 ? 8 : 0);
@@ -99,22 +139,40 @@ static void walk(const wsc_ctx* c, uint8_t* w, uint64_t a, uint64_t b, uint32_t 
             pos += hl;
             break;
         }
-        if (b - pos < hl + plen) break;
+        const bool data = op <= 2;
+        const bool bad = data && ((op == 0 && st.message_mode == 0) || (op != 0 && st.cont_len));
+        uint64_t take = plen;
+        bool piece = false;
+        if (b - pos < hl + plen) {
+            if (!data || bad) break;   // control frames wait whole (the stand-in checks errors first)
+            take = b - pos - hl;
+            piece = true;
+        }
         const uint8_t* m = w + pos + hl - 4;
-        for (uint64_t i = 0; i < plen; ++i) w[pos + hl + i] ^= m[i & 3];
+        uint32_t mask;
+        std::memcpy(&mask, m, 4);
+        if (!bad) xor_run(w + pos + hl, take, mask);
         f.hdr_len = (uint8_t)hl;
-        f.payload_len = (uint32_t)plen;
-        f.payload_len_hi = (uint8_t)(plen >> 32);
-        std::memcpy(&f.mask, m, 4);
+        f.payload_len = (uint32_t)take;
+        f.payload_len_hi = (uint8_t)(take >> 32);
+        f.mask = mask;
         f.flags = WSC_FF_UNMASKED;
         bool stop = false;
-        if (op == 1 || op == 2 || op == 0) {
-            if ((op == 0 && st.message_mode == 0) || (op != 0 && st.cont_len)) {
+        if (data) {
+            if (bad) {
                 f.kind = WSC_FK_ERROR;
                 f.err = WSC_ERR_OPCODE_FAIL;
                 f.flags = 0;
                 status = WSC_SEG_ERROR; code = 1002; err = WSC_ERR_OPCODE_FAIL;
                 stop = true;
+            } else if (piece) {
+                f.kind = WSC_FK_PIECE;
+                if (op) st.message_mode = (uint8_t)op;
+                f.mode = st.message_mode;
+                st.frame_rem = plen - take;
+                st.frame_len = plen;
+                st.frame_mask = rotr(mask, 8 * (uint32_t)(take & 3));
+                st.frame_hdr = (uint8_t)(fin << 7 | op);
             } else if (fin) {
                 f.kind = WSC_FK_MESSAGE;
                 f.mode = op ? (uint8_t)op : st.message_mode;
@@ -141,10 +199,11 @@ static void walk(const wsc_ctx* c, uint8_t* w, uint64_t a, uint64_t b, uint32_t 
         }
         if (nf < cap) fr[nf] = f;
         ++nf;
-        pos += hl + plen;
+        pos += hl + (bad ? 0 : take);
         if (stop) break;
     }
     st.status = (uint8_t)status;
+    if (status != WSC_SEG_OPEN) st.frame_rem = 0;
     *out = st;
     r->consumed = pos - a;
     r->frame_begin = k0;
@@ -182,7 +241,15 @@ int wsc_decode_host(wsc_ctx* c, uint8_t* wire, uint64_t, const uint64_t* seg_off
 }
 }
 
+namespace wsc {
+int set_last_error(int code, const std::string& msg) {   // (wsc_api.cpp in the real library)
+    g_err = msg;
+    return code;
+}
+}  // namespace wsc
+
 // ---- the HIP runtime calls the session makes ----
+const char* hipGetErrorString(hipError_t) { return "stub HIP error"; }
 hipError_t hipSetDevice(int) { return hipSuccess; }
 hipError_t hipStreamCreateWithFlags(hipStream_t* s, unsigned int) {
     *s = reinterpret_cast<hipStream_t>(new int(0));

@@ -32,9 +32,9 @@ def test_struct_sizes_match_header(codec_lib):
 
 
 def test_config_default_and_version(codec_lib):
-    assert codec_lib.wsc_abi_version() == K.ABI_VERSION == 2
+    assert codec_lib.wsc_abi_version() == K.ABI_VERSION == 3
     cfg = K.default_config()
-    assert cfg.max_frame_len == 0x7FFFFFFF and cfg.unmask_window == 4096
+    assert cfg.max_frame_len == (1 << 40) - 1 and cfg.unmask_window == 4096
 
 
 def test_no_silent_cpu_fallback(codec_lib):

@@ -61,7 +61,7 @@ def test_frame_over_4gib(codec_lib, monkeypatch, compact, walk_mode):
     tail = np.frombuffer(post + seg1, dtype=np.uint8)
     wire[p0 + big:p0 + big + len(tail)] = torch.from_numpy(tail.copy()).to(dev)
     seg_off = torch.tensor([0, seg0_len, n_bytes], dtype=torch.int64, device=dev)
-    st_out = torch.zeros(2 * 16, dtype=torch.uint8, device=dev)
+    st_out = torch.zeros(2 * K.STATE_BYTES, dtype=torch.uint8, device=dev)
     seg_out = torch.zeros(2 * 32, dtype=torch.uint8, device=dev)
     frames = torch.zeros(64 * 32, dtype=torch.uint8, device=dev)
     summ = torch.zeros(32, dtype=torch.uint8, device=dev)
@@ -165,7 +165,7 @@ def test_text_frame_over_1gib(codec_lib, compact, bad):
     tail = np.frombuffer(post, dtype=np.uint8)
     wire[p0 + big:p0 + big + len(tail)] = torch.from_numpy(tail.copy()).to(dev)
     seg_off = torch.tensor([0, n_bytes], dtype=torch.int64, device=dev)
-    st_out = torch.zeros(16, dtype=torch.uint8, device=dev)
+    st_out = torch.zeros(K.STATE_BYTES, dtype=torch.uint8, device=dev)
     seg_out = torch.zeros(32, dtype=torch.uint8, device=dev)
     frames = torch.zeros(64 * 32, dtype=torch.uint8, device=dev)
     summ = torch.zeros(32, dtype=torch.uint8, device=dev)

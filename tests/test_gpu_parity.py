@@ -25,7 +25,7 @@ def codec(codec_lib):
     c.close()
 
 
-def _check_batch(codec, streams, compact=False, max_frame_len=0x7FFFFFFF):
+def _check_batch(codec, streams, compact=False, max_frame_len=O.MAX_FRAME_LEN):
     wire, off = pack_streams(streams)
     orig = wire.copy()
     res = codec.decode_host(wire, off, compact=compact)
@@ -243,7 +243,7 @@ def test_device_resident_uniform_64k(codec_lib):
     wire = torch.from_numpy(cfg["wire"]).to(dev)
     seg_off = torch.from_numpy(cfg["seg_off"].view(np.int64)).to(dev)
     n = len(cfg["seg_off"]) - 1
-    st_out = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
+    st_out = torch.zeros(n * K.STATE_BYTES, dtype=torch.uint8, device=dev)
     seg_out = torch.zeros(n * 32, dtype=torch.uint8, device=dev)
     frames = torch.zeros((1 << 16) * 32, dtype=torch.uint8, device=dev)
     summ = torch.zeros(32, dtype=torch.uint8, device=dev)
@@ -293,7 +293,7 @@ def _device_batch(c, cfg, torch, compact=False):
     n = len(cfg["seg_off"]) - 1
     t = dict(wire=torch.from_numpy(cfg["wire"]).to(dev),
              seg_off=torch.from_numpy(cfg["seg_off"].view(np.int64)).to(dev),
-             st_out=torch.zeros(n * 16, dtype=torch.uint8, device=dev),
+             st_out=torch.zeros(n * K.STATE_BYTES, dtype=torch.uint8, device=dev),
              seg_out=torch.zeros(n * 32, dtype=torch.uint8, device=dev),
              frames=torch.zeros((cfg["n_frames"] + 16) * 32, dtype=torch.uint8, device=dev),
              summ=torch.zeros(32, dtype=torch.uint8, device=dev))
@@ -503,7 +503,7 @@ def test_decode_split_pipeline_matches_oracle(codec_lib, compact, layout, inline
                 os.environ["WSC_U8_INLINE_MAX"] = old
         n = len(streams)
         t = dict(wire=torch.from_numpy(wire.copy()).to(dev), seg_off=torch.from_numpy(off.view(np.int64)).to(dev),
-                 st_out=torch.zeros(n * 16, dtype=torch.uint8, device=dev),
+                 st_out=torch.zeros(n * K.STATE_BYTES, dtype=torch.uint8, device=dev),
                  seg_out=torch.zeros(n * 32, dtype=torch.uint8, device=dev),
                  frames=torch.zeros((1 << 15) * 32, dtype=torch.uint8, device=dev),
                  summ=torch.zeros(32, dtype=torch.uint8, device=dev))
@@ -575,7 +575,7 @@ def test_staged_pipeline_back_to_back(codec_lib, monkeypatch, inline_max):
         c = K.Codec(0, max_batch_bytes=len(wire) + 4096, max_segs=len(streams), max_frames=1 << 15)
         n = len(streams)
         t = dict(wire=torch.from_numpy(wire.copy()).to(dev), seg_off=torch.from_numpy(off.view(np.int64)).to(dev),
-                 st_out=torch.zeros(n * 16, dtype=torch.uint8, device=dev),
+                 st_out=torch.zeros(n * K.STATE_BYTES, dtype=torch.uint8, device=dev),
                  seg_out=torch.zeros(n * 32, dtype=torch.uint8, device=dev),
                  frames=torch.zeros((1 << 15) * 32, dtype=torch.uint8, device=dev),
                  summ=torch.zeros(32, dtype=torch.uint8, device=dev),

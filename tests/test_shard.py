@@ -75,3 +75,32 @@ def test_dealt_shards_are_split_of_global_batch():
     # the headers/masks decode like any other batch: the numpy restatement unmasks the payload
     ref = synth.unmask_reference(glob["wire"], glob["payload_off"], glob["plen"], glob["mask"])
     assert np.array_equal(synth.unmask_uniform(glob), ref)
+
+
+def _bench(*args, env_extra=None):
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra or {})
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), *args], capture_output=True, text=True,
+                       timeout=240, env=env, cwd=root)
+    lines = [x for x in p.stdout.splitlines() if x.startswith("{")]
+    return p.returncode, (json.loads(lines[-1]) if lines else None), p.stderr
+
+
+def test_bench_gpus_n_launches_n_ranks():
+    """`bench.py --gpus 2` (the driver's BENCH form, no launcher) must start 2
+    ranks itself -- before touching a GPU -- and report n_gpus == 2; the dry run exercises the
+    launch, the gloo process group, the barrier and the max-over-ranks time without device work"""
+    rc, out, err = _bench("--gpus", "2", "--steps", "3", "--warmup", "1", "--dry-run")
+    assert rc == 0, err[-2000:]
+    assert out["n_gpus"] == 2 and out["rank_sum"] == 1, out     # ranks 0 and 1 both took part
+
+
+def test_bench_world_size_mismatch_fails():
+    """under a launcher whose world size differs from --gpus, the bench refuses to run"""
+    rc, out, err = _bench("--gpus", "4", "--steps", "1", "--warmup", "0", "--dry-run",
+                          env_extra={"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert rc == 2 and out is None and "WORLD_SIZE=2" in err

@@ -28,7 +28,7 @@ for j in range(DEPTH):
     c = K.Codec(0, max_batch_bytes=n_bytes + 4096, max_segs=n_segs, max_frames=16384 + 16)
     t = dict(wire=torch.from_numpy(cfg["wire"]).to(dev),
              seg_off=torch.from_numpy(cfg["seg_off"].view(np.int64)).to(dev),
-             st_out=torch.zeros(n_segs * 16, dtype=torch.uint8, device=dev),
+             st_out=torch.zeros(n_segs * K.STATE_BYTES, dtype=torch.uint8, device=dev),
              seg_out=torch.zeros(n_segs * 32, dtype=torch.uint8, device=dev),
              frames=torch.zeros((16384 + 16) * 32, dtype=torch.uint8, device=dev),
              summ=torch.zeros(32, dtype=torch.uint8, device=dev))

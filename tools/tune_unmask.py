@@ -39,7 +39,7 @@ dev = torch.device("cuda:0")
 n_segs = len(cfg["seg_off"]) - 1
 wire = torch.from_numpy(cfg["wire"]).to(dev)
 seg_off = torch.from_numpy(cfg["seg_off"].view(np.int64)).to(dev)
-st_out = torch.zeros(n_segs * 16, dtype=torch.uint8, device=dev)
+st_out = torch.zeros(n_segs * K.STATE_BYTES, dtype=torch.uint8, device=dev)
 seg_out = torch.zeros(n_segs * 32, dtype=torch.uint8, device=dev)
 frames = torch.zeros((cfg["n_frames"] + 16) * 32, dtype=torch.uint8, device=dev)
 summ = torch.zeros(32, dtype=torch.uint8, device=dev)
