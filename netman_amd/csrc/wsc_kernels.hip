@@ -127,21 +127,22 @@ __device__ __forceinline__ void emit_frame(const WalkArgs& a, EmitCtx& e, const 
         }
     }
     if (have_span) {
-        // a payload of 4 GiB or more is cut into SPAN_CHUNK-byte spans (multiples of 4 bytes, so
-        // every piece keeps the frame's wire-phased key); span_chunks() counted them the same way
-        const uint32_t nch = span_chunks(plen);
+        // a payload of 4 GiB or more is cut at absolute SPAN_CHUNK-aligned wire offsets (the key
+        // is wire-phased, so every piece keeps it); span_chunks() counted them the same way
         const uint64_t src0 = fr.hdr_off + fr.hdr_len;
+        const uint32_t nch = span_chunks(src0, plen);
         uint64_t dst0 = src0;
         if (COMPACT && region) dst0 = e.abase + e.own_bytes0 + e.nb1;
         else if (COMPACT) dst0 = e.abase + e.nb0;
         // the key is phased at the wire: every aligned wire dword XORs with one register
         const uint32_t key = rotr32(fr.mask, 8u * ((uint32_t)(0u - (uint32_t)src0) & 3u));
         for (uint32_t c = 0; c < nch; ++c) {
-            const uint64_t off = (uint64_t)c * SPAN_CHUNK;
+            const uint64_t cs = c == 0 ? src0 : ((src0 >> 31) + c) << 31;
+            const uint64_t ce = c + 1 == nch ? src0 + plen : ((src0 >> 31) + c + 1) << 31;
             Span sp;
-            sp.src = src0 + off;
-            sp.dst = dst0 + off;
-            sp.len = (uint32_t)(c + 1 == nch ? plen - off : SPAN_CHUNK);
+            sp.src = cs;
+            sp.dst = dst0 + (cs - src0);
+            sp.len = (uint32_t)(ce - cs);
             sp.key = key;
             const uint32_t idx = e.sbase + e.ns0 + e.ns1 + c;   // stream order
             if (idx < a.spans_cap) a.spans[idx] = sp;
@@ -424,7 +425,7 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
         nf += 1;
         if (have_span) {
             if (COMPACT && region) { ns1 += 1; nb1 += plen; }   // control payloads: <= 125 B
-            else { ns0 += span_chunks(plen); nb0 += plen; }
+            else { ns0 += span_chunks(fr.hdr_off + fr.hdr_len, plen); nb0 += plen; }
         }
     };
 
@@ -697,7 +698,7 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
         msg += 1;
         mode = 0;
         nf += 1;
-        if (have_span) { ns0 += span_chunks(plen); nb0 += plen; }
+        if (have_span) { ns0 += span_chunks(pos + hl, plen); nb0 += plen; }
         pos += hl + plen;
         return true;
     };

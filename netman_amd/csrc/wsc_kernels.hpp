@@ -64,10 +64,12 @@ struct U8Seg {          // per segment with deferred items (written by the walk)
 // same bytes (in place) or the arena (COMPACT).  `key` is the mask word rotated so that it XORs
 // 4-byte-aligned destination dwords directly: key = rotr(mask, 8 * ((-dst) & 3)).
 // spans carry u32 lengths: a payload of 4 GiB or more (64-bit length, websocket.go:291-299) is
-// cut into spans of SPAN_CHUNK bytes; everything shorter is one span
+// cut into spans at the ABSOLUTE wire offsets that are multiples of SPAN_CHUNK (2 GiB) -- window
+// boundaries, so no unmask window ever holds a cut (every window inside a text payload stays a
+// one-span fast-path window whose UTF-8 map the unmask folds); everything shorter is one span
 constexpr uint64_t SPAN_CHUNK = 1ull << 31;
-__host__ __device__ __forceinline__ uint32_t span_chunks(uint64_t plen) {
-    return plen <= 0xFFFFFFFFull ? 1u : (uint32_t)((plen + SPAN_CHUNK - 1) >> 31);
+__host__ __device__ __forceinline__ uint32_t span_chunks(uint64_t src, uint64_t plen) {
+    return plen <= 0xFFFFFFFFull ? 1u : (uint32_t)(((src + plen - 1) >> 31) - (src >> 31) + 1);
 }
 
 struct Span {

@@ -128,17 +128,21 @@ def test_max_frame_len_limit(codec_lib):
         K.Codec(0, max_batch_bytes=1 << 20, max_segs=4, max_frames=64, max_frame_len=1 << 40)
 
 
-@pytest.mark.parametrize("compact,bad", [(False, False), (False, True), (True, True)])
-def test_text_frame_over_1gib(codec_lib, compact, bad):
+@pytest.mark.parametrize("compact,bad,big", [(False, False, (2 << 30) + 4100), (False, True, (2 << 30) + 4100),
+                                             (True, True, (2 << 30) + 4100), (False, False, (4 << 30) + 4100),
+                                             (True, True, (4 << 30) + 4100)])
+def test_text_frame_over_1gib(codec_lib, compact, bad, big):
     """a TEXT frame of 2 GiB + 4100 B: three UTF-8 items cut at 1 GiB-aligned wire offsets with
     2-byte characters straddling every cut, most of it folded window by window inside the unmask,
     the item ends in k_u8_check, the three items composed by k_u8_verdict.  With one 0xFF byte at
     1.5 GiB the connection must stop at that frame with 1007 (websocket_frame.go:71-73,
     epoll.go:126-127) and the TEXT frame after it must be left masked (re-masked after the unmask);
-    valid, the frame after it is a Message.  The payload is built and checked on the device."""
+    valid, the frame after it is a Message.  The payload is built and checked on the device.
+    4 GiB + 4100 B: the payload (starting 24 B into the wire, not window-aligned) is
+    cut into 2 GiB spans -- at absolute 2 GiB wire offsets, so no unmask window holds a cut and
+    every window inside the text is folded (a cut inside a window left its map unwritten)."""
     torch = pytest.importorskip("torch")
     dev = torch.device("cuda:0")
-    big = (2 << 30) + 4100
     mask_big = 0x5EC0DE11
     pre = synth.frame(1, "pré".encode(), mask=0x01020304)
     post = synth.frame(1, "après".encode(), mask=0x0BADF00D)
@@ -177,6 +181,7 @@ def test_text_frame_over_1gib(codec_lib, compact, bad):
     c.sync()
     sm = summ.cpu().numpy().copy().view(K.SUMMARY_DTYPE)[0]
     assert K.Codec.summary_status(sm) == K.WSC_OK and int(sm["n_frames"]) == 3
+    assert int(sm["n_spans"]) == 2 + (1 if big < (4 << 30) else 3)
     seg = seg_out.cpu().numpy().copy().view(K.SEG_RESULT_DTYPE)[0]
     fr = frames.cpu().numpy().copy().view(K.FRAME_DTYPE)[:3]
     assert K.frame_len(fr[1]) == big and int(fr[1]["opcode"]) == 1
