@@ -20,7 +20,6 @@ template <bool COMPACT> __global__ void k_walk_count(WalkArgs);
 __global__ void k_walk_scan(WalkArgs, uint32_t);
 template <bool COMPACT> __global__ void k_walk_emit(WalkArgs);
 template <uint32_t NCH> __global__ void k_u8_check(U8Args);
-__global__ void k_u8_verdict(U8Args);
 template <bool COMPACT, int P, int NT, int MINW, bool U8>
 __global__ void k_unmask(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*,
                          const wsc_summary*, uint32_t*, uint32_t, uint32_t*, uint32_t*, uint32_t, U8Win);
@@ -95,10 +94,13 @@ struct wsc_ctx {
     U8Seg* u8seg = nullptr;
     uint32_t* win_flag = nullptr;       // per unmask window: inside a deferred text item (walk sets, unmask clears)
     uint64_t* win_map = nullptr;        // per unmask window: the DFA map the unmask folded
-    uint32_t* u8done = nullptr;         // [0] k_u8_verdict finished workgroups, [32] listed segments (self re-arming)
-    uint32_t* u8seglist = nullptr;      // segments with deferred UTF-8 items
+    uint32_t* u8ctr = nullptr;          // UTF-8 item counters, one per decode parity ([0], [32]): a decode's walk
+                                        // allocates from its own, its unmask zeroes the other (the next decode's)
+    uint32_t u8par = 0;                 // parity of the decode the last walk belongs to
     uint32_t u8_inline_max = 256;
     uint32_t u8_grid = 0;               // WSC_U8_GRID: k_u8_check workgroups (A/B experiments; 0 = 5 per CU)
+    bool ab_no_u8 = false;              // WSC_AB_NO_U8=1: A/B timing only -- binary unmask, no UTF-8 launches
+                                        // (wrong for text batches; never set in tests or the bench)
     int walk_mode = 0;                  // WSC_WALK_MODE: 64, 256 or 3 pins the walk geometry (A/B, tests); 0 = auto
     uint32_t walk_used = 0;             // geometry (64 / 256 / 3) and block count of the last walk launched:
     uint32_t walk_blocks = 0;           // the staged unmask re-arms exactly that walk's look-back flags
@@ -294,16 +296,16 @@ int wsc_create(int device, const wsc_config* cfg_in, wsc_ctx** out) {
     chk(hipMalloc(&c->u8seg, (uint64_t)cfg.max_segs * sizeof(U8Seg)), "hipMalloc u8seg");
     chk(hipMalloc(&c->win_flag, c->tile_entries * sizeof(uint32_t)), "hipMalloc win_flag");
     chk(hipMalloc(&c->win_map, c->tile_entries * sizeof(uint64_t)), "hipMalloc win_map");
-    chk(hipMalloc(&c->u8done, 64 * sizeof(uint32_t)), "hipMalloc u8done");
-    chk(hipMalloc(&c->u8seglist, (uint64_t)cfg.max_segs * sizeof(uint32_t)), "hipMalloc u8seglist");
+    chk(hipMalloc(&c->u8ctr, 64 * sizeof(uint32_t)), "hipMalloc u8ctr");
     if (rc == WSC_OK) {
         chk(hipMemsetAsync(c->win_flag, 0, c->tile_entries * sizeof(uint32_t), c->stream), "hipMemset win_flag");
-        chk(hipMemsetAsync(c->u8done, 0, 64 * sizeof(uint32_t), c->stream), "hipMemset u8done");
+        chk(hipMemsetAsync(c->u8ctr, 0, 64 * sizeof(uint32_t), c->stream), "hipMemset u8ctr");
         chk(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
     }
     if (const char* e = std::getenv("WSC_UNMASK_BUF"); e && *e) c->unmask_buf = std::atoi(e);
     if (const char* e = std::getenv("WSC_U8_CHAINS"); e && *e) c->u8_chains = std::atoi(e);
     if (const char* e = std::getenv("WSC_U8_GRID"); e && *e) c->u8_grid = (uint32_t)std::strtoul(e, nullptr, 10);
+    if (const char* e = std::getenv("WSC_AB_NO_U8"); e && e[0] == '1') c->ab_no_u8 = true;
     if (const char* e = std::getenv("WSC_WALK_MODE"); e && *e) {   // pin a walk geometry (tests, A/B): 64, 256 or 3
         const int m = std::atoi(e);
         c->walk_mode = (m == 64 || m == 256 || m == 3) ? m : 0;
@@ -339,7 +341,7 @@ int wsc_destroy(wsc_ctx* c) {
                     c->d_seg_off, c->d_state_in, c->d_state_out, c->d_seg_out, c->d_frames,
                     c->d_frame_dst, c->d_summary, c->enc_lb_state, c->enc_lb_agg, c->enc_lb_incl, c->enc_tile,
                     c->d_enc_msgs, c->d_enc_src, c->d_enc_out, c->d_enc_off, c->u8items, c->u8maps, c->u8seg,
-                    c->win_flag, c->win_map, c->u8done, c->u8seglist};
+                    c->win_flag, c->win_map, c->u8ctr};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -417,15 +419,14 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     wa.summary = b->summary;
     wa.u8items = c->u8items;
     wa.u8items_cap = c->u8items_cap;
-    wa.u8count = c->lb_state + 2;
+    if (phase != 2) c->u8par ^= 1u;   // a new decode: the other item counter (zeroed by the last unmask)
+    wa.u8count = c->u8ctr + 32 * c->u8par;
     wa.u8seg = c->u8seg;
     wa.u8_inline_max = c->u8_inline_max;
     wa.sticky = c->sticky;
     wa.u8host = c->hflag;
     wa.win_flag = c->win_flag;
-    wa.u8seglist = c->u8seglist;
     wa.compact = compact ? 1u : 0u;
-    wa.u8segcnt = c->u8done + 32;
 
     // walk geometry: the fused walk with blocks that fill the CUs once (64 lanes for up to 64
     // segments per CU, else 256), or -- for more segments than the chip holds lanes at once -- the
@@ -482,7 +483,7 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     // deferred UTF-8 (large text) runs after the unmask (which folds the text windows it unmasks):
     // both the fold and the check are skipped when the walk has completed and its host-visible
     // flag says it deferred nothing -- the check would still be a launch between two unmasks
-    const bool need_u8 = !(walked && __atomic_load_n(&c->hflag[0], __ATOMIC_ACQUIRE) == 0);
+    const bool need_u8 = !c->ab_no_u8 && !(walked && __atomic_load_n(&c->hflag[0], __ATOMIC_ACQUIRE) == 0);
     const bool signal = phase == 2;   // staged: the decode's last kernel signals the host, no ev_done
 
     uint8_t* udst = compact ? b->arena : b->wire;
@@ -515,10 +516,11 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
         kern = table_buf[ui][pi][c->unmask_buf - 1];
     const bool sig_unmask = signal && !need_u8;
     U8Win uw{};
+    uw.rearm = c->u8ctr + 32 * (c->u8par ^ 1u);
     if (need_u8) {
         uw.flag = c->win_flag;
         uw.map = c->win_map;
-        uw.count = c->lb_state + 2;
+        uw.count = c->u8ctr + 32 * c->u8par;
     }
     hipLaunchKernelGGL(kern, ugrid, ublk, 0, st, udst, (const uint8_t*)b->wire, b->n_bytes, b->n_bytes,
                        (const Span*)c->spans, (const uint32_t*)c->tile, (const wsc_summary*)b->summary,
@@ -532,7 +534,7 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
         ua.n_bytes = b->n_bytes;
         ua.seg_off = b->seg_off;
         ua.items = c->u8items;
-        ua.count = c->lb_state + 2;
+        ua.count = c->u8ctr + 32 * c->u8par;
         ua.items_cap = c->u8items_cap;
         ua.maps = c->u8maps;
         ua.seg = c->u8seg;
@@ -545,10 +547,8 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
         ua.win_shift = ilog2(c->pieces * 1024);
         ua.unmasked = compact ? 0u : 1u;
         ua.out = udst;
-        ua.done = c->u8done;
         ua.n_segs = n;
-        ua.seglist = c->u8seglist;
-        ua.segcnt = c->u8done + 32;
+        ua.fin_ctr = c->fin_ctr;
         ua.fin_host = signal ? c->hflag + 1 : nullptr;
         ua.fin_seq = c->fin_seq + 1;
         const dim3 ug(c->u8_grid ? c->u8_grid : (uint32_t)c->n_cu * 4);   // resident: 4 waves/SIMD (128 VGPRs;
@@ -556,9 +556,6 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
         if (c->u8_chains == 1) hipLaunchKernelGGL(k_u8_check<1>, ug, dim3(256), 0, st, ua);
         else if (c->u8_chains == 4) hipLaunchKernelGGL(k_u8_check<4>, ug, dim3(256), 0, st, ua);
         else hipLaunchKernelGGL(k_u8_check<2>, ug, dim3(256), 0, st, ua);
-        HIP_TRY(hipGetLastError());
-        // (grid-stride over the listed segments; a small grid: an empty launch costs ~2 us)
-        hipLaunchKernelGGL(k_u8_verdict, dim3(std::min<uint32_t>((n + 255) / 256, (uint32_t)c->n_cu / 2)), dim3(256), 0, st, ua);
         HIP_TRY(hipGetLastError());
     }
     rec(3);

@@ -131,5 +131,27 @@ __device__ __forceinline__ void st16(uint8_t* p, uint4 v) {
     st16v<NT>(p, t);
 }
 
+// Staged pipeline: the LAST workgroup of a grid to finish writes fin_seq to the host-visible word
+// (wsc_api.cpp fin_wait) -- called by thread 0 of every workgroup after a __syncthreads, once its
+// workgroup's accesses to the walk's scratch are done.  A grid is up to 2^16+ workgroups: one
+// device-scope counter would serialise them (measured 5.9 ms for 64 Ki), so the count is
+// two-level -- FIN_GROUPS counters a cache line apart, each finished by its last workgroup, which
+// bumps the top counter.  Every level re-arms itself for the next launch.  Vector atomics only.
+constexpr uint32_t FIN_GROUPS = 256, FIN_STRIDE = 32;   // fin_ctr: (FIN_GROUPS + 1) * FIN_STRIDE words
+__device__ __forceinline__ void fin_signal(uint32_t* fin_ctr, uint32_t* fin_host, uint32_t fin_seq) {
+    const uint32_t g = blockIdx.x % FIN_GROUPS;
+    const uint32_t in_g = (gridDim.x - g + FIN_GROUPS - 1) / FIN_GROUPS;   // workgroups of group g
+    uint32_t* cg = fin_ctr + (1 + g) * FIN_STRIDE;
+    if (__hip_atomic_fetch_add(cg, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == in_g - 1) {
+        __hip_atomic_store(cg, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t groups = gridDim.x < FIN_GROUPS ? gridDim.x : FIN_GROUPS;
+        if (__hip_atomic_fetch_add(fin_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == groups - 1) {
+            __hip_atomic_store(fin_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __threadfence_system();
+            __hip_atomic_store(fin_host, fin_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __threadfence_system();
+        }
+    }
+}
 
 }  // namespace wsc

@@ -9,7 +9,7 @@
 //   utf8.Valid (websocket_frame.go:71-73, websocket.go:170-172): payloads up to u8_inline_max run
 //   inside the walk's counting pass on the still-masked wire, so a connection whose text is invalid
 //   stops at that frame.  Larger ones are deferred: the unmask folds the windows it unmasks
-//   (wsc_unmask.inl), k_u8_check the partial windows, k_u8_verdict applies 1007 (below).
+//   (wsc_unmask.inl), k_u8_check the partial windows and applies 1007 (below).
 #include "wsc_kernels.hpp"
 #include "wsc_dev.hpp"
 #include "wsc_u8.hpp"
@@ -750,19 +750,6 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
             a.u8info[2 * s] = u8fail;
             a.u8info[2 * s + 1] = u8dfa;
         }
-        // segments with deferred items are listed for k_u8_verdict (one atomic per wave, at the
-        // segment's end: off the header chain, and never for binary batches)
-        const uint64_t has = __ballot(u8_n != 0);
-        if (has) {
-            const uint32_t leader = (uint32_t)__builtin_ctzll(has);
-            uint32_t base = 0;
-            if (lane_id() == leader)
-                base = __hip_atomic_fetch_add(a.u8segcnt, (uint32_t)__builtin_popcountll(has), __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_AGENT);
-            base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)leader);
-            if (u8_n)
-                a.u8seglist[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(has >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)has, 0u))] = s;
-        }
         if (u8_n) {
             U8Seg g{};
             g.head = u8_head;
@@ -1270,21 +1257,30 @@ __global__ __launch_bounds__(NT) void k_walk_fused(WalkArgs a) {
 // their ends, folds them (each lane one 64-byte chunk, waves compose lanes), composes head, window
 // maps and tail per item: a whole TEXT message (one piece, SELF) is decided on the spot (its
 // ordinal min-folded into the segment's first failure), any other item publishes its map.
-// k_u8_verdict, one lane per segment, composes the published maps in frame order with the states
-// the walk recorded and applies the verdict: the first failing frame becomes WSC_FK_ERROR / 1007,
-// the segment stops there, and the spans of later frames -- already unmasked -- are XORed again,
-// so the bytes are left as the reference leaves them (never read).  Maps: wsc_u8.hpp.
+// Decoupled verdicts, in the same launch: every published item counts itself into its segment
+// (U8Seg.done); the lane whose item completes a segment composes the segment's published maps in
+// frame order with the states the walk recorded and applies the verdict: the first failing frame
+// becomes WSC_FK_ERROR / 1007, the segment stops there, and the spans of later frames -- already
+// unmasked -- are XORed again by the wave, so the bytes are left as the reference leaves them
+// (never read).  No second launch and no grid-wide wait.  Maps: wsc_u8.hpp.
+// Cross-XCD hand-off (L2 is per XCD): maps are published with agent-scope (sc1) stores and the
+// failures with agent-scope atomics, drained (s_waitcnt) before the segment's counter increment;
+// the completing lane reads them with agent-scope atomic RMWs (MI355X_MICROARCH.md "Valid forms").
 // ---------------------------------------------------------------------------------------------
 
-// One item's result: no waiting, no counter (the verdict kernel runs after this launch).
-__device__ __forceinline__ void u8_publish(const U8Args& a, uint32_t it, const U8Item& self, uint64_t acc) {
-    if (self.seg == U8_DEAD) return;   // an unused slot of a walk pool
+// One item's result; true if it was the last item of its segment to finish (its lane then decides
+// the segment's verdict).
+__device__ __forceinline__ bool u8_publish(const U8Args& a, uint32_t it, const U8Item& self, uint64_t acc) {
+    if (self.seg == U8_DEAD) return false;   // an unused slot of a walk pool
     if (self.kind == U8K_SELF && self.first && self.last) {
         if (u8m_get(acc, 0) != 0)
             __hip_atomic_fetch_min(&a.seg[self.seg].minfail, self.ordinal, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
-        a.maps[it] = acc;
+        __hip_atomic_store(a.maps + it, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t n = a.seg[self.seg].n;
+    return __hip_atomic_fetch_add(&a.seg[self.seg].done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 == n;
 }
 
 // A segment's verdict (one lane): the first failing frame -- the single-piece SELF items' minimum
@@ -1292,7 +1288,7 @@ __device__ __forceinline__ void u8_publish(const U8Args& a, uint32_t it, const U
 // end (the wave then re-masks the later spans), else ~0.
 __device__ __forceinline__ uint64_t u8_verdict(const U8Args& a, uint32_t s, const U8Seg& g) {
     uint32_t cur = 0, start = 0;   // states 0..7, 0xFF = reject
-    uint32_t fail = g.minfail;
+    uint32_t fail = __hip_atomic_fetch_add(&a.seg[s].minfail, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // compose the composite items in frame order with the walk's states (a chain never has a
     // single-piece SELF item inside it)
     uint64_t fm = u8m_id();
@@ -1301,7 +1297,7 @@ __device__ __forceinline__ uint64_t u8_verdict(const U8Args& a, uint32_t s, cons
         const U8Item x = a.items[j];
         if (x.ordinal >= fail) break;   // a single-piece SELF frame failed first
         if (x.kind == U8K_SELF && x.first && x.last) { j = x.next; continue; }
-        const uint64_t m = a.maps[j];
+        const uint64_t m = __hip_atomic_fetch_add(a.maps + j, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (x.first) {
             start = x.kind == U8K_SELF ? 0u : (x.s_in != 0xFF ? (x.s_in > 7 ? 0xFFu : (uint32_t)x.s_in) : cur);
             fm = u8m_id();
@@ -1374,8 +1370,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
     __shared__ U8Lds T;
     __shared__ uint4 stage[4][U8_STAGE];
     const uint32_t lane = threadIdx.x & 63;
-    if (blockIdx.x * 4 >= n_items) return;   // nothing deferred (or fewer units than waves)
-    {
+    // a batch whose records overflowed is invalid as a whole (the caller re-decodes it): its
+    // verdicts are not applied -- the failing frame or its later spans may lie past the capacity
+    const bool ovf = a.summary->overflow != 0;
+    // segments completed by this wave's items: their verdicts (one lane each, serial over the
+    // segment's items), failing ones re-masked by the whole wave
+    auto settle = [&](bool trig, uint32_t seg) {
+        uint64_t pend = __ballot(trig);
+        while (pend) {
+            const uint32_t l = (uint32_t)__builtin_ctzll(pend);
+            pend &= pend - 1;
+            const uint32_t sg = (uint32_t)__builtin_amdgcn_readlane((int)seg, (int)l);
+            uint64_t fe = ~0ull;
+            if (lane == l && !ovf) fe = u8_verdict(a, sg, a.seg[sg]);
+            const uint64_t fend = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(fe >> 32), (int)l) << 32 |
+                                  (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)fe, (int)l);
+            if (fend != ~0ull) u8_remask(a, sg, fend, lane);
+        }
+    };
+    if (blockIdx.x * 4 < n_items) {   // (nothing deferred, or fewer units than waves: only the signal)
     u8_tables_init(T, threadIdx.x);
     __syncthreads();
     const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
@@ -1475,7 +1488,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
                 b0 = nb;
             }
             if (!mids_in) acc = u8m_then(acc, mids);
-            if (lane == 0) u8_publish(a, i0 + j, item, acc);
+            bool done = false;
+            if (lane == 0) done = u8_publish(a, i0 + j, item, acc);
+            settle(done, item.seg);
         }
     };
     const uint32_t n_units = (n_items + 3) / 4;
@@ -1539,7 +1554,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
                 nsmall = unit_small(xn);
                 if (nsmall) unit_data(xn, qn);
             }
-            if ((lane & 15) == 0 && r < cnt) u8_publish(a, i0 + r, xr, rm);
+            bool done = false;
+            if ((lane & 15) == 0 && r < cnt) done = u8_publish(a, i0 + r, xr, rm);
+            settle(done, xr.seg);
         } else {
             unit_large(i0, cnt);
             if (un < n_units) {
@@ -1554,55 +1571,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
         if (un + nw < n_units) unit_items(un + nw, xn);
     }
     }
-}
-
-// One lane per listed segment (the walk lists those with deferred items).  The last workgroup
-// re-arms the item count (the next walk allocates from it) and, in the staged pipeline, tells the
-// host that this decode no longer reads the context's scratch (every scratch access before the
-// count is complete: reads were consumed).  No fence per workgroup: an agent-scope release writes
-// back the XCD's L2 (1,280 of them cost ~0.4 ms, measured).
-__global__ __launch_bounds__(256) void k_u8_verdict(U8Args a) {
-    // a batch whose records overflowed is invalid as a whole (the caller re-decodes it): its
-    // verdicts are not applied -- the failing frame or its later spans may lie past the capacity
-    const bool ovf = a.summary->overflow != 0;
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t listed = *a.segcnt;
-    // nothing deferred (a binary batch through wsc_decode): nothing to decide, nothing to re-arm,
-    // nobody to signal -- every workgroup sees the same words and leaves without the counter
-    if (listed == 0 && *a.count == 0 && a.fin_host == nullptr) return;
-    const uint32_t nseg = listed < a.n_segs ? listed : a.n_segs;   // segments with deferred items
-    // grid-stride over the list, whole waves per step (the re-mask below is wave-cooperative)
-    for (uint32_t b = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); b < nseg && !ovf; b += gridDim.x * blockDim.x) {
-        const uint32_t i = b + lane;
-        uint32_t s = 0;
-        uint64_t fe = ~0ull;
-        if (i < nseg) {
-            s = a.seglist[i];
-            fe = u8_verdict(a, s, a.seg[s]);
-        }
-        // failing segments: their later spans re-masked by the whole wave
-        uint64_t pend = __ballot(fe != ~0ull);
-        while (pend) {
-            const uint32_t l = (uint32_t)__builtin_ctzll(pend);
-            pend &= pend - 1;
-            const uint32_t seg = (uint32_t)__builtin_amdgcn_readlane((int)s, (int)l);
-            const uint64_t fend = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(fe >> 32), (int)l) << 32 |
-                                  (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)fe, (int)l);
-            u8_remask(a, seg, fend, lane);
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        if (__hip_atomic_fetch_add(a.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
-            __hip_atomic_store(a.count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(a.segcnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(a.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (a.fin_host) {
-                __threadfence_system();
-                __hip_atomic_store(a.fin_host, a.fin_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                __threadfence_system();
-            }
-        }
+    // staged pipeline: the decode's last kernel tells the host its scratch is free
+    if (a.fin_host) {
+        __syncthreads();
+        if (threadIdx.x == 0) fin_signal(a.fin_ctr, a.fin_host, a.fin_seq);
     }
 }
 

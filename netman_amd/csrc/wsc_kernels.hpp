@@ -107,28 +107,27 @@ struct WalkArgs {
     uint32_t* u8info;            // per segment: {first utf8-failing frame ordinal, DFA state}
     U8Item* u8items;             // deferred UTF-8 items
     uint32_t u8items_cap;
-    uint32_t* u8count;           // item counter (re-armed by k_unmask)
+    uint32_t* u8count;           // item counter, one per decode parity (re-armed by the next decode's k_unmask)
     U8Seg* u8seg;
     uint32_t u8_inline_max;      // text payloads up to this many bytes are validated in the walk
     uint32_t* sticky;            // context error bits, never re-armed by a kernel (wsc_error_flags)
     uint32_t* u8host;            // host-visible word set when any UTF-8 item is deferred (cleared by the host)
     uint32_t* win_flag;          // per unmask window: 1 = inside a deferred text item (k_unmask folds its map)
-    uint32_t* u8seglist;         // segments with deferred items (for k_u8_verdict)
-    uint32_t* u8segcnt;          // ... their count (re-armed by k_u8_verdict)
     uint32_t compact;            // WSC_F_COMPACT (k_walk_scan: the other kernels are templated on it)
 };
 
 // k_u8_check runs AFTER the unmask: the unmask has already folded every text window that lies
 // inside an item (win_map), so the check reads only the items' partial windows at their ends --
 // in place from the unmasked wire (mask 0), COMPACT from the still-masked wire -- composes, and
-// applies the verdicts.  Frames after a failing one were unmasked too: their spans are XORed
-// again (re-masked), so the output equals what the reference leaves (it never reads them).
+// applies the verdicts (segment by segment, as their last items finish).  Frames after a failing
+// one were unmasked too: their spans are XORed again (re-masked), so the output equals what the
+// reference leaves (it never reads them).
 struct U8Args {
     const uint8_t* wire;
     uint64_t n_bytes;
     const uint64_t* seg_off;
     const U8Item* items;
-    uint32_t* count;             // item count: re-armed by the check's last workgroup
+    const uint32_t* count;       // item count (this decode's parity)
     uint32_t items_cap;
     uint64_t* maps;              // per item: DFA transition map (9 x 4 bits)
     U8Seg* seg;
@@ -142,10 +141,8 @@ struct U8Args {
     uint32_t unmasked;           // 1: the wire is already unmasked (in place): items are read with mask 0
     uint8_t* out;                // where the spans' bytes went: the wire (in place) or the arena (COMPACT)
     uint32_t n_segs;
-    const uint32_t* seglist;     // segments with deferred items (the walk's list)
-    uint32_t* segcnt;            // ... their count (re-armed with the item count)
-    uint32_t* done;              // k_u8_verdict's finished workgroups (self re-arming)
-    uint32_t* fin_host;          // staged pipeline: the last workgroup writes fin_seq here
+    uint32_t* fin_ctr;           // staged pipeline: finished-workgroup counters (fin_signal)
+    uint32_t* fin_host;          // ... the last workgroup writes fin_seq here
     uint32_t fin_seq;
 };
 
@@ -155,6 +152,7 @@ struct U8Win {
     uint32_t* flag;
     uint64_t* map;
     const uint32_t* count;
+    uint32_t* rearm;             // the next decode's item counter (zeroed by the unmask: always launched)
 };
 
 

@@ -406,10 +406,12 @@ __device__ __forceinline__ void unmask_all(uint8_t* __restrict__ dst, const uint
     if constexpr (U8) if (threadIdx.x == 0) g_u8b.state = 0;
     __syncthreads();
     // re-arm the walk's look-back state for the next decode (this launch is ordered after it):
-    // lb_state[0] = ticket, [1] = timeout flag, [3 ...] = per-block flags ([2], the UTF-8 item
-    // count, is read by k_u8_check after this launch, which re-arms it)
+    // lb_state[0] = ticket, [1] = timeout flag, [3 ...] = per-block flags; and the UTF-8 item
+    // counter of the OTHER parity (the next decode's; this decode's is read by k_u8_check after
+    // this launch, and re-armed by the next decode's unmask)
     for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n_walk_blocks + 2; t += gridDim.x * blockDim.x)
-        if (t != 2) lb_state[t] = 0;
+        lb_state[t] = 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && u8w.rearm) *u8w.rearm = 0;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t waves_per_block = blockDim.x >> 6;
     const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * waves_per_block + (threadIdx.x >> 6));
@@ -470,14 +472,10 @@ __device__ __forceinline__ void unmask_all(uint8_t* __restrict__ dst, const uint
 }
 
 // fin_host (staged pipeline): the last workgroup to finish writes fin_seq to the host-visible
-// word, after every workgroup has done all its reads of the walk's spans / window index -- the
-// host then lets the next walk reuse them (wsc_api.cpp fin_wait).  A grid is up to 2^16+
-// workgroups: one device-scope counter would serialise them (measured 5.9 ms for 64 Ki), so the
-// count is two-level -- FIN_GROUPS counters a cache line apart, each finished by its last
-// workgroup, which bumps the top counter.  The workgroups that re-armed lb_state release it
-// before counting (the next walk may run while this grid's tail drains).  Every level re-arms
-// itself for the next launch.  Vector atomics and stores only.
-constexpr uint32_t FIN_GROUPS = 256, FIN_STRIDE = 32;   // fin_ctr: (FIN_GROUPS + 1) * FIN_STRIDE words
+// word (fin_signal, wsc_dev.hpp), after every workgroup has done all its reads of the walk's spans
+// / window index -- the host then lets the next walk reuse them (wsc_api.cpp fin_wait).  The
+// workgroups that re-armed lb_state release it before counting (the next walk may run while this
+// grid's tail drains).
 template <bool COMPACT, int P, int NT, int MINW = 1, bool U8 = false>
 __global__ __launch_bounds__(256, (P == 4 ? 4 : 2) * MINW) void k_unmask(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src,
                                                 uint64_t src_bytes, uint64_t total,
@@ -491,19 +489,7 @@ __global__ __launch_bounds__(256, (P == 4 ? 4 : 2) * MINW) void k_unmask(uint8_t
     __syncthreads();
     if (threadIdx.x == 0) {
         if (blockIdx.x * blockDim.x < n_walk_blocks + 2) __threadfence();   // lb_state re-arm visible first
-        const uint32_t g = blockIdx.x % FIN_GROUPS;
-        const uint32_t in_g = (gridDim.x - g + FIN_GROUPS - 1) / FIN_GROUPS;   // workgroups of group g
-        uint32_t* cg = fin_ctr + (1 + g) * FIN_STRIDE;
-        if (__hip_atomic_fetch_add(cg, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == in_g - 1) {
-            __hip_atomic_store(cg, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const uint32_t groups = gridDim.x < FIN_GROUPS ? gridDim.x : FIN_GROUPS;
-            if (__hip_atomic_fetch_add(fin_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == groups - 1) {
-                __hip_atomic_store(fin_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __threadfence_system();
-                __hip_atomic_store(fin_host, fin_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                __threadfence_system();
-            }
-        }
+        fin_signal(fin_ctr, fin_host, fin_seq);
     }
 }
 

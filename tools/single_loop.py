@@ -1,6 +1,7 @@
 """Back-to-back decodes of one device batch on one stream (one batch in flight), for kernel-trace
 gap analysis:  python tools/single_loop.py <config> [iters]
 config: head (16384 x 64 KiB, 4/seg) | c1 (1M x 1 KiB, 16/seg) | c2 (256k mixed, 16/seg) |
+c4 (64k fragmented messages, COMPACT) |
 t64 / t1 (TEXT 16384 x 64 KiB / 262144 x 1 KiB; wire restored before each decode, wall time includes the copy)"""
 import os
 import sys
@@ -22,6 +23,8 @@ def main():
            "c1": lambda: synth.uniform_batch(1 << 20, 1024, 16, seed=synth.SEED_BASE + 1),
            "c11": lambda: synth.uniform_batch(1 << 20, 1024, 1, seed=synth.SEED_BASE + 1),
            "c2": lambda: synth.mixed_batch(),
+           "c21": lambda: synth.mixed_batch(frames_per_seg=1),
+           "c4": lambda: synth.fragmented_batch(),
            "t64": lambda: synth.text_batch(16384, 65536, 4, seed=synth.SEED_BASE + 7),
            "t1": lambda: synth.text_batch(262144, 1024, 16, seed=synth.SEED_BASE + 8)}[which]()
     dev = torch.device("cuda:0")
@@ -31,7 +34,12 @@ def main():
     t = dict(wire=torch.from_numpy(cfg["wire"]).to(dev), seg_off=torch.from_numpy(cfg["seg_off"].view(np.int64)).to(dev),
              st=torch.zeros(n * K.STATE_BYTES, dtype=torch.uint8, device=dev), so=torch.zeros(n * 32, dtype=torch.uint8, device=dev),
              fr=torch.zeros((cfg["n_frames"] + 16) * 32, dtype=torch.uint8, device=dev), sm=torch.zeros(32, dtype=torch.uint8, device=dev))
-    b = c.make_batch(t["wire"], t["seg_off"], None, t["st"], t["so"], t["fr"], t["sm"])
+    compact = which == "c4"
+    if compact:
+        t["arena"] = torch.zeros(len(cfg["wire"]) + 64, dtype=torch.uint8, device=dev)
+        t["fd"] = torch.zeros(cfg["n_frames"] + 16, dtype=torch.int64, device=dev)
+    b = c.make_batch(t["wire"], t["seg_off"], None, t["st"], t["so"], t["fr"], t["sm"], compact=compact,
+                     arena=t.get("arena"), frame_dst=t.get("fd"))
     st = torch.cuda.Stream(device=dev)
     # TEXT batches are decoded from the pristine masked wire every time (an in-place decode leaves
     # the payload unmasked; decoding it again would validate garbage); the copy is its own kernel
