@@ -695,19 +695,29 @@ def echo_configs(with_cpu=True):
     (libwscodec wsc_session: recv straight into pinned staging, round r+1 submitted to the device
     while round r is echoed); gpu_sync = the same with one synchronous decode per round; cpu = oracle/_build/ws_echo_cpu,
     the reference's frame-at-a-time decode ported to C++ (cpu_baseline leg, kind "port").  Each
-    run is a separate process; msgs/s and GiB/s of echoed payload, every byte checked."""
+    run is a separate process; msgs/s and GiB/s of echoed payload, every byte checked.  P pollers
+    (netman runs NumCPU, eventloop/event.go:33-37): connection i on poller i % P, each poller its
+    own decoder -- for the GPU its own wsc_session on the one device."""
     import subprocess
-    runs = [("1 conn x 4000 x 64 KiB (configs[0])", ["--conns", "1", "--frames", "4000", "--size", "65536"]),
-            ("64 conns x 200 x 64 KiB", ["--conns", "64", "--frames", "200", "--size", "65536", "--client-threads", "4"]),
-            ("64 conns x 2000 x 1 KiB", ["--conns", "64", "--frames", "2000", "--size", "1024", "--client-threads", "4"])]
-    bins = [("gpu", os.path.join(ROOT, "tools", "ws_echo"), []),
-            ("gpu_sync", os.path.join(ROOT, "tools", "ws_echo"), ["--sync"])]
-    if with_cpu:
-        bins.append(("cpu_port", os.path.join(ROOT, "oracle", "_build", "ws_echo_cpu"), []))
+    gpu = os.path.join(ROOT, "tools", "ws_echo")
+    cpu = os.path.join(ROOT, "oracle", "_build", "ws_echo_cpu")
+    runs = [("1 conn x 4000 x 64 KiB (configs[0])", ["--conns", "1", "--frames", "4000", "--size", "65536"],
+             ["gpu", "gpu_sync", "cpu_port"])]
+    for P in (1, 4, 8):
+        runs.append((f"64 conns x 200 x 64 KiB, {P} poller(s)", ["--conns", "64", "--frames", "200", "--size", "65536",
+                                                                  "--client-threads", "4", "--pollers", str(P)],
+                     ["gpu", "cpu_port"]))
+        runs.append((f"64 conns x 2000 x 1 KiB, {P} poller(s)", ["--conns", "64", "--frames", "2000", "--size", "1024",
+                                                                 "--client-threads", "4", "--pollers", str(P)],
+                     ["gpu", "gpu_sync", "cpu_port"]))
+    bins = {"gpu": (gpu, []), "gpu_sync": (gpu, ["--sync"]), "cpu_port": (cpu, [])}
     res = {}
-    for name, args in runs:
+    for name, args, kinds in runs:
         row = {}
-        for kind, exe, extra in bins:
+        for kind in kinds:
+            if kind == "cpu_port" and not with_cpu:
+                continue
+            exe, extra = bins[kind]
             if not os.path.exists(exe):
                 row[kind] = None
                 continue

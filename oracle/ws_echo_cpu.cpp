@@ -78,12 +78,12 @@ struct CpuDecoder : echo::Decoder {
 }  // namespace
 
 int main(int argc, char** argv) {
-    int conns = 1, frames = 4000, threads = 1;
+    int conns = 1, frames = 4000, threads = 1, pollers = 1;
     size_t size = 65536;
-    echo::parse_args(argc, argv, conns, frames, size, threads);
-    CpuDecoder d;
-    const echo::Result r = echo::run(d, conns, frames, size, threads);
-    echo::print_json("cpu port: reference frame-at-a-time decode (websocket.go / websocket_frame.go)", r, conns,
-                     frames, size);
+    echo::parse_args(argc, argv, conns, frames, size, threads, pollers);
+    const echo::Result r = echo::run([](int) { return std::unique_ptr<echo::Decoder>(new CpuDecoder()); }, pollers,
+                                     conns, frames, size, threads);
+    echo::print_json("cpu port: reference frame-at-a-time decode (websocket.go / websocket_frame.go), one per poller",
+                     r, pollers, conns, frames, size);
     return r.ok ? 0 : 1;
 }

@@ -25,7 +25,9 @@ def cpu_echo():
 
 @pytest.mark.parametrize("args", [("--conns", "1", "--frames", "50", "--size", "65536"),
                                   ("--conns", "8", "--frames", "40", "--size", "70000", "--client-threads", "2"),
-                                  ("--conns", "16", "--frames", "300", "--size", "100", "--client-threads", "4")])
+                                  ("--conns", "16", "--frames", "300", "--size", "100", "--client-threads", "4"),
+                                  ("--conns", "16", "--frames", "100", "--size", "3000", "--client-threads", "4",
+                                   "--pollers", "4")])
 def test_cpu_echo_roundtrip(cpu_echo, args):
     rc, d = _run(cpu_echo, *args)
     assert rc == 0 and d["ok"], d
@@ -35,10 +37,17 @@ def test_cpu_echo_roundtrip(cpu_echo, args):
 @pytest.mark.gpu
 @pytest.mark.parametrize("args", [("--conns", "1", "--frames", "200", "--size", "65536"),
                                   ("--conns", "32", "--frames", "50", "--size", "70000", "--client-threads", "4"),
-                                  ("--conns", "16", "--frames", "500", "--size", "125", "--client-threads", "4")])
+                                  ("--conns", "16", "--frames", "500", "--size", "125", "--client-threads", "4"),
+                                  # 4 pollers x 16 connections, each poller its own
+                                  # wsc_session on the one device (eventloop/event.go:33-37)
+                                  ("--conns", "64", "--frames", "60", "--size", "65536", "--client-threads", "4",
+                                   "--pollers", "4"),
+                                  ("--conns", "64", "--frames", "400", "--size", "1024", "--client-threads", "4",
+                                   "--pollers", "4", "--sync")])
 def test_gpu_echo_roundtrip(codec_lib, args):
     from netman_amd import _build
     exe = _build.build_tools()
     rc, d = _run(exe, *args)
     assert rc == 0 and d["ok"], d
     assert d["messages"] == int(args[1]) * int(args[3])
+    assert d["pollers"] == (int(args[args.index("--pollers") + 1]) if "--pollers" in args else 1)

@@ -2,12 +2,16 @@
 // reference's examples/websocket echo server needs Go, which this image and the GPU box lack, so
 // the harness rebuilds the same traffic around a pluggable decoder).
 //
-// One server thread plays one netman poller (eventloop/epoll.go:36-143): level-triggered epoll,
-// ONE bulk read per ready connection per round fed to a Decoder, one decode pass per round, then
-// every delivered message echoed as an unmasked server frame -- the examples/websocket handler's
-// connect.Binary(message.Bytes()) (examples/websocket/server.go:30-44, encode at
-// server/websocket_ctrl.go:23-70; the handler's fmt.Println is left out).  Client threads send
-// `frames` masked 0x82 frames of `frame_bytes` per connection and check every echoed byte.
+// P server threads play netman's P pollers (eventloop/event.go:33-37, NumCPU by default in
+// examples/websocket/server.go:72): accepted connection i belongs to poller i % P
+// (eventloop/event.go:47-58), and each poller owns its own Decoder (for the product path its own
+// wsc_session: contexts, streams, pinned staging) and runs eventloop/epoll.go:36-143's loop --
+// level-triggered epoll, ONE bulk read per ready connection per round fed to its Decoder, one
+// decode pass per round, then every delivered message echoed as an unmasked server frame -- the
+// examples/websocket handler's connect.Binary(message.Bytes()) (examples/websocket/server.go:30-44,
+// encode at server/websocket_ctrl.go:23-70; the handler's fmt.Println is left out).  Client
+// threads send `frames` masked 0x82 frames of `frame_bytes` per connection and check every echoed
+// byte.
 //
 // The Decoder is what the two binaries differ in:
 //   tools/ws_echo.cpp       product path: libwscodec's wsc_session, one batched device decode per round
@@ -28,6 +32,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
+#include <memory>
+#include <mutex>
 #include <random>
 #include <string>
 #include <thread>
@@ -86,7 +93,10 @@ struct ServerConn {
     bool want_out = false;
 };
 
-inline Result run(Decoder& dec, int conns, int frames, size_t frame_bytes, int client_threads, int timeout_s = 60) {
+using DecoderFactory = std::function<std::unique_ptr<Decoder>(int conns_of_poller)>;
+
+inline Result run(const DecoderFactory& make_decoder, int pollers, int conns, int frames, size_t frame_bytes,
+                  int client_threads, int timeout_s = 60) {
     Result res;
     const int lfd = socket(AF_INET, SOCK_STREAM, 0);
     int one = 1;
@@ -212,10 +222,22 @@ inline Result run(Decoder& dec, int conns, int frames, size_t frame_bytes, int c
         });
     }
 
-    // server: accept every connection, then the poller loop
-    std::vector<ServerConn> sc;
-    const int ep = epoll_create1(0);
-    while ((int)sc.size() < conns && client_fail.load() == 0) {
+    // server: accept every connection (connection i -> poller i % P), then P poller threads
+    struct Poller {
+        std::unique_ptr<Decoder> dec;
+        int ep = -1;
+        std::vector<ServerConn> sc;
+        uint64_t served = 0, payload = 0, rounds = 0;
+        std::string error;
+    };
+    if (pollers < 1) pollers = 1;
+    if (pollers > conns) pollers = conns;
+    std::vector<Poller> pl(pollers);
+    for (int p = 0; p < pollers; ++p) {
+        pl[p].dec = make_decoder(conns / pollers + (p < conns % pollers ? 1 : 0));
+        pl[p].ep = epoll_create1(0);
+    }
+    for (int i = 0; i < conns && client_fail.load() == 0; ++i) {
         const int fd = accept(lfd, nullptr, nullptr);
         if (fd < 0) {
             res.error = "accept";
@@ -224,139 +246,159 @@ inline Result run(Decoder& dec, int conns, int frames, size_t frame_bytes, int c
         set_nonblock(fd);
         setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
         big_buffers(fd);
+        Poller& P = pl[i % pollers];
         ServerConn c;
         c.fd = fd;
-        c.id = dec.open();
+        c.id = P.dec->open();
         epoll_event e{};
         e.events = EPOLLIN;
-        e.data.u64 = sc.size();
-        epoll_ctl(ep, EPOLL_CTL_ADD, fd, &e);
-        sc.push_back(c);
+        e.data.u64 = P.sc.size();
+        epoll_ctl(P.ep, EPOLL_CTL_ADD, fd, &e);
+        P.sc.push_back(c);
     }
-    std::vector<uint8_t> rb(4 << 20);
-    std::vector<size_t> fed;
-    epoll_event evs[1024];
-    uint64_t served = 0;
-    const uint64_t want = (uint64_t)conns * (uint64_t)frames;
     while (ready.load() < client_threads && client_fail.load() == 0) std::this_thread::yield();
     const auto t0 = std::chrono::steady_clock::now();
     go = true;
     const auto deadline = t0 + std::chrono::seconds(timeout_s);
-    // pipelined decoders: round r+1's reads are submitted to the device before round r's messages
-    // are echoed, so the device decodes while this thread builds and sends the replies
-    const bool pipe = dec.pipelined();
-    std::vector<size_t> drain;   // connections whose messages are ready to echo (previous round)
-    auto echo_round = [&](const std::vector<size_t>& conns_ready) {
-        for (size_t q : conns_ready) {   // every delivered message is echoed
-            ServerConn& c = sc[q];
-            const uint8_t* d;
-            size_t len;
-            while (dec.next(c.id, &d, &len)) {
-                uint8_t h[10];
-                const size_t hl = put_header(h, 0x82, len);
-                c.out.insert(c.out.end(), h, h + hl);
-                c.out.insert(c.out.end(), d, d + len);
-                served++;
-                res.payload_bytes += len;
+
+    auto poller_loop = [&](Poller& P) {
+        Decoder& dec = *P.dec;
+        std::vector<ServerConn>& sc = P.sc;
+        std::vector<uint8_t> rb(4 << 20);
+        std::vector<size_t> fed;
+        epoll_event evs[1024];
+        const uint64_t want = (uint64_t)sc.size() * (uint64_t)frames;
+        // pipelined decoders: round r+1's reads are submitted to the device before round r's
+        // messages are echoed, so the device decodes while this thread builds and sends the replies
+        const bool pipe = dec.pipelined();
+        std::vector<size_t> drain;   // connections whose messages are ready to echo (previous round)
+        auto echo_round = [&](const std::vector<size_t>& conns_ready) {
+            for (size_t q : conns_ready) {   // every delivered message is echoed
+                ServerConn& c = sc[q];
+                const uint8_t* d;
+                size_t len;
+                while (dec.next(c.id, &d, &len)) {
+                    uint8_t h[10];
+                    const size_t hl = put_header(h, 0x82, len);
+                    c.out.insert(c.out.end(), h, h + hl);
+                    c.out.insert(c.out.end(), d, d + len);
+                    P.served++;
+                    P.payload += len;
+                }
             }
-        }
-    };
-    while (res.error.empty() && served < want && client_fail.load() == 0) {
-        if (std::chrono::steady_clock::now() > deadline) {
-            res.error = "server timeout";
-            break;
-        }
-        const int n = epoll_wait(ep, evs, 1024, pipe && !drain.empty() ? 0 : 100);
-        fed.clear();
-        for (int k = 0; k < n; ++k) {
-            ServerConn& c = sc[evs[k].data.u64];
-            if (evs[k].events & EPOLLIN) {
-                uint8_t* p = nullptr;
-                size_t avail = 0;
-                if (dec.reserve(c.id, rb.size(), &p, &avail)) {   // ONE bulk read per event, into pinned staging
-                    const ssize_t r = recv(c.fd, p, avail, 0);
-                    dec.commit(c.id, r > 0 ? (size_t)r : 0);
-                    if (r > 0) fed.push_back(evs[k].data.u64);
-                } else {
-                    const ssize_t r = recv(c.fd, rb.data(), rb.size(), 0);   // ONE bulk read per event
-                    if (r > 0) {
-                        dec.feed(c.id, rb.data(), (size_t)r);
-                        fed.push_back(evs[k].data.u64);
+        };
+        while (P.error.empty() && P.served < want && client_fail.load() == 0) {
+            if (std::chrono::steady_clock::now() > deadline) {
+                P.error = "server timeout";
+                break;
+            }
+            const int n = epoll_wait(P.ep, evs, 1024, pipe && !drain.empty() ? 0 : 100);
+            fed.clear();
+            for (int k = 0; k < n; ++k) {
+                ServerConn& c = sc[evs[k].data.u64];
+                if (evs[k].events & EPOLLIN) {
+                    uint8_t* p = nullptr;
+                    size_t avail = 0;
+                    if (dec.reserve(c.id, rb.size(), &p, &avail)) {   // ONE bulk read per event, into pinned staging
+                        const ssize_t r = recv(c.fd, p, avail, 0);
+                        dec.commit(c.id, r > 0 ? (size_t)r : 0);
+                        if (r > 0) fed.push_back(evs[k].data.u64);
+                    } else {
+                        const ssize_t r = recv(c.fd, rb.data(), rb.size(), 0);   // ONE bulk read per event
+                        if (r > 0) {
+                            dec.feed(c.id, rb.data(), (size_t)r);
+                            fed.push_back(evs[k].data.u64);
+                        }
                     }
                 }
             }
-        }
-        if (pipe) {
-            if (!fed.empty() || dec.pending()) {
-                dec.submit();          // round r+1 on the device ...
-                res.rounds++;
+            if (pipe) {
+                if (!fed.empty() || dec.pending()) {
+                    dec.submit();          // round r+1 on the device ...
+                    P.rounds++;
+                }
+                echo_round(drain);         // ... while round r is echoed
+                dec.complete();
+                drain = fed;
+            } else {
+                if (!fed.empty()) {
+                    dec.decode();
+                    P.rounds++;
+                }
+                echo_round(fed);
             }
-            echo_round(drain);         // ... while round r is echoed
-            dec.complete();
-            drain = fed;
-        } else {
-            if (!fed.empty()) {
-                dec.decode();
-                res.rounds++;
+            for (size_t i = 0; i < sc.size(); ++i) {
+                ServerConn& c = sc[i];
+                while (c.out_pos < c.out.size()) {   // until the socket buffer is full
+                    const ssize_t w = send(c.fd, c.out.data() + c.out_pos, c.out.size() - c.out_pos, MSG_NOSIGNAL);
+                    if (w <= 0) break;
+                    c.out_pos += (size_t)w;
+                }
+                if (c.out_pos == c.out.size()) {
+                    c.out.clear();
+                    c.out_pos = 0;
+                }
+                const bool need = c.out_pos < c.out.size();
+                if (need != c.want_out) {
+                    epoll_event e{};
+                    e.events = EPOLLIN | (need ? EPOLLOUT : 0u);
+                    e.data.u64 = i;
+                    epoll_ctl(P.ep, EPOLL_CTL_MOD, c.fd, &e);
+                    c.want_out = need;
+                }
             }
-            echo_round(fed);
         }
-        for (size_t i = 0; i < sc.size(); ++i) {
-            ServerConn& c = sc[i];
-            while (c.out_pos < c.out.size()) {   // until the socket buffer is full
+        // flush what is left (the clients check every echo)
+        for (auto& c : sc) {
+            while (c.out_pos < c.out.size() && client_fail.load() == 0 && P.error.empty()) {
                 const ssize_t w = send(c.fd, c.out.data() + c.out_pos, c.out.size() - c.out_pos, MSG_NOSIGNAL);
-                if (w <= 0) break;
-                c.out_pos += (size_t)w;
-            }
-            if (c.out_pos == c.out.size()) {
-                c.out.clear();
-                c.out_pos = 0;
-            }
-            const bool need = c.out_pos < c.out.size();
-            if (need != c.want_out) {
-                epoll_event e{};
-                e.events = EPOLLIN | (need ? EPOLLOUT : 0u);
-                e.data.u64 = i;
-                epoll_ctl(ep, EPOLL_CTL_MOD, c.fd, &e);
-                c.want_out = need;
+                if (w > 0) c.out_pos += (size_t)w;
+                else std::this_thread::yield();
             }
         }
-    }
-    // flush what is left, then wait for the clients to have checked every echo
-    for (auto& c : sc) {
-        while (c.out_pos < c.out.size() && client_fail.load() == 0 && res.error.empty()) {
-            const ssize_t w = send(c.fd, c.out.data() + c.out_pos, c.out.size() - c.out_pos, MSG_NOSIGNAL);
-            if (w > 0) c.out_pos += (size_t)w;
-            else std::this_thread::yield();
-        }
-    }
-    if (!res.error.empty()) client_fail++;   // release the client threads
+        if (!P.error.empty()) client_fail++;   // release the client threads
+    };
+    std::vector<std::thread> server;
+    if (res.error.empty())
+        for (int p = 0; p < pollers; ++p) server.emplace_back(poller_loop, std::ref(pl[p]));
+    else
+        client_fail++;
+    for (auto& t : server) t.join();
     for (auto& t : clients) t.join();
     const auto t1 = std::chrono::steady_clock::now();
     res.seconds = std::chrono::duration<double>(t1 - t0).count();
-    res.messages = served;
-    res.ok = res.error.empty() && client_fail.load() == 0 && client_msgs.load() == want;
+    for (auto& P : pl) {
+        res.messages += P.served;
+        res.payload_bytes += P.payload;
+        res.rounds += P.rounds;
+        if (res.error.empty() && !P.error.empty()) res.error = P.error;
+        for (auto& c : P.sc) close(c.fd);
+        close(P.ep);
+        P.dec.reset();
+    }
+    const uint64_t want_all = (uint64_t)conns * (uint64_t)frames;
+    res.ok = res.error.empty() && client_fail.load() == 0 && client_msgs.load() == want_all && res.messages == want_all;
     if (!res.ok && res.error.empty()) res.error = "client check failed";
-    for (auto& c : sc) close(c.fd);
-    close(ep);
     close(lfd);
     return res;
 }
 
-inline void print_json(const char* codec, const Result& r, int conns, int frames, size_t frame_bytes) {
-    printf("{\"codec\": \"%s\", \"ok\": %s, \"connections\": %d, \"frames_per_conn\": %d, \"frame_bytes\": %zu, "
+inline void print_json(const char* codec, const Result& r, int pollers, int conns, int frames, size_t frame_bytes) {
+    printf("{\"codec\": \"%s\", \"ok\": %s, \"pollers\": %d, \"connections\": %d, \"frames_per_conn\": %d, \"frame_bytes\": %zu, "
            "\"seconds\": %.4f, \"messages\": %llu, \"msgs_per_s\": %.1f, \"gib_s\": %.3f, \"rounds\": %llu, "
            "\"error\": \"%s\"}\n",
-           codec, r.ok ? "true" : "false", conns, frames, frame_bytes, r.seconds, (unsigned long long)r.messages,
+           codec, r.ok ? "true" : "false", pollers, conns, frames, frame_bytes, r.seconds, (unsigned long long)r.messages,
            r.seconds > 0 ? (double)r.messages / r.seconds : 0.0,
            r.seconds > 0 ? (double)r.payload_bytes / r.seconds / 1073741824.0 : 0.0, (unsigned long long)r.rounds,
            r.error.c_str());
 }
 
-inline void parse_args(int argc, char** argv, int& conns, int& frames, size_t& frame_bytes, int& threads) {
-    for (int i = 1; i + 1 < argc; i += 2) {
+inline void parse_args(int argc, char** argv, int& conns, int& frames, size_t& frame_bytes, int& threads,
+                       int& pollers) {
+    for (int i = 1; i + 1 < argc; ++i) {
         const std::string k = argv[i];
-        if (k == "--conns") conns = atoi(argv[i + 1]);
+        if (k == "--pollers") pollers = atoi(argv[i + 1]);
+        else if (k == "--conns") conns = atoi(argv[i + 1]);
         else if (k == "--frames") frames = atoi(argv[i + 1]);
         else if (k == "--size") frame_bytes = (size_t)atoll(argv[i + 1]);
         else if (k == "--client-threads") threads = atoi(argv[i + 1]);
@@ -364,6 +406,8 @@ inline void parse_args(int argc, char** argv, int& conns, int& frames, size_t& f
     if (conns < 1) conns = 1;
     if (threads > conns) threads = conns;
     if (threads < 1) threads = 1;
+    if (pollers > conns) pollers = conns;
+    if (pollers < 1) pollers = 1;
 }
 
 }  // namespace echo

@@ -2,7 +2,9 @@
 // (the DecodePacket mirror above the C ABI) decodes every round's bulk reads in ONE batched device
 // pass on the MI355X.  Harness: tools/echo_harness.hpp.  The CPU baseline twin is
 // oracle/ws_echo_cpu.cpp.  Prints one JSON line.
-//   ws_echo [--conns C] [--frames N] [--size BYTES] [--client-threads T] [--sync]
+//   ws_echo [--pollers P] [--conns C] [--frames N] [--size BYTES] [--client-threads T] [--sync]
+// --pollers P: P poller threads, each with its own wsc_session on the same device (netman runs
+// NumCPU pollers, eventloop/event.go:33-37); connection i belongs to poller i % P.
 #include "../include/wscodec.h"
 #include "echo_harness.hpp"
 
@@ -11,10 +13,11 @@ namespace {
 struct GpuDecoder : echo::Decoder {
     wsc_session* s = nullptr;
     wsc_event ev{};
-    explicit GpuDecoder(int conns) {
+    GpuDecoder(int conns, bool pipelined) : pipe(pipelined) {
         wsc_config cfg;
         wsc_config_default(&cfg);
-        cfg.max_batch_bytes = 320ull << 20;   // one device batch per poller round (64 conns x 4 MiB reads)
+        // one device batch per poller round: its connections' 4 MiB reads (+ a margin)
+        cfg.max_batch_bytes = (uint64_t)(conns < 4 ? 4 : conns) * (5ull << 20);
         cfg.max_segs = (uint32_t)conns + 16;
         cfg.max_frames = 1u << 18;
         if (wsc_session_create(0, &cfg, 0, &s) != WSC_OK) {
@@ -51,7 +54,7 @@ struct GpuDecoder : echo::Decoder {
             exit(3);
         }
     }
-    bool pipe = true;
+    bool pipe;
     bool next(int conn, const uint8_t** data, size_t* len) override {
         while (true) {
             wsc_session_next(s, (uint32_t)conn, &ev);
@@ -68,15 +71,17 @@ struct GpuDecoder : echo::Decoder {
 }  // namespace
 
 int main(int argc, char** argv) {
-    int conns = 1, frames = 4000, threads = 1;
+    int conns = 1, frames = 4000, threads = 1, pollers = 1;
     size_t size = 65536;
-    echo::parse_args(argc, argv, conns, frames, size, threads);
-    GpuDecoder d(conns);
+    echo::parse_args(argc, argv, conns, frames, size, threads, pollers);
+    bool pipe = true;
     for (int i = 1; i < argc; ++i)
-        if (std::string(argv[i]) == "--sync") d.pipe = false;   // one synchronous decode per round
-    const echo::Result r = echo::run(d, conns, frames, size, threads);
-    echo::print_json(d.pipe ? "gpu: libwscodec wsc_session, recv into pinned staging, submit r+1 / echo r / complete"
-                            : "gpu: libwscodec wsc_session, one synchronous device decode per poller round",
-                     r, conns, frames, size);
+        if (std::string(argv[i]) == "--sync") pipe = false;   // one synchronous decode per round
+    const echo::Result r = echo::run(
+        [pipe](int n) { return std::unique_ptr<echo::Decoder>(new GpuDecoder(n, pipe)); }, pollers, conns, frames,
+        size, threads);
+    echo::print_json(pipe ? "gpu: libwscodec wsc_session per poller, recv into pinned staging, submit r+1 / echo r / complete"
+                          : "gpu: libwscodec wsc_session per poller, one synchronous device decode per poller round",
+                     r, pollers, conns, frames, size);
     return r.ok ? 0 : 1;
 }
