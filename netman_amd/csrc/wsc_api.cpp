@@ -16,6 +16,7 @@
 
 namespace wsc {
 template <bool COMPACT, uint32_t KR, uint32_t NT, uint32_t G> __global__ void k_walk_fused(WalkArgs);
+template <bool COMPACT, uint32_t KR, uint32_t NT> __global__ void k_walk_tiled(WalkArgs, uint32_t);
 template <bool COMPACT> __global__ void k_walk_count(WalkArgs);
 __global__ void k_walk_scan(WalkArgs, uint32_t);
 template <bool COMPACT> __global__ void k_walk_emit(WalkArgs);
@@ -99,6 +100,7 @@ struct wsc_ctx {
     uint32_t u8par = 0;                 // parity of the decode the last walk belongs to
     uint32_t u8_inline_max = 256;
     uint32_t u8_grid = 0;               // WSC_U8_GRID: k_u8_check workgroups (A/B experiments; 0 = 5 per CU)
+    bool walk_tiled = true;             // WSC_WALK_TILED=0: the three-launch walk for mode 3 (A/B)
     bool ab_no_u8 = false;              // WSC_AB_NO_U8=1: A/B timing only -- binary unmask, no UTF-8 launches
                                         // (wrong for text batches; never set in tests or the bench)
     int walk_mode = 0;                  // WSC_WALK_MODE: 64, 256 or 3 pins the walk geometry (A/B, tests); 0 = auto
@@ -306,6 +308,7 @@ int wsc_create(int device, const wsc_config* cfg_in, wsc_ctx** out) {
     if (const char* e = std::getenv("WSC_U8_CHAINS"); e && *e) c->u8_chains = std::atoi(e);
     if (const char* e = std::getenv("WSC_U8_GRID"); e && *e) c->u8_grid = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("WSC_AB_NO_U8"); e && e[0] == '1') c->ab_no_u8 = true;
+    if (const char* e = std::getenv("WSC_WALK_TILED"); e && e[0] == '0') c->walk_tiled = false;
     if (const char* e = std::getenv("WSC_WALK_MODE"); e && *e) {   // pin a walk geometry (tests, A/B): 64, 256 or 3
         const int m = std::atoi(e);
         c->walk_mode = (m == 64 || m == 256 || m == 3) ? m : 0;
@@ -441,7 +444,7 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
         c->walk_used = mode;
         c->walk_blocks = wgrid.x;
     }
-    const uint32_t rearm = mode == 3 ? 1u : (phase == 2 ? c->walk_blocks : wgrid.x) + 1;
+    uint32_t rearm = 0;   // (after the launch below: the tiled walk sets walk_blocks)
     auto rec = [&](int i) {
         if (ev) (void)hipEventRecord(ev[i], st);
     };
@@ -455,7 +458,15 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     c->walk_waited = false;
     if (split) HIP_TRY(hipStreamWaitEvent(ws, c->ev_done, 0));
     // fused: 16 frame records per lane in LDS (segments with more frames re-walk their headers)
-    if (mode == 3) {
+    if (mode == 3 && c->walk_tiled) {
+        // tiled: a persistent grid (2 blocks per CU of the walk's stream), contiguous segment ranges
+        const uint32_t nb = std::max<uint32_t>(1u, std::min<uint32_t>(2u * stream_cus(c, ws), (n + 255) / 256));
+        const uint32_t per = ((n + nb - 1) / nb + 255) / 256 * 256;
+        const uint32_t used = (n + per - 1) / per;
+        c->walk_blocks = used;
+        if (compact) hipLaunchKernelGGL((k_walk_tiled<true, 4, 256>), dim3(used), dim3(256), 0, ws, wa, per);
+        else hipLaunchKernelGGL((k_walk_tiled<false, 4, 256>), dim3(used), dim3(256), 0, ws, wa, per);
+    } else if (mode == 3) {
         if (compact) hipLaunchKernelGGL((k_walk_count<true>), wgrid, wblk, 0, ws, wa);
         else hipLaunchKernelGGL((k_walk_count<false>), wgrid, wblk, 0, ws, wa);
         HIP_TRY(hipGetLastError());
@@ -474,6 +485,8 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     if (split) HIP_TRY(hipEventRecord(c->ev_walked, ws));
     }   // phase != 2
     if (phase == 1) return WSC_OK;
+    // look-back flags the walk used (the three-launch walk has none): ticket, timeout, flags
+    rearm = (mode == 3 && !c->walk_tiled) ? 1u : c->walk_blocks + 1;
     // a stream wait is a barrier packet between this unmask and the previous one on st: skipped
     // when the host already knows the walk has finished (the staged pipeline waits for it)
     const bool walked = split && (c->walk_waited || hipEventQuery(c->ev_walked) == hipSuccess);

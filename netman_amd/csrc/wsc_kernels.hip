@@ -229,7 +229,7 @@ __device__ __forceinline__ uint4 rec_pack(const wsc_frame& fr, uint64_t seg_star
 // speculative header is used only when its address is the real next position, so results never
 // depend on the guess; frames that repeat their size (the common case on one connection) cost
 // one round trip per SPEC_D frames.  All loads of a round are waited together.
-template <bool EMIT, bool COMPACT, uint32_t LS = 64, int SPEC_D = 4>
+template <bool EMIT, bool COMPACT, uint32_t LS = 64, int SPEC_D = 4, bool PURE = false>
 __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, const SegCount& base,
                                                  const SegCount& own, uint4* lrec, WalkEnd* wend,
                                                  uint4* lrec2 = nullptr, uint32_t cap = 0, uint32_t tag = 0) {
@@ -297,6 +297,11 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
     auto defer = [&](uint64_t src, uint64_t n, uint32_t mk, bool part, bool chain, uint32_t hl) {
         // large text (or a chain already deferred): validated chip-wide by k_u8_check,
         // which also applies the verdict; the walk goes on as if it were valid
+        if constexpr (PURE) {   // a count without side effects: only the chain state the walk keys on
+            if (part) u8_pending = true;
+            if (chain) u8_pending = false;
+            return;
+        }
         const uint8_t kind = part ? U8K_PART : (chain ? U8K_CHAIN : U8K_SELF);
         const uint8_t s_in = (part || chain) ? (u8_pending ? 0xFF : (uint8_t)u8dfa) : 0;
         // a payload up to U8_PIECE is one piece; longer ones are cut at absolute
@@ -746,7 +751,7 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
     if constexpr (!EMIT) {
         // the LDS records replay the segment only if all fit and every offset / length fits 32 bits
         replay = lrec && nf <= cap && seg_end - seg_start <= 0xFFFFFFFFull && !(sflags & SEGF_LONG);
-        if (!replay) {   // only a re-walking emit pass reads them back
+        if (!replay && !PURE) {   // only a re-walking emit pass reads them back
             a.u8info[2 * s] = u8fail;
             a.u8info[2 * s + 1] = u8dfa;
         }
@@ -943,77 +948,76 @@ __global__ __launch_bounds__(256) void k_walk_emit(WalkArgs a) {
     walk_segment<true, COMPACT, 256>(a, s, base, own, nullptr, nullptr);
 }
 
-// The fused walk kernel: NT lanes (64 or 256) per block, G consecutive segments per lane, KR frame
-// records per lane in LDS.  The host picks NT so that the blocks fill the CUs once (the count
-// phase wants every CU; the look-back wants few blocks).  Phases: count (each lane walks its segments; records in LDS) -> block scan -> decoupled
-// look-back -> cooperative emit of every frame held in LDS (flat order = memory order) -> per
-// segment results; segments whose frames did not fit re-walk their headers to emit.
+// LDS of one tile of the walk: NT lanes, G consecutive segments per lane, KR frame records per lane
 template <bool COMPACT, uint32_t KR, uint32_t NT, uint32_t G>
-__global__ __launch_bounds__(NT) void k_walk_fused(WalkArgs a) {
-    constexpr uint32_t NW = NT / 64;
-    __shared__ uint32_t sh_bid;
-    __shared__ SegCount sh_prefix;
-    __shared__ SegCount sh_wave[NW];
-    __shared__ uint32_t sh_wtot[NW];
-    __shared__ uint4 sh_rec[KR * NT];    // [record][lane]: conflict-free 16 B per lane
-    __shared__ uint4 sh_rec2[KR * NT];   // the frame's MsgID / span ordinal / arena offset / previous span end
-    __shared__ uint8_t sh_owner[KR * NT];   // flat replayed frame -> its lane
-    __shared__ uint32_t sh_rpre[NT];        // lane's first flat replayed frame
-    __shared__ uint32_t sh_nbig;            // long spans whose window index the wave writes
-    __shared__ uint4 sh_big[64];
+struct WalkLds {
+    SegCount prefix;
+    SegCount wave[NT / 64];
+    uint32_t wtot[NT / 64];
+    uint4 rec[KR * NT];      // [record][lane]: conflict-free 16 B per lane
+    uint4 rec2[KR * NT];     // the frame's MsgID / span ordinal / arena offset / previous span end
+    uint8_t owner[KR * NT];  // flat replayed frame -> its lane
+    uint32_t rpre[NT];       // lane's first flat replayed frame
+    uint32_t nbig;           // long spans whose window index the wave writes
+    uint4 big[64];
     // per segment, [segment of the lane][lane]: start, global frame / span (/ arena) bases, counts,
     // consumed bytes + terminal status, wire end of its last span, replayed from LDS or not
-    __shared__ uint64_t sh_sstart[G * NT], sh_ldend[G * NT];
-    __shared__ uint32_t sh_fbase[G * NT], sh_sbase[G * NT], sh_nf[G * NT], sh_ns[G * NT];
-    __shared__ uint32_t sh_cons[G * NT], sh_endst[G * NT];
-    __shared__ uint64_t sh_abase[COMPACT ? G * NT : 1], sh_ob0[COMPACT ? G * NT : 1];
-    __shared__ uint8_t sh_rep[G * NT], sh_r0[G * NT];   // (sh_r0: the segment's first record in the lane's list)
-    const uint32_t lane = threadIdx.x, wl = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (lane == 0) sh_bid = __hip_atomic_fetch_add(a.lb_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    const uint32_t bid = sh_bid;
-    const uint32_t n_blocks = (a.n_segs + NT * G - 1) / (NT * G);
-    const uint32_t s0 = (bid * NT + lane) * G;
-    const SegCount zero = {};
+    uint64_t sstart[G * NT], ldend[G * NT];
+    uint32_t fbase[G * NT], sbase[G * NT], nf[G * NT], ns[G * NT];
+    uint32_t cons[G * NT], endst[G * NT];
+    uint64_t abase[COMPACT ? G * NT : 1], ob0[COMPACT ? G * NT : 1];
+    uint8_t rep[G * NT], r0[G * NT];   // (r0: the segment's first record in the lane's list)
+};
 
-    uint64_t t0 = 0, t1 = 0, t2 = 0;
-    if (a.dbg && lane == 0) t0 = __builtin_amdgcn_s_memrealtime();
-    // ---- count ----
+// Count phase of a tile: each lane walks its G segments (first one s0; segments from seg_lim on
+// are not the tile's), keeping up to KR frame records in LDS; writes the connections' carried
+// state.  Returns the lane's total.
+template <bool COMPACT, uint32_t KR, uint32_t NT, uint32_t G>
+__device__ __forceinline__ SegCount tile_count(const WalkArgs& a, WalkLds<COMPACT, KR, NT, G>& L, uint32_t s0,
+                                               uint32_t seg_lim, uint32_t lane, uint32_t& nrec) {
+    const SegCount zero = {};
     SegCount tot = zero;
-    uint32_t nrec = 0;
+    nrec = 0;
     for (uint32_t j = 0; j < G; ++j) {
         const uint32_t s = s0 + j;
         const uint32_t q = j * NT + lane;
-        if (s >= a.n_segs) {
-            sh_nf[q] = sh_ns[q] = 0;
-            sh_rep[q] = 0;
-            sh_sstart[q] = ~0ull;
+        if (s >= seg_lim) {
+            L.nf[q] = L.ns[q] = 0;
+            L.rep[q] = 0;
+            L.sstart[q] = ~0ull;
             continue;
         }
         WalkEnd we;
         const uint32_t cap = KR - nrec;
-        const SegCount c = walk_segment<false, COMPACT, NT>(a, s, zero, zero, sh_rec + nrec * NT + lane, &we,
-                                                            sh_rec2 + nrec * NT + lane, cap, j);
+        const SegCount c = walk_segment<false, COMPACT, NT>(a, s, zero, zero, L.rec + nrec * NT + lane, &we,
+                                                            L.rec2 + nrec * NT + lane, cap, j);
         const uint64_t ss = a.seg_off[s];
         const bool rep = we.replay;
-        sh_r0[q] = (uint8_t)nrec;
+        L.r0[q] = (uint8_t)nrec;
         if (rep) nrec += c.frames;
-        sh_rep[q] = rep ? 1 : 0;
-        sh_sstart[q] = ss;
-        sh_ldend[q] = we.last_dend;
-        sh_nf[q] = c.frames;
-        sh_ns[q] = c.spans0 + c.spans1;
-        sh_cons[q] = (uint32_t)(we.pos - ss);
-        sh_endst[q] = we.status | we.err << 4 | we.close_code << 8;
-        sh_fbase[q] = c.flags;   // (the flags until the bases are known)
+        L.rep[q] = rep ? 1 : 0;
+        L.sstart[q] = ss;
+        L.ldend[q] = we.last_dend;
+        L.nf[q] = c.frames;
+        L.ns[q] = c.spans0 + c.spans1;
+        L.cons[q] = (uint32_t)(we.pos - ss);
+        L.endst[q] = we.status | we.err << 4 | we.close_code << 8;
+        L.fbase[q] = c.flags;   // (the flags until the bases are known)
         if constexpr (COMPACT) {
-            sh_abase[q] = c.bytes0 + c.bytes1;
-            sh_ob0[q] = c.bytes0;
+            L.abase[q] = c.bytes0 + c.bytes1;
+            L.ob0[q] = c.bytes0;
         }
         a.state_out[s] = end_state(we);   // the connection's carried state
         tot = sc_add(tot, c);
     }
-    // ---- block scan of the lanes' totals (64-lane shuffles, then across the waves) ----
+    return tot;
+}
+
+// Block-wide exclusive scan of the lanes' totals (64-lane shuffles, then across the waves); also
+// the block's total.  Ends with a __syncthreads.
+template <uint32_t NT, typename LDS>
+__device__ __forceinline__ SegCount tile_scan(const SegCount& tot, LDS& L, uint32_t wl, uint32_t wave, SegCount& btot) {
+    const SegCount zero = {};
     SegCount inc = tot;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -1022,93 +1026,108 @@ __global__ __launch_bounds__(NT) void k_walk_fused(WalkArgs a) {
     }
     SegCount excl = sc_shfl_up(inc, 1);
     if (wl == 0) excl = zero;
-    if (wl == 63) sh_wave[wave] = inc;
+    if (wl == 63) L.wave[wave] = inc;
     __syncthreads();
-    SegCount btot = zero;
+    btot = zero;
 #pragma unroll
-    for (uint32_t w = 0; w < NW; ++w) {
-        if (w < wave) excl = sc_add(excl, sh_wave[w]);
-        btot = sc_add(btot, sh_wave[w]);
+    for (uint32_t w = 0; w < NT / 64; ++w) {
+        if (w < wave) excl = sc_add(excl, L.wave[w]);
+        btot = sc_add(btot, L.wave[w]);
     }
-    // ---- decoupled look-back by the first wave: 64 predecessors are examined per round ----
-    if (wave == 0) {
-        if (a.dbg && wl == 0) t1 = __builtin_amdgcn_s_memrealtime();
-        uint32_t* flag = a.lb_flag;
-        uint64_t* agg = a.lb_agg;      // [block][4]
-        uint64_t* incl = a.lb_incl;    // [block][4]
-        if (wl == 0) {
-            lb_store(bid == 0 ? incl : agg + 4ull * bid, btot);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __hip_atomic_store(flag + bid, bid == 0 ? 2u : 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        SegCount prefix = zero;
-        int64_t j0 = (int64_t)bid - 1;
-        uint32_t spins = 0;
-        while (j0 >= 0) {
-            const int64_t j = j0 - (int64_t)wl;
-            const uint32_t f = j >= 0 ? __hip_atomic_fetch_add(flag + j, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                      : 2u;   // before block 0: an inclusive prefix of zero
-            const uint64_t m2 = __ballot(f == 2);
-            const uint64_t m0 = __ballot(f == 0);
-            const uint32_t first2 = m2 ? (uint32_t)__builtin_ctzll(m2) : 64u;
-            const uint64_t need = first2 >= 63 ? ~0ull : ((2ull << first2) - 1);   // wls 0..first2
-            if (m0 & need) {   // a predecessor in range has not published yet: poll again
-                if (++spins > (1u << 22)) {   // bounded: never hang the device
-                    if (wl == 0) __hip_atomic_fetch_or(a.lb_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
-                continue;
+    return excl;
+}
+
+// Decoupled look-back by one wave (64 predecessors examined per round): publishes block bid's
+// total, returns the sum of every earlier block's total.  Look-back hand-off (MI355X_MICROARCH.md
+// "Valid forms", row 1): one lane stores the aggregate / inclusive prefix with agent-scope (sc1,
+// write-through) stores, drains them with s_waitcnt vmcnt(0), then publishes the flag with an
+// agent-scope atomic; readers poll the flag and read the payload with agent-scope atomic RMWs.
+__device__ __forceinline__ SegCount block_lookback(const WalkArgs& a, uint32_t bid, const SegCount& btot, uint32_t wl) {
+    const SegCount zero = {};
+    uint32_t* flag = a.lb_flag;
+    uint64_t* agg = a.lb_agg;      // [block][4]
+    uint64_t* incl = a.lb_incl;    // [block][4]
+    if (wl == 0) {
+        lb_store(bid == 0 ? incl : agg + 4ull * bid, btot);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(flag + bid, bid == 0 ? 2u : 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    SegCount prefix = zero;
+    int64_t j0 = (int64_t)bid - 1;
+    uint32_t spins = 0;
+    while (j0 >= 0) {
+        const int64_t j = j0 - (int64_t)wl;
+        const uint32_t f = j >= 0 ? __hip_atomic_fetch_add(flag + j, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                  : 2u;   // before block 0: an inclusive prefix of zero
+        const uint64_t m2 = __ballot(f == 2);
+        const uint64_t m0 = __ballot(f == 0);
+        const uint32_t first2 = m2 ? (uint32_t)__builtin_ctzll(m2) : 64u;
+        const uint64_t need = first2 >= 63 ? ~0ull : ((2ull << first2) - 1);   // wls 0..first2
+        if (m0 & need) {   // a predecessor in range has not published yet: poll again
+            if (++spins > (1u << 22)) {   // bounded: never hang the device
+                if (wl == 0) __hip_atomic_fetch_or(a.lb_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
             }
-            SegCount v = zero;
-            if (wl <= first2 && j >= 0) v = lb_load((wl == first2 ? incl : agg) + 4ull * j);
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        SegCount v = zero;
+        if (wl <= first2 && j >= 0) v = lb_load((wl == first2 ? incl : agg) + 4ull * j);
 #pragma unroll
-            for (int d = 32; d >= 1; d >>= 1) {
-                SegCount o;
-                o.frames = __shfl_xor(v.frames, d);
-                o.spans0 = __shfl_xor(v.spans0, d);
-                o.spans1 = __shfl_xor(v.spans1, d);
-                o.flags = __shfl_xor(v.flags, d);
-                o.bytes0 = __shfl_xor(v.bytes0, d);
-                o.bytes1 = __shfl_xor(v.bytes1, d);
-                v = sc_add(v, o);
-            }
-            prefix = sc_add(prefix, v);
-            if (first2 < 64) break;
-            j0 -= 64;
+        for (int d = 32; d >= 1; d >>= 1) {
+            SegCount o;
+            o.frames = __shfl_xor(v.frames, d);
+            o.spans0 = __shfl_xor(v.spans0, d);
+            o.spans1 = __shfl_xor(v.spans1, d);
+            o.flags = __shfl_xor(v.flags, d);
+            o.bytes0 = __shfl_xor(v.bytes0, d);
+            o.bytes1 = __shfl_xor(v.bytes1, d);
+            v = sc_add(v, o);
         }
-        if (wl == 0) {
-            if (bid != 0) {
-                lb_store(incl + 4ull * bid, sc_add(prefix, btot));
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __hip_atomic_store(flag + bid, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            sh_prefix = prefix;
-        }
+        prefix = sc_add(prefix, v);
+        if (first2 < 64) break;
+        j0 -= 64;
     }
-    __syncthreads();
-    if (a.dbg && lane == 0) t2 = __builtin_amdgcn_s_memrealtime();
+    if (wl == 0 && bid != 0) {
+        lb_store(incl + 4ull * bid, sc_add(prefix, btot));
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(flag + bid, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return prefix;
+}
+
+// Emit phase of a tile, once the lane's first output position `lb` is known (the tile's prefix +
+// the lane's exclusive scan): per segment bases, then every frame held in LDS emitted
+// cooperatively in flat order (consecutive records, spans and arena offsets in memory, so each
+// store instruction covers contiguous bytes), then the per segment results; segments whose frames
+// did not fit re-walk their (cache-warm) headers to emit.  lane o's first segment is seg0 + o * G.
+template <bool COMPACT, uint32_t KR, uint32_t NT, uint32_t G>
+__device__ __forceinline__ void tile_emit(const WalkArgs& a, WalkLds<COMPACT, KR, NT, G>& L, const SegCount& lb,
+                                          uint32_t nrec, uint32_t seg0, uint32_t seg_lim, uint32_t lane) {
+    constexpr uint32_t NW = NT / 64;
+    const uint32_t wl = lane & 63, wave = lane >> 6;
+    const uint32_t s0 = seg0 + lane * G;
+    const SegCount zero = {};
     // ---- per segment bases ----
     {
-        const SegCount lb = sc_add(sh_prefix, excl);   // the lane's first frame / span / arena byte
         uint32_t fb = lb.frames, sb = lb.spans0 + lb.spans1;
         uint64_t ab = lb.bytes0 + lb.bytes1;
         for (uint32_t j = 0; j < G; ++j) {
             const uint32_t q = j * NT + lane;
             const uint32_t s = s0 + j;
-            const uint32_t fl = sh_fbase[q];
-            if (s < a.n_segs && (fl & SEGF_U8DEFER)) {
+            const uint32_t fl = L.fbase[q];
+            if (s < seg_lim && (fl & SEGF_U8DEFER)) {
                 a.u8seg[s].sbase = sb;
-                a.u8seg[s].nspans = sh_ns[q];
+                a.u8seg[s].nspans = L.ns[q];
                 a.u8seg[s].fbase = fb;
             }
-            sh_fbase[q] = fb;
-            sh_sbase[q] = sb;
-            fb += sh_nf[q];
-            sb += sh_ns[q];
+            L.fbase[q] = fb;
+            L.sbase[q] = sb;
+            fb += L.nf[q];
+            sb += L.ns[q];
             if constexpr (COMPACT) {
-                const uint64_t n = sh_abase[q];
-                sh_abase[q] = ab;
+                const uint64_t n = L.abase[q];
+                L.abase[q] = ab;
                 ab += n;
             }
         }
@@ -1120,39 +1139,38 @@ __global__ __launch_bounds__(NT) void k_walk_fused(WalkArgs a) {
         const uint32_t o = __shfl_up(rv, d);
         if (wl >= (uint32_t)d) rv += o;
     }
-    if (wl == 63) sh_wtot[wave] = rv;
-    if (lane == 0) sh_nbig = 0;
+    if (wl == 63) L.wtot[wave] = rv;
+    if (lane == 0) L.nbig = 0;
     __syncthreads();
     uint32_t rpre = rv - nrec, F = 0;
 #pragma unroll
     for (uint32_t w = 0; w < NW; ++w) {
-        if (w < wave) rpre += sh_wtot[w];
-        F += sh_wtot[w];
+        if (w < wave) rpre += L.wtot[w];
+        F += L.wtot[w];
     }
-    sh_rpre[lane] = rpre;
-    for (uint32_t k = 0; k < nrec; ++k) sh_owner[rpre + k] = (uint8_t)lane;
+    L.rpre[lane] = rpre;
+    for (uint32_t k = 0; k < nrec; ++k) L.owner[rpre + k] = (uint8_t)lane;
     __syncthreads();
-    // ---- cooperative emit: the block's replayed frames in flat order are consecutive records,
-    //      spans and arena offsets in memory, so each store instruction covers contiguous bytes ----
+    // ---- cooperative emit ----
     const uint32_t W = 1u << a.win_shift;
     for (uint32_t f = lane; f < F; f += NT) {
-        const uint32_t o = sh_owner[f];
-        const uint32_t k = f - sh_rpre[o];
-        const uint4 r = sh_rec[k * NT + o];
-        const uint4 q = sh_rec2[k * NT + o];
+        const uint32_t o = L.owner[f];
+        const uint32_t k = f - L.rpre[o];
+        const uint4 r = L.rec[k * NT + o];
+        const uint4 q = L.rec2[k * NT + o];
         const uint32_t j = r.w >> 28;
         const uint32_t qi = j * NT + o;
-        const uint64_t ss = sh_sstart[qi];
+        const uint64_t ss = L.sstart[qi];
         const uint32_t hl = (r.w >> 14) & 15, fl = (r.w >> 18) & 0xFF, region = (r.w >> 26) & 1;
         const bool have_span = (r.w >> 27) & 1;
         const uint64_t hdr_off = ss + r.x;
         uint64_t dst = ~0ull;
         if constexpr (COMPACT)
-            if (fl & WSC_FF_UNMASKED) dst = sh_abase[qi] + (region ? sh_ob0[qi] : 0ull) + q.z;
-        const uint32_t fidx = sh_fbase[qi] + (k - sh_r0[qi]);   // the segment's first frame + ordinal
+            if (fl & WSC_FF_UNMASKED) dst = L.abase[qi] + (region ? L.ob0[qi] : 0ull) + q.z;
+        const uint32_t fidx = L.fbase[qi] + (k - L.r0[qi]);   // the segment's first frame + ordinal
         if (fidx < a.frames_cap) {
             const uint4 r0 = make_uint4((uint32_t)hdr_off, (uint32_t)(hdr_off >> 32), r.y, r.z);
-            const uint4 r1 = make_uint4((bid * NT + o) * G + j, q.x,
+            const uint4 r1 = make_uint4(seg0 + o * G + j, q.x,
                                         (r.w & 0xF) | ((r.w >> 4) & 1) << 8 | ((r.w >> 5) & 15) << 16 |
                                             ((r.w >> 9) & 3) << 24,
                                         ((r.w >> 11) & 7) | hl << 8 | fl << 16);
@@ -1161,7 +1179,7 @@ __global__ __launch_bounds__(NT) void k_walk_fused(WalkArgs a) {
             if constexpr (COMPACT) a.frame_dst[fidx] = dst;
         }
         if (have_span) {
-            const uint32_t idx = sh_sbase[qi] + q.y;
+            const uint32_t idx = L.sbase[qi] + q.y;
             Span sp;
             sp.src = hdr_off + hl;
             sp.len = r.y;
@@ -1172,9 +1190,9 @@ __global__ __launch_bounds__(NT) void k_walk_fused(WalkArgs a) {
             uint64_t t = (ss + q.w + W - 1) >> a.win_shift;
             const uint64_t t_end = ((sp.src + r.y - 1) >> a.win_shift) + 1;
             if (t_end > t + 64) {   // a long span: its windows are written by the whole wave below
-                const uint32_t jb = atomicAdd(&sh_nbig, 1u);
+                const uint32_t jb = atomicAdd(&L.nbig, 1u);
                 if (jb < 64) {
-                    sh_big[jb] = make_uint4((uint32_t)t, (uint32_t)(t >> 32), (uint32_t)(t_end - t), idx);
+                    L.big[jb] = make_uint4((uint32_t)t, (uint32_t)(t >> 32), (uint32_t)(t_end - t), idx);
                     t = t_end;
                 }
             }
@@ -1186,44 +1204,93 @@ __global__ __launch_bounds__(NT) void k_walk_fused(WalkArgs a) {
     }
     __syncthreads();
     {
-        const uint32_t nbig = sh_nbig < 64 ? sh_nbig : 64;
+        const uint32_t nbig = L.nbig < 64 ? L.nbig : 64;
         for (uint32_t jb = wave; jb < nbig; jb += NW) {   // one wave per long span
-            const uint64_t tb = sh_big[jb].x | (uint64_t)sh_big[jb].y << 32;
-            const uint32_t nw = sh_big[jb].z, idx = sh_big[jb].w;
+            const uint64_t tb = L.big[jb].x | (uint64_t)L.big[jb].y << 32;
+            const uint32_t nw = L.big[jb].z, idx = L.big[jb].w;
             for (uint32_t i = wl; i < nw; i += 64) a.tile_first[tb + i] = idx;
         }
     }
     // ---- per segment results; segments not held in LDS re-walk their (cache-warm) headers ----
     for (uint32_t j = 0; j < G; ++j) {
         const uint32_t s = s0 + j;
-        if (s >= a.n_segs) break;
+        if (s >= seg_lim) break;
         const uint32_t q = j * NT + lane;
         const uint64_t se = a.seg_off[s + 1];
-        if (sh_rep[q]) {
+        if (L.rep[q]) {
             const uint64_t Wd = W;   // windows that start after the last span, up to the segment end
-            const uint32_t nx = sh_sbase[q] + sh_ns[q];
-            for (uint64_t x = (sh_ldend[q] + Wd - 1) & ~(Wd - 1); x < se; x += Wd) a.tile_first[x >> a.win_shift] = nx;
+            const uint32_t nx = L.sbase[q] + L.ns[q];
+            for (uint64_t x = (L.ldend[q] + Wd - 1) & ~(Wd - 1); x < se; x += Wd) a.tile_first[x >> a.win_shift] = nx;
             wsc_seg_result r;
-            r.consumed = sh_cons[q];
-            r.frame_begin = sh_fbase[q];
-            r.frame_count = sh_nf[q];
-            r.status = sh_endst[q] & 0xF;
-            r.close_code = sh_endst[q] >> 8;
-            r.err = (sh_endst[q] >> 4) & 0xF;
+            r.consumed = L.cons[q];
+            r.frame_begin = L.fbase[q];
+            r.frame_count = L.nf[q];
+            r.status = L.endst[q] & 0xF;
+            r.close_code = L.endst[q] >> 8;
+            r.err = (L.endst[q] >> 4) & 0xF;
             r.pad = 0;
             a.seg_out[s] = r;
         } else {
             SegCount base = zero, own = zero;
-            base.frames = sh_fbase[q];
-            base.spans0 = sh_sbase[q];
-            own.frames = sh_nf[q];
+            base.frames = L.fbase[q];
+            base.spans0 = L.sbase[q];
+            own.frames = L.nf[q];
             if constexpr (COMPACT) {
-                base.bytes0 = sh_abase[q];
-                own.bytes0 = sh_ob0[q];
+                base.bytes0 = L.abase[q];
+                own.bytes0 = L.ob0[q];
             }
             walk_segment<true, COMPACT, NT>(a, s, base, own, nullptr, nullptr);
         }
     }
+}
+
+// The batch summary, by the block holding the last segments: totals `tt` of the whole batch.
+template <bool COMPACT>
+__device__ __forceinline__ void write_summary(const WalkArgs& a, const SegCount& tt) {
+    wsc_summary sm;
+    sm.data_bytes = COMPACT ? tt.bytes0 : 0;
+    sm.ctrl_bytes = COMPACT ? tt.bytes1 : 0;
+    sm.n_frames = tt.frames;
+    // spans past the capacity were never written: the unmask must not read them (an overflowed
+    // batch unmasks the spans that fit; n_spans = spans unmasked)
+    sm.n_spans = tt.spans0 + tt.spans1 < a.spans_cap ? tt.spans0 + tt.spans1 : a.spans_cap;
+    sm.overflow = (tt.frames > a.frames_cap || tt.spans0 + tt.spans1 > a.spans_cap) ? 1u : 0u;
+    if (__hip_atomic_load(a.lb_err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) sm.overflow |= 2u;
+    sm.pad = 0;
+    *a.summary = sm;
+    if (sm.overflow) __hip_atomic_fetch_or(a.sticky, sm.overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The fused walk kernel: NT lanes (64 or 256) per block, G consecutive segments per lane, KR frame
+// records per lane in LDS.  The host picks NT so that the blocks fill the CUs once (the count
+// phase wants every CU; the look-back wants few blocks).  Phases: count (each lane walks its
+// segments; records in LDS) -> block scan -> decoupled look-back -> cooperative emit.  Block ids
+// come from a ticket counter in dispatch order, so every block a block waits for has already
+// started.  Flags and the ticket are zeroed by k_unmask (the next launch on the stream) of every
+// decode, and at context creation.
+template <bool COMPACT, uint32_t KR, uint32_t NT, uint32_t G>
+__global__ __launch_bounds__(NT) void k_walk_fused(WalkArgs a) {
+    __shared__ uint32_t sh_bid;
+    __shared__ WalkLds<COMPACT, KR, NT, G> L;
+    const uint32_t lane = threadIdx.x, wl = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) sh_bid = __hip_atomic_fetch_add(a.lb_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const uint32_t bid = sh_bid;
+    const uint32_t n_blocks = (a.n_segs + NT * G - 1) / (NT * G);
+    uint64_t t0 = 0, t1 = 0, t2 = 0;
+    if (a.dbg && lane == 0) t0 = __builtin_amdgcn_s_memrealtime();
+    uint32_t nrec;
+    const SegCount tot = tile_count<COMPACT, KR, NT, G>(a, L, (bid * NT + lane) * G, a.n_segs, lane, nrec);
+    SegCount btot;
+    const SegCount excl = tile_scan<NT>(tot, L, wl, wave, btot);
+    if (wave == 0) {
+        if (a.dbg && wl == 0) t1 = __builtin_amdgcn_s_memrealtime();
+        const SegCount prefix = block_lookback(a, bid, btot, wl);
+        if (wl == 0) L.prefix = prefix;
+    }
+    __syncthreads();
+    if (a.dbg && lane == 0) t2 = __builtin_amdgcn_s_memrealtime();
+    tile_emit<COMPACT, KR, NT, G>(a, L, sc_add(L.prefix, excl), nrec, bid * NT * G, a.n_segs, lane);
     if (a.dbg) {   // diagnostic timestamps (100 MHz s_memrealtime), written only to the dbg buffer
         __syncthreads();
         if (lane == 0) {
@@ -1233,21 +1300,55 @@ __global__ __launch_bounds__(NT) void k_walk_fused(WalkArgs a) {
             a.dbg[4 * bid + 3] = __builtin_amdgcn_s_memrealtime();
         }
     }
-    if (bid == n_blocks - 1 && lane == 0) {
-        const SegCount tt = sc_add(sh_prefix, btot);
-        wsc_summary sm;
-        sm.data_bytes = COMPACT ? tt.bytes0 : 0;
-        sm.ctrl_bytes = COMPACT ? tt.bytes1 : 0;
-        sm.n_frames = tt.frames;
-        // spans past the capacity were never written: the unmask must not read them (an overflowed
-        // batch unmasks the spans that fit; n_spans = spans unmasked)
-        sm.n_spans = tt.spans0 + tt.spans1 < a.spans_cap ? tt.spans0 + tt.spans1 : a.spans_cap;
-        sm.overflow = (tt.frames > a.frames_cap || tt.spans0 + tt.spans1 > a.spans_cap) ? 1u : 0u;
-        if (__hip_atomic_load(a.lb_err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) sm.overflow |= 2u;
-        sm.pad = 0;
-        *a.summary = sm;
-        if (sm.overflow) __hip_atomic_fetch_or(a.sticky, sm.overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (bid == n_blocks - 1 && lane == 0) write_summary<COMPACT>(a, sc_add(L.prefix, btot));
+}
+
+// Tiled walk for batches of many (short) segments (more than 256 per CU: one connection read per
+// segment, e.g. configs[1] with one frame per segment).  A persistent grid whose blocks are all
+// resident; block b (by ticket) owns the contiguous segments [b * per, (b + 1) * per) and walks
+// them in tiles of NT lanes, one segment per lane:
+//   phase 1  count every tile with a PURE walk (no side effects: no records, items or state) into
+//            the block's total;
+//   look-back  the block's prefix (every block is running, so no block waits on one not started);
+//   phase 2  per tile: the count walk again with LDS records (headers now cache-warm), tile scan
+//            on top of the running prefix, cooperative emit from LDS.
+// One launch and no per-segment counts in HBM (the three-launch walk wrote and re-read 32 B of
+// counts per segment and re-walked every header in its emit pass).
+template <bool COMPACT, uint32_t KR, uint32_t NT>
+__global__ __launch_bounds__(NT) void k_walk_tiled(WalkArgs a, uint32_t per_block) {
+    __shared__ uint32_t sh_bid;
+    __shared__ WalkLds<COMPACT, KR, NT, 1> L;
+    const uint32_t lane = threadIdx.x, wl = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) sh_bid = __hip_atomic_fetch_add(a.lb_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const uint32_t bid = sh_bid;
+    const uint32_t sb = bid * per_block < a.n_segs ? bid * per_block : a.n_segs;
+    const uint32_t se = a.n_segs - sb < per_block ? a.n_segs : sb + per_block;
+    const SegCount zero = {};
+    // ---- phase 1: the block's total ----
+    SegCount tot = zero;
+    for (uint32_t t = sb; t < se; t += NT)
+        if (t + lane < se) tot = sc_add(tot, walk_segment<false, COMPACT, NT, 4, true>(a, t + lane, zero, zero, nullptr, nullptr));
+    SegCount btot;
+    (void)tile_scan<NT>(tot, L, wl, wave, btot);
+    if (wave == 0) {
+        const SegCount prefix = block_lookback(a, bid, btot, wl);
+        if (wl == 0) L.prefix = prefix;
     }
+    __syncthreads();
+    const SegCount block_prefix = L.prefix;
+    // ---- phase 2: tiles in order, each on top of the running prefix ----
+    SegCount run = block_prefix;
+    for (uint32_t t = sb; t < se; t += NT) {
+        uint32_t nrec;   // (lanes past the block's last segment count nothing)
+        const SegCount c = tile_count<COMPACT, KR, NT, 1>(a, L, t + lane, se, lane, nrec);
+        SegCount ttot;
+        const SegCount excl = tile_scan<NT>(c, L, wl, wave, ttot);
+        tile_emit<COMPACT, KR, NT, 1>(a, L, sc_add(run, excl), nrec, t, se, lane);
+        run = sc_add(run, ttot);
+        __syncthreads();   // (the tile's LDS is reused by the next tile)
+    }
+    if (se == a.n_segs && sb < se && lane == 0) write_summary<COMPACT>(a, sc_add(block_prefix, btot));
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1588,6 +1689,8 @@ template __global__ void k_walk_fused<false, 16, 64, 1>(WalkArgs);
 template __global__ void k_walk_fused<true, 16, 64, 1>(WalkArgs);
 template __global__ void k_walk_fused<false, 16, 256, 1>(WalkArgs);
 template __global__ void k_walk_fused<true, 16, 256, 1>(WalkArgs);
+template __global__ void k_walk_tiled<false, 4, 256>(WalkArgs, uint32_t);
+template __global__ void k_walk_tiled<true, 4, 256>(WalkArgs, uint32_t);
 template __global__ void k_walk_count<false>(WalkArgs);
 template __global__ void k_walk_count<true>(WalkArgs);
 template __global__ void k_walk_emit<false>(WalkArgs);

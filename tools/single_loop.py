@@ -1,7 +1,7 @@
 """Back-to-back decodes of one device batch on one stream (one batch in flight), for kernel-trace
 gap analysis:  python tools/single_loop.py <config> [iters]
 config: head (16384 x 64 KiB, 4/seg) | c1 (1M x 1 KiB, 16/seg) | c2 (256k mixed, 16/seg) |
-c4 (64k fragmented messages, COMPACT) |
+c4 (64k fragmented messages, COMPACT) | c4i (the same batch unmasked in place) |
 t64 / t1 (TEXT 16384 x 64 KiB / 262144 x 1 KiB; wire restored before each decode, wall time includes the copy)"""
 import os
 import sys
@@ -25,6 +25,7 @@ def main():
            "c2": lambda: synth.mixed_batch(),
            "c21": lambda: synth.mixed_batch(frames_per_seg=1),
            "c4": lambda: synth.fragmented_batch(),
+           "c4i": lambda: synth.fragmented_batch(),
            "t64": lambda: synth.text_batch(16384, 65536, 4, seed=synth.SEED_BASE + 7),
            "t1": lambda: synth.text_batch(262144, 1024, 16, seed=synth.SEED_BASE + 8)}[which]()
     dev = torch.device("cuda:0")
