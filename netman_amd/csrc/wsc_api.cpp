@@ -15,7 +15,7 @@
 #include "wsc_kernels.hpp"
 
 namespace wsc {
-template <bool COMPACT, uint32_t KR, uint32_t NT, uint32_t G> __global__ void k_walk_fused(WalkArgs);
+template <bool COMPACT, uint32_t KR, uint32_t NT, uint32_t G, uint32_t WL> __global__ void k_walk_fused(WalkArgs);
 template <bool COMPACT, uint32_t KR, uint32_t NT> __global__ void k_walk_tiled(WalkArgs, uint32_t);
 template <bool COMPACT> __global__ void k_walk_count(WalkArgs);
 __global__ void k_walk_scan(WalkArgs, uint32_t);
@@ -103,9 +103,10 @@ struct wsc_ctx {
     bool walk_tiled = true;             // WSC_WALK_TILED=0: the three-launch walk for mode 3 (A/B)
     bool ab_no_u8 = false;              // WSC_AB_NO_U8=1: A/B timing only -- binary unmask, no UTF-8 launches
                                         // (wrong for text batches; never set in tests or the bench)
-    int walk_mode = 0;                  // WSC_WALK_MODE: 64, 256 or 3 pins the walk geometry (A/B, tests); 0 = auto
+    int walk_mode = 0;                  // WSC_WALK_MODE: 64, 65, 256 or 3 pins the walk geometry (A/B, tests); 0 = auto
     uint32_t walk_used = 0;             // geometry (64 / 256 / 3) and block count of the last walk launched:
     uint32_t walk_blocks = 0;           // the staged unmask re-arms exactly that walk's look-back flags
+    uint32_t max_walk_blocks = 0;       // look-back state allocated for this many walk blocks
     SegCount* counts = nullptr;         // three-launch walk: per-segment counts
     uint64_t tile_entries = 0;
     // host-staged path buffers (lazily allocated)
@@ -159,7 +160,8 @@ static uint32_t walk_mode(const wsc_ctx* c, uint32_t n_segs, uint32_t cus) {
     // resident still beat the three-launch walk there (configs[1] on 32 CUs: 0.435 vs 0.497 ms)
     if (cus < (uint32_t)c->n_cu && n_segs <= 256u * cus) return 64;
     const uint32_t all = (uint32_t)c->n_cu;
-    if (n_segs <= 64u * all) return 64;
+    // up to one wave of segments per CU: one walking wave per CU, four emitting (mode 65)
+    if (n_segs <= 64u * all) return 65;
     if (n_segs <= 256u * all) return 256;
     return 3;
 }
@@ -275,7 +277,10 @@ int wsc_create(int device, const wsc_config* cfg_in, wsc_ctx** out) {
     chk(hipMalloc(&c->sticky, sizeof(uint32_t)), "hipMalloc sticky");
     chk(hipMalloc(&c->counts, (uint64_t)cfg.max_segs * sizeof(SegCount)), "hipMalloc counts");
     if (rc == WSC_OK) chk(hipMemsetAsync(c->sticky, 0, sizeof(uint32_t), c->stream), "hipMemset sticky");
-    const uint64_t max_blocks = (cfg.max_segs + 63) / 64 + 1;   // the most walk blocks (64-lane blocks)
+    // the most walk blocks (64 segments per block); the look-back flags, aggregates and prefixes
+    // are indexed by block
+    const uint64_t max_blocks = (cfg.max_segs + 63) / 64 + 1;
+    c->max_walk_blocks = (uint32_t)max_blocks;
     chk(hipMalloc(&c->lb_state, (max_blocks + 3) * sizeof(uint32_t)), "hipMalloc lb_state");
     chk(hipMalloc(&c->u8info, (uint64_t)cfg.max_segs * 2 * sizeof(uint32_t)), "hipMalloc u8info");
     chk(hipMalloc(&c->lb_agg, max_blocks * 4 * sizeof(uint64_t)), "hipMalloc lb_agg");
@@ -309,9 +314,9 @@ int wsc_create(int device, const wsc_config* cfg_in, wsc_ctx** out) {
     if (const char* e = std::getenv("WSC_U8_GRID"); e && *e) c->u8_grid = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("WSC_AB_NO_U8"); e && e[0] == '1') c->ab_no_u8 = true;
     if (const char* e = std::getenv("WSC_WALK_TILED"); e && e[0] == '0') c->walk_tiled = false;
-    if (const char* e = std::getenv("WSC_WALK_MODE"); e && *e) {   // pin a walk geometry (tests, A/B): 64, 256 or 3
+    if (const char* e = std::getenv("WSC_WALK_MODE"); e && *e) {   // pin a walk geometry (tests, A/B): 64, 65, 256 or 3
         const int m = std::atoi(e);
-        c->walk_mode = (m == 64 || m == 256 || m == 3) ? m : 0;
+        c->walk_mode = (m == 64 || m == 65 || m == 256 || m == 3) ? m : 0;
     }
     if (const char* e = std::getenv("WSC_U8_INLINE_MAX"); e && *e)   // test knob: 0 sends all text chip-wide
         c->u8_inline_max = (uint32_t)std::strtoul(e, nullptr, 10);
@@ -439,10 +444,13 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     // fewer flags and leave stale inclusive prefixes for the next walk)
     const uint32_t mode = phase == 2 && c->walk_used ? c->walk_used : walk_mode(c, n, stream_cus(c, split ? sw : st));
     const uint32_t wnt = mode == 64 ? 64u : 256u;
-    const dim3 wblk(wnt), wgrid((n + wnt - 1) / wnt);
+    const uint32_t spb = mode == 65 ? 64u : wnt;   // segments per walk block
+    const dim3 wblk(wnt), wgrid((n + spb - 1) / spb);
     if (phase != 2) {
         c->walk_used = mode;
         c->walk_blocks = wgrid.x;
+        if (wgrid.x + 1 > c->max_walk_blocks)   // never index look-back state past its allocation
+            return fail(WSC_E_INTERNAL, "walk geometry needs more look-back blocks than allocated");
     }
     uint32_t rearm = 0;   // (after the launch below: the tiled walk sets walk_blocks)
     auto rec = [&](int i) {
@@ -475,11 +483,13 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
         if (compact) hipLaunchKernelGGL((k_walk_emit<true>), wgrid, wblk, 0, ws, wa);
         else hipLaunchKernelGGL((k_walk_emit<false>), wgrid, wblk, 0, ws, wa);
     } else if (compact) {
-        if (wnt == 64) hipLaunchKernelGGL((k_walk_fused<true, 16, 64, 1>), wgrid, wblk, 0, ws, wa);
-        else hipLaunchKernelGGL((k_walk_fused<true, 16, 256, 1>), wgrid, wblk, 0, ws, wa);
+        if (mode == 65) hipLaunchKernelGGL((k_walk_fused<true, 16, 256, 1, 64>), wgrid, wblk, 0, ws, wa);
+        else if (wnt == 64) hipLaunchKernelGGL((k_walk_fused<true, 16, 64, 1, 64>), wgrid, wblk, 0, ws, wa);
+        else hipLaunchKernelGGL((k_walk_fused<true, 16, 256, 1, 256>), wgrid, wblk, 0, ws, wa);
     } else {
-        if (wnt == 64) hipLaunchKernelGGL((k_walk_fused<false, 16, 64, 1>), wgrid, wblk, 0, ws, wa);
-        else hipLaunchKernelGGL((k_walk_fused<false, 16, 256, 1>), wgrid, wblk, 0, ws, wa);
+        if (mode == 65) hipLaunchKernelGGL((k_walk_fused<false, 16, 256, 1, 64>), wgrid, wblk, 0, ws, wa);
+        else if (wnt == 64) hipLaunchKernelGGL((k_walk_fused<false, 16, 64, 1, 64>), wgrid, wblk, 0, ws, wa);
+        else hipLaunchKernelGGL((k_walk_fused<false, 16, 256, 1, 256>), wgrid, wblk, 0, ws, wa);
     }
     HIP_TRY(hipGetLastError());
     if (split) HIP_TRY(hipEventRecord(c->ev_walked, ws));

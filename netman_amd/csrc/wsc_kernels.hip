@@ -948,39 +948,42 @@ __global__ __launch_bounds__(256) void k_walk_emit(WalkArgs a) {
     walk_segment<true, COMPACT, 256>(a, s, base, own, nullptr, nullptr);
 }
 
-// LDS of one tile of the walk: NT lanes, G consecutive segments per lane, KR frame records per lane
-template <bool COMPACT, uint32_t KR, uint32_t NT, uint32_t G>
+// LDS of one tile of the walk: NT lanes of which the first WL walk segments (G consecutive
+// segments per walking lane), KR frame records per walking lane; every lane emits
+template <bool COMPACT, uint32_t KR, uint32_t NT, uint32_t G, uint32_t WL = NT>
 struct WalkLds {
+    static_assert(WL % 64 == 0 && WL <= NT && WL <= 256, "walking lanes: whole waves, owner is a byte");
     SegCount prefix;
     SegCount wave[NT / 64];
     uint32_t wtot[NT / 64];
-    uint4 rec[KR * NT];      // [record][lane]: conflict-free 16 B per lane
-    uint4 rec2[KR * NT];     // the frame's MsgID / span ordinal / arena offset / previous span end
-    uint8_t owner[KR * NT];  // flat replayed frame -> its lane
-    uint32_t rpre[NT];       // lane's first flat replayed frame
+    uint4 rec[KR * WL];      // [record][lane]: conflict-free 16 B per lane
+    uint4 rec2[KR * WL];     // the frame's MsgID / span ordinal / arena offset / previous span end
+    uint8_t owner[KR * WL];  // flat replayed frame -> its lane
+    uint32_t rpre[WL];       // lane's first flat replayed frame
     uint32_t nbig;           // long spans whose window index the wave writes
     uint4 big[64];
     // per segment, [segment of the lane][lane]: start, global frame / span (/ arena) bases, counts,
     // consumed bytes + terminal status, wire end of its last span, replayed from LDS or not
-    uint64_t sstart[G * NT], ldend[G * NT];
-    uint32_t fbase[G * NT], sbase[G * NT], nf[G * NT], ns[G * NT];
-    uint32_t cons[G * NT], endst[G * NT];
-    uint64_t abase[COMPACT ? G * NT : 1], ob0[COMPACT ? G * NT : 1];
-    uint8_t rep[G * NT], r0[G * NT];   // (r0: the segment's first record in the lane's list)
+    uint64_t sstart[G * WL], ldend[G * WL];
+    uint32_t fbase[G * WL], sbase[G * WL], nf[G * WL], ns[G * WL];
+    uint32_t cons[G * WL], endst[G * WL];
+    uint64_t abase[COMPACT ? G * WL : 1], ob0[COMPACT ? G * WL : 1];
+    uint8_t rep[G * WL], r0[G * WL];   // (r0: the segment's first record in the lane's list)
 };
 
 // Count phase of a tile: each lane walks its G segments (first one s0; segments from seg_lim on
 // are not the tile's), keeping up to KR frame records in LDS; writes the connections' carried
-// state.  Returns the lane's total.
-template <bool COMPACT, uint32_t KR, uint32_t NT, uint32_t G>
-__device__ __forceinline__ SegCount tile_count(const WalkArgs& a, WalkLds<COMPACT, KR, NT, G>& L, uint32_t s0,
+// state.  Returns the lane's total (lanes from WL on walk nothing).
+template <bool COMPACT, uint32_t KR, uint32_t NT, uint32_t G, uint32_t WL>
+__device__ __forceinline__ SegCount tile_count(const WalkArgs& a, WalkLds<COMPACT, KR, NT, G, WL>& L, uint32_t s0,
                                                uint32_t seg_lim, uint32_t lane, uint32_t& nrec) {
     const SegCount zero = {};
     SegCount tot = zero;
     nrec = 0;
+    if (lane >= WL) return tot;
     for (uint32_t j = 0; j < G; ++j) {
         const uint32_t s = s0 + j;
-        const uint32_t q = j * NT + lane;
+        const uint32_t q = j * WL + lane;
         if (s >= seg_lim) {
             L.nf[q] = L.ns[q] = 0;
             L.rep[q] = 0;
@@ -989,8 +992,8 @@ __device__ __forceinline__ SegCount tile_count(const WalkArgs& a, WalkLds<COMPAC
         }
         WalkEnd we;
         const uint32_t cap = KR - nrec;
-        const SegCount c = walk_segment<false, COMPACT, NT>(a, s, zero, zero, L.rec + nrec * NT + lane, &we,
-                                                            L.rec2 + nrec * NT + lane, cap, j);
+        const SegCount c = walk_segment<false, COMPACT, WL>(a, s, zero, zero, L.rec + nrec * WL + lane, &we,
+                                                            L.rec2 + nrec * WL + lane, cap, j);
         const uint64_t ss = a.seg_off[s];
         const bool rep = we.replay;
         L.r0[q] = (uint8_t)nrec;
@@ -1100,20 +1103,22 @@ __device__ __forceinline__ SegCount block_lookback(const WalkArgs& a, uint32_t b
 // the lane's exclusive scan): per segment bases, then every frame held in LDS emitted
 // cooperatively in flat order (consecutive records, spans and arena offsets in memory, so each
 // store instruction covers contiguous bytes), then the per segment results; segments whose frames
-// did not fit re-walk their (cache-warm) headers to emit.  lane o's first segment is seg0 + o * G.
-template <bool COMPACT, uint32_t KR, uint32_t NT, uint32_t G>
-__device__ __forceinline__ void tile_emit(const WalkArgs& a, WalkLds<COMPACT, KR, NT, G>& L, const SegCount& lb,
+// did not fit re-walk their (cache-warm) headers to emit.  Walking lane o's first segment is
+// seg0 + o * G; lanes from WL on only take part in the cooperative emit.
+template <bool COMPACT, uint32_t KR, uint32_t NT, uint32_t G, uint32_t WL>
+__device__ __forceinline__ void tile_emit(const WalkArgs& a, WalkLds<COMPACT, KR, NT, G, WL>& L, const SegCount& lb,
                                           uint32_t nrec, uint32_t seg0, uint32_t seg_lim, uint32_t lane) {
     constexpr uint32_t NW = NT / 64;
     const uint32_t wl = lane & 63, wave = lane >> 6;
     const uint32_t s0 = seg0 + lane * G;
+    const bool walker = lane < WL;
     const SegCount zero = {};
     // ---- per segment bases ----
-    {
+    if (walker) {
         uint32_t fb = lb.frames, sb = lb.spans0 + lb.spans1;
         uint64_t ab = lb.bytes0 + lb.bytes1;
         for (uint32_t j = 0; j < G; ++j) {
-            const uint32_t q = j * NT + lane;
+            const uint32_t q = j * WL + lane;
             const uint32_t s = s0 + j;
             const uint32_t fl = L.fbase[q];
             if (s < seg_lim && (fl & SEGF_U8DEFER)) {
@@ -1148,7 +1153,7 @@ __device__ __forceinline__ void tile_emit(const WalkArgs& a, WalkLds<COMPACT, KR
         if (w < wave) rpre += L.wtot[w];
         F += L.wtot[w];
     }
-    L.rpre[lane] = rpre;
+    if (walker) L.rpre[lane] = rpre;
     for (uint32_t k = 0; k < nrec; ++k) L.owner[rpre + k] = (uint8_t)lane;
     __syncthreads();
     // ---- cooperative emit ----
@@ -1156,10 +1161,10 @@ __device__ __forceinline__ void tile_emit(const WalkArgs& a, WalkLds<COMPACT, KR
     for (uint32_t f = lane; f < F; f += NT) {
         const uint32_t o = L.owner[f];
         const uint32_t k = f - L.rpre[o];
-        const uint4 r = L.rec[k * NT + o];
-        const uint4 q = L.rec2[k * NT + o];
+        const uint4 r = L.rec[k * WL + o];
+        const uint4 q = L.rec2[k * WL + o];
         const uint32_t j = r.w >> 28;
-        const uint32_t qi = j * NT + o;
+        const uint32_t qi = j * WL + o;
         const uint64_t ss = L.sstart[qi];
         const uint32_t hl = (r.w >> 14) & 15, fl = (r.w >> 18) & 0xFF, region = (r.w >> 26) & 1;
         const bool have_span = (r.w >> 27) & 1;
@@ -1212,10 +1217,10 @@ __device__ __forceinline__ void tile_emit(const WalkArgs& a, WalkLds<COMPACT, KR
         }
     }
     // ---- per segment results; segments not held in LDS re-walk their (cache-warm) headers ----
-    for (uint32_t j = 0; j < G; ++j) {
+    for (uint32_t j = 0; j < G && walker; ++j) {
         const uint32_t s = s0 + j;
         if (s >= seg_lim) break;
-        const uint32_t q = j * NT + lane;
+        const uint32_t q = j * WL + lane;
         const uint64_t se = a.seg_off[s + 1];
         if (L.rep[q]) {
             const uint64_t Wd = W;   // windows that start after the last span, up to the segment end
@@ -1261,26 +1266,29 @@ __device__ __forceinline__ void write_summary(const WalkArgs& a, const SegCount&
     if (sm.overflow) __hip_atomic_fetch_or(a.sticky, sm.overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// The fused walk kernel: NT lanes (64 or 256) per block, G consecutive segments per lane, KR frame
-// records per lane in LDS.  The host picks NT so that the blocks fill the CUs once (the count
-// phase wants every CU; the look-back wants few blocks).  Phases: count (each lane walks its
+// The fused walk kernel: NT lanes (64 or 256) per block, the first WL of them walk G consecutive
+// segments each, KR frame records per walking lane in LDS.  The host picks the geometry so that
+// the blocks fill the CUs once (the count phase wants every CU; the look-back wants few blocks).
+// WL < NT (64 walking lanes in a 256-lane block): one wave per CU walks -- the chain of headers of
+// a segment is serial whatever the wave count -- and all four emit, so the emit's stores issue
+// from every SIMD (configs[2]: 64 segments per CU, the emit was 10 us on one wave).  Phases: count (each lane walks its
 // segments; records in LDS) -> block scan -> decoupled look-back -> cooperative emit.  Block ids
 // come from a ticket counter in dispatch order, so every block a block waits for has already
 // started.  Flags and the ticket are zeroed by k_unmask (the next launch on the stream) of every
 // decode, and at context creation.
-template <bool COMPACT, uint32_t KR, uint32_t NT, uint32_t G>
+template <bool COMPACT, uint32_t KR, uint32_t NT, uint32_t G, uint32_t WL>
 __global__ __launch_bounds__(NT) void k_walk_fused(WalkArgs a) {
     __shared__ uint32_t sh_bid;
-    __shared__ WalkLds<COMPACT, KR, NT, G> L;
+    __shared__ WalkLds<COMPACT, KR, NT, G, WL> L;
     const uint32_t lane = threadIdx.x, wl = threadIdx.x & 63, wave = threadIdx.x >> 6;
     if (lane == 0) sh_bid = __hip_atomic_fetch_add(a.lb_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     const uint32_t bid = sh_bid;
-    const uint32_t n_blocks = (a.n_segs + NT * G - 1) / (NT * G);
+    const uint32_t n_blocks = (a.n_segs + WL * G - 1) / (WL * G);
     uint64_t t0 = 0, t1 = 0, t2 = 0;
     if (a.dbg && lane == 0) t0 = __builtin_amdgcn_s_memrealtime();
     uint32_t nrec;
-    const SegCount tot = tile_count<COMPACT, KR, NT, G>(a, L, (bid * NT + lane) * G, a.n_segs, lane, nrec);
+    const SegCount tot = tile_count<COMPACT, KR, NT, G>(a, L, (bid * WL + lane) * G, a.n_segs, lane, nrec);
     SegCount btot;
     const SegCount excl = tile_scan<NT>(tot, L, wl, wave, btot);
     if (wave == 0) {
@@ -1290,7 +1298,7 @@ __global__ __launch_bounds__(NT) void k_walk_fused(WalkArgs a) {
     }
     __syncthreads();
     if (a.dbg && lane == 0) t2 = __builtin_amdgcn_s_memrealtime();
-    tile_emit<COMPACT, KR, NT, G>(a, L, sc_add(L.prefix, excl), nrec, bid * NT * G, a.n_segs, lane);
+    tile_emit<COMPACT, KR, NT, G>(a, L, sc_add(L.prefix, excl), nrec, bid * WL * G, a.n_segs, lane);
     if (a.dbg) {   // diagnostic timestamps (100 MHz s_memrealtime), written only to the dbg buffer
         __syncthreads();
         if (lane == 0) {
@@ -1685,10 +1693,12 @@ template __global__ void k_u8_check<4>(U8Args);
 
 // explicit instantiations used by the host code: 16 frame records per lane, one segment per
 // lane, blocks of 64 or 256 lanes; batches of more segments use the three-launch walk below
-template __global__ void k_walk_fused<false, 16, 64, 1>(WalkArgs);
-template __global__ void k_walk_fused<true, 16, 64, 1>(WalkArgs);
-template __global__ void k_walk_fused<false, 16, 256, 1>(WalkArgs);
-template __global__ void k_walk_fused<true, 16, 256, 1>(WalkArgs);
+template __global__ void k_walk_fused<false, 16, 64, 1, 64>(WalkArgs);
+template __global__ void k_walk_fused<true, 16, 64, 1, 64>(WalkArgs);
+template __global__ void k_walk_fused<false, 16, 256, 1, 256>(WalkArgs);
+template __global__ void k_walk_fused<true, 16, 256, 1, 256>(WalkArgs);
+template __global__ void k_walk_fused<false, 16, 256, 1, 64>(WalkArgs);
+template __global__ void k_walk_fused<true, 16, 256, 1, 64>(WalkArgs);
 template __global__ void k_walk_tiled<false, 4, 256>(WalkArgs, uint32_t);
 template __global__ void k_walk_tiled<true, 4, 256>(WalkArgs, uint32_t);
 template __global__ void k_walk_count<false>(WalkArgs);

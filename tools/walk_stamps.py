@@ -30,7 +30,10 @@ if n > 256 * n_cu:   # the library's walk geometry (wsc_api.cpp walk_mode): thre
     print(f"{wl}: {n} segments -> three-launch walk (no per-block stamps)")
     print(c.profile(b, 5) if False else "")
     raise SystemExit(0)
-nb = (n + 63) // 64 if n <= 64 * n_cu else (n + 255) // 256
+mode = int(os.environ.get("WSC_WALK_MODE", "0"))
+if mode == 0:
+    mode = 65 if n <= 64 * n_cu else 256
+nb = (n + 63) // 64 if mode in (64, 65) else (n + 255) // 256
 for it in range(3):
     c.decode(b)
     c.sync()
