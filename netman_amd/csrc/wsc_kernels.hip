@@ -259,7 +259,7 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
     uint32_t u8fail = 0xFFFFFFFFu;
     uint32_t u8dfa = (cont || frem) ? st.cont_utf8 : 0u;
     bool u8_pending = false;                      // a text chain has a deferred (chip-wide) part
-    uint32_t u8_head = 0xFFFFFFFFu, u8_last = 0xFFFFFFFFu, u8_n = 0;
+    uint32_t u8_head = 0xFFFFFFFFu, u8_last = 0xFFFFFFFFu, u8_n = 0, u8_ncomp = 0;
     bool u8_comp = false;                         // an item whose verdict needs the segment's composition
     uint32_t pool_next = 0, pool_end = 0;         // the segment's unused item slots
     auto dead_fill = [&](uint32_t i, uint32_t e) {
@@ -378,6 +378,7 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
                 else u8_head = idx;
                 u8_last = idx;
                 u8_n += 1;
+                if (part || chain || pieces != 1) u8_ncomp += 1;   // counted by k_u8_check
             }
         }
         if (part || chain || pieces != 1) u8_comp = true;
@@ -758,7 +759,7 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
         if (u8_n) {
             U8Seg g{};
             g.head = u8_head;
-            g.n = u8_n;
+            g.n = u8_ncomp;   // the composite items (single-piece messages are never counted)
             g.done = 0;
             g.pending_end = (u8_pending ? 1u : 0u) | (u8_comp ? 2u : 0u);
             g.minfail = 0xFFFFFFFFu;
@@ -1377,34 +1378,34 @@ __global__ __launch_bounds__(NT) void k_walk_tiled(WalkArgs a, uint32_t per_bloc
 // the completing lane reads them with agent-scope atomic RMWs (MI355X_MICROARCH.md "Valid forms").
 // ---------------------------------------------------------------------------------------------
 
-// One item's result; true if it was the last item of its segment to finish (its lane then decides
-// the segment's verdict).
-__device__ __forceinline__ bool u8_publish(const U8Args& a, uint32_t it, const U8Item& self, uint64_t acc) {
-    if (self.seg == U8_DEAD) return false;   // an unused slot of a walk pool
-    if (self.kind == U8K_SELF && self.first && self.last) {
-        if (u8m_get(acc, 0) != 0)
-            __hip_atomic_fetch_min(&a.seg[self.seg].minfail, self.ordinal, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-        __hip_atomic_store(a.maps + it, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const uint32_t n = a.seg[self.seg].n;
-    return __hip_atomic_fetch_add(&a.seg[self.seg].done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 == n;
+// One item's result: U8R_DEAD (an unused pool slot), U8R_PASS / U8R_FAIL (a single-piece TEXT
+// message: nothing is written when it passes), U8R_COMP (any other item: its map is published,
+// then counted into its segment once drained).
+enum : uint32_t { U8R_DEAD = 0, U8R_PASS = 1, U8R_FAIL = 2, U8R_COMP = 3 };
+__device__ __forceinline__ uint32_t u8_store(const U8Args& a, uint32_t it, const U8Item& self, uint64_t acc) {
+    if (self.seg == U8_DEAD) return U8R_DEAD;
+    if (self.kind == U8K_SELF && self.first && self.last) return u8m_get(acc, 0) != 0 ? U8R_FAIL : U8R_PASS;
+    __hip_atomic_store(a.maps + it, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return U8R_COMP;
+}
+// `cnt` composite items counted into their segment, after the lane's map stores are drained:
+// `ret` = the count before them, `n` = the segment's composite items (ret + cnt == n: they
+// complete it -- the lane composes the segment's chains).  The caller reads ret / n late.
+__device__ __forceinline__ void u8_count(const U8Args& a, uint32_t seg, uint32_t cnt, uint32_t& ret, uint32_t& n) {
+    n = a.seg[seg].n;
+    ret = __hip_atomic_fetch_add(&a.seg[seg].done, cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// A segment's verdict (one lane): the first failing frame -- the single-piece SELF items' minimum
-// or the first failing composition -- and, if any, its results.  Returns the failing frame's wire
-// end (the wave then re-masks the later spans), else ~0.
-__device__ __forceinline__ uint64_t u8_verdict(const U8Args& a, uint32_t s, const U8Seg& g) {
+// A segment's composite items composed in frame order with the walk's states (one lane, once all
+// are published): the first failing composite frame's ordinal, 0xFFFFFFFF if none -- then an open
+// text chain (continueBuffer and/or a streamed frame's pieces) carries its DFA state.  Single-piece
+// SELF items never sit inside a chain and are skipped.
+__device__ __forceinline__ uint32_t u8_comp_verdict(const U8Args& a, uint32_t s, const U8Seg& g) {
     uint32_t cur = 0, start = 0;   // states 0..7, 0xFF = reject
-    uint32_t fail = __hip_atomic_fetch_add(&a.seg[s].minfail, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // compose the composite items in frame order with the walk's states (a chain never has a
-    // single-piece SELF item inside it)
     uint64_t fm = u8m_id();
-    uint32_t j = (g.pending_end & 2u) ? g.head : 0xFFFFFFFFu;
-    for (uint32_t c = 0; c < g.n && j != 0xFFFFFFFFu; ++c) {
+    uint32_t j = g.head;
+    for (uint32_t c = 0; c < a.items_cap && j != 0xFFFFFFFFu; ++c) {
         const U8Item x = a.items[j];
-        if (x.ordinal >= fail) break;   // a single-piece SELF frame failed first
         if (x.kind == U8K_SELF && x.first && x.last) { j = x.next; continue; }
         const uint64_t m = __hip_atomic_fetch_add(a.maps + j, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (x.first) {
@@ -1417,42 +1418,56 @@ __device__ __forceinline__ uint64_t u8_verdict(const U8Args& a, uint32_t s, cons
             if (x.kind == U8K_PART) {
                 cur = end;
             } else {
-                if (end != 0) { fail = x.ordinal; break; }   // (ordinal < fail: checked above)
+                if (end != 0) return x.ordinal;
                 if (x.kind == U8K_CHAIN) cur = 0;
             }
         }
         j = x.next;
     }
-    if (fail == 0xFFFFFFFFu) {
-        // an open text chain (continueBuffer and/or a streamed frame's pieces) carries its state
-        if ((g.pending_end & 1u) && (a.state_out[s].cont_len || a.state_out[s].frame_rem))
-            a.state_out[s].cont_utf8 = (uint8_t)(cur > 7 ? 8u : cur);
-        return ~0ull;
-    }
-    // frame `fail` fails: CloseCode(1007) there (epoll.go:126-127), nothing after it is read
-    wsc_frame* f = a.frames + g.fbase + fail;
-    f->kind = WSC_FK_ERROR;
-    f->err = WSC_ERR_MUST_UTF8;
-    const uint64_t fend = f->hdr_off + f->hdr_len + (f->payload_len | (uint64_t)f->payload_len_hi << 32);
-    wsc_seg_result r = a.seg_out[s];
-    r.consumed = fend - a.seg_off[s];
-    r.frame_count = fail + 1;
-    r.status = WSC_SEG_ERROR;
-    r.close_code = 1007;
-    r.err = WSC_ERR_MUST_UTF8;
-    a.seg_out[s] = r;
-    a.state_out[s].status = WSC_SEG_ERROR;
-    return fend;
+    if ((g.pending_end & 1u) && (a.state_out[s].cont_len || a.state_out[s].frame_rem))
+        a.state_out[s].cont_utf8 = (uint8_t)(cur > 7 ? 8u : cur);
+    return 0xFFFFFFFFu;
 }
 
-// The segment's spans that start at or after `fend` were unmasked although the reference never
-// reads them: XOR them again, the whole wave 16 B per lane (1 KiB per step).  The key is phased at
-// the wire (byte x takes key byte x & 3), in place and in the arena alike.
-__device__ __forceinline__ void u8_remask(const U8Args& a, uint32_t seg, uint64_t fend, uint32_t lane) {
+// Frame `ord` of segment s fails utf8.Valid (one lane): CloseCode(1007) there (epoll.go:126-127),
+// nothing after it is read.  Failures of one segment may be found in any order, so each takes
+// part only if it lowers the segment's minimum: its record becomes WSC_FK_ERROR, the segment's
+// consumed bytes and frame count are min-folded (a smaller failure always gives smaller values),
+// and the spans between this frame's end and the previous minimum's end are re-masked (those past
+// the previous minimum's end were re-masked when it took part).  Returns that wire range
+// [lo, hi) (empty: nothing to re-mask).
+__device__ __forceinline__ void u8_fail(const U8Args& a, uint32_t s, uint32_t ord, uint64_t& lo, uint64_t& hi) {
+    lo = hi = 0;
+    const uint32_t old = __hip_atomic_fetch_min(&a.seg[s].minfail, ord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (ord >= old) return;   // an earlier frame already failed
+    const uint32_t fbase = a.seg[s].fbase;
+    auto frame_end = [&](uint32_t o) {
+        const wsc_frame* f = a.frames + fbase + o;
+        return f->hdr_off + f->hdr_len + (f->payload_len | (uint64_t)f->payload_len_hi << 32);
+    };
+    wsc_frame* f = a.frames + fbase + ord;
+    f->kind = WSC_FK_ERROR;
+    f->err = WSC_ERR_MUST_UTF8;
+    const uint64_t fend = frame_end(ord);
+    wsc_seg_result* r = a.seg_out + s;
+    __hip_atomic_fetch_min(&r->consumed, fend - a.seg_off[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_min(&r->frame_count, ord + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    r->status = WSC_SEG_ERROR;
+    r->close_code = 1007;
+    r->err = WSC_ERR_MUST_UTF8;
+    a.state_out[s].status = WSC_SEG_ERROR;
+    lo = fend;
+    hi = old == 0xFFFFFFFFu ? ~0ull : frame_end(old);
+}
+
+// The segment's spans that start in [lo, hi) were unmasked although the reference never reads
+// them: XOR them again, the whole wave 16 B per lane (1 KiB per step).  The key is phased at the
+// wire (byte x takes key byte x & 3), in place and in the arena alike.
+__device__ __forceinline__ void u8_remask(const U8Args& a, uint32_t seg, uint64_t lo, uint64_t hi, uint32_t lane) {
     const U8Seg g = a.seg[seg];
     for (uint32_t k = 0; k < g.nspans; ++k) {
         const Span sp = a.spans[g.sbase + k];
-        if (sp.src < fend) continue;
+        if (sp.src < lo || sp.src >= hi) continue;
         uint8_t* d = a.out + sp.dst;
         for (uint32_t i = lane * 16u; i < sp.len; i += 1024u) {
             const uint32_t key = rotr32(sp.key, 8u * (uint32_t)((sp.src + i) & 3));
@@ -1482,20 +1497,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
     // a batch whose records overflowed is invalid as a whole (the caller re-decodes it): its
     // verdicts are not applied -- the failing frame or its later spans may lie past the capacity
     const bool ovf = a.summary->overflow != 0;
-    // segments completed by this wave's items: their verdicts (one lane each, serial over the
-    // segment's items), failing ones re-masked by the whole wave
-    auto settle = [&](bool trig, uint32_t seg) {
-        uint64_t pend = __ballot(trig);
+    // failing frames of this wave (ordinal `ord` of segment `seg` on the lanes where `f`): each
+    // applied by its lane, the spans it hands back re-masked by the whole wave
+    auto rd64 = [](uint64_t v, uint32_t l) {
+        return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), (int)l) << 32 |
+               (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)l);
+    };
+    auto fail_settle = [&](bool f, uint32_t seg, uint32_t ord) {
+        uint64_t pend = __ballot(f && !ovf);
         while (pend) {
             const uint32_t l = (uint32_t)__builtin_ctzll(pend);
             pend &= pend - 1;
             const uint32_t sg = (uint32_t)__builtin_amdgcn_readlane((int)seg, (int)l);
-            uint64_t fe = ~0ull;
-            if (lane == l && !ovf) fe = u8_verdict(a, sg, a.seg[sg]);
-            const uint64_t fend = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(fe >> 32), (int)l) << 32 |
-                                  (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)fe, (int)l);
-            if (fend != ~0ull) u8_remask(a, sg, fend, lane);
+            uint64_t lo = 0, hi = 0;
+            if (lane == l) u8_fail(a, sg, ord, lo, hi);
+            lo = rd64(lo, l);
+            hi = rd64(hi, l);
+            if (lo < hi) u8_remask(a, sg, lo, hi, lane);
         }
+    };
+    // segments whose composite items this wave completed: their chains composed (one lane each,
+    // serial over the segment's items), a failing frame applied as above
+    auto settle = [&](bool trig, uint32_t seg) {
+        uint32_t ord = 0xFFFFFFFFu;
+        if (trig && !ovf) ord = u8_comp_verdict(a, seg, a.seg[seg]);
+        fail_settle(ord != 0xFFFFFFFFu, seg, ord);
     };
     if (blockIdx.x * 4 < n_items) {   // (nothing deferred, or fewer units than waves: only the signal)
     u8_tables_init(T, threadIdx.x);
@@ -1597,9 +1623,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
                 b0 = nb;
             }
             if (!mids_in) acc = u8m_then(acc, mids);
-            bool done = false;
-            if (lane == 0) done = u8_publish(a, i0 + j, item, acc);
-            settle(done, item.seg);
+            uint32_t res = U8R_DEAD, ret = 0, n = 0;
+            if (lane == 0) res = u8_store(a, i0 + j, item, acc);
+            res = (uint32_t)__builtin_amdgcn_readfirstlane((int)res);
+            fail_settle(lane == 0 && res == U8R_FAIL, item.seg, item.ordinal);
+            if (res == U8R_COMP) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the map before the count
+                if (lane == 0) u8_count(a, item.seg, 1u, ret, n);
+            }
+            settle(lane == 0 && res == U8R_COMP && ret + 1 == n, item.seg);
         }
     };
     const uint32_t n_units = (n_items + 3) / 4;
@@ -1634,6 +1666,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
     UnitS xc, xn;
     u32x4 qc[4] = {};
     bool cur_small = false;
+    // the previous small unit's counts, settled one unit later (after the next unit's loads are
+    // out): the counter round trip is then never waited for on its own
+    bool pact = false;
+    uint32_t pret = 0, pn = 0, pseg = 0, pcnt = 0;
     if (gw < n_units) {
         unit_items(gw, xc);
         cur_small = unit_small(xc);
@@ -1663,10 +1699,37 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
                 nsmall = unit_small(xn);
                 if (nsmall) unit_data(xn, qn);
             }
-            bool done = false;
-            if ((lane & 15) == 0 && r < cnt) done = u8_publish(a, i0 + r, xr, rm);
-            settle(done, xr.seg);
+            settle(pact && pret + pcnt == pn, pseg);
+            // the unit's items: failures applied at once; composite items counted per run of
+            // rows on one segment (a walk pool hands a segment 4 consecutive slots), one counter
+            // atomic per run
+            uint32_t res = U8R_DEAD;
+            if ((lane & 15) == 0 && r < cnt) res = u8_store(a, i0 + r, xr, rm);
+            fail_settle(res == U8R_FAIL, xr.seg, xr.ordinal);
+            const bool ok = res == U8R_COMP;
+            if (__ballot(ok)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // maps before counts
+            const uint64_t okm = __ballot(ok);
+            uint32_t rs[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) rs[q] = (uint32_t)__builtin_amdgcn_readlane((int)xr.seg, 16 * q);
+            auto row_ok = [&](uint32_t q) { return ((okm >> (16 * q)) & 1) != 0; };
+            pact = false;
+            pcnt = 0;
+            if (ok) {
+                const uint32_t sg = xr.seg;
+                const bool head = !(r > 0 && row_ok(r - 1) && rs[r - 1] == sg);
+                if (head) {
+                    uint32_t run = 1;
+                    while (r + run < 4 && row_ok(r + run) && rs[r + run] == sg) ++run;
+                    u8_count(a, sg, run, pret, pn);
+                    pact = true;
+                    pcnt = run;
+                }
+            }
+            pseg = xr.seg;
         } else {
+            settle(pact && pret + pcnt == pn, pseg);
+            pact = false;
             unit_large(i0, cnt);
             if (un < n_units) {
                 nsmall = unit_small(xn);
@@ -1679,6 +1742,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
         cur_small = nsmall;
         if (un + nw < n_units) unit_items(un + nw, xn);
     }
+    settle(pact && pret + pcnt == pn, pseg);
     }
     // staged pipeline: the decode's last kernel tells the host its scratch is free
     if (a.fin_host) {

@@ -145,3 +145,42 @@ def test_text_large_frames_cross_piece_characters(codec_lib):
         compare_segment(i, s, int(off[i]), res, O.run(s), wire_after=wire)
     assert [int(x) for x in res.seg["status"]] == [K.SEG_OPEN, K.SEG_OPEN, K.SEG_ERROR, K.SEG_CLOSED]
     c.close()
+
+
+@pytest.mark.parametrize("compact", [False, True])
+def test_text_1k_several_failures_per_connection(codec_lib, compact):
+    """1 KiB TEXT frames (deferred single-piece messages, checked 4 per wave step in any order):
+    connections with 1-3 bad frames each, and connections whose text chain (fragments of 300 B)
+    fails after a bad single-piece frame or before one.  Failures of one connection are applied in
+    whatever order the waves finish: each takes part only if it lowers the connection's first
+    failure, re-masking just the spans between its frame and the previous minimum's -- the
+    records, consumed bytes and bytes must equal the oracle's (first failure wins)."""
+    rng = np.random.default_rng(17)
+    good = ("ab" + "é" * 300 + "xyz" + "€" * 40).encode()[:1024]
+    good = good + b"a" * (1024 - len(good))
+    bad = bytearray(good)
+    streams = []
+    for i in range(2048):
+        n = 16
+        bad_at = set(int(x) for x in rng.choice(n, int(rng.integers(0, 4)), replace=False))
+        parts = []
+        for k in range(n):
+            if k in bad_at:
+                b = bytearray(good)
+                b[int(rng.integers(0, 1024))] = 0xFF
+                parts.append(synth.frame(1, bytes(b)))
+            elif i % 5 == 0 and k == 8:   # a fragmented text message, maybe bad in its second piece
+                frag = ("é" * 450).encode()
+                f2 = bytearray(frag[300:])
+                if i % 10 == 0:
+                    f2[7] = 0xC0
+                parts.append(synth.frame(1, frag[:300], fin=False) + synth.frame(0, bytes(f2), fin=True))
+            else:
+                parts.append(synth.frame(1, good))
+        streams.append(b"".join(parts))
+    c = K.Codec(0, max_batch_bytes=64 << 20, max_segs=4096, max_frames=1 << 16)
+    try:
+        res = _check(c, streams, compact=compact)
+        assert int((res.seg["status"] == K.SEG_ERROR).sum()) > 0
+    finally:
+        c.close()
