@@ -178,9 +178,15 @@ __device__ __forceinline__ void pm_mask(const u32x4* __restrict__ pm, uint32_t l
     m[0] = h[0] & ~l[0]; m[1] = h[1] & ~l[1]; m[2] = h[2] & ~l[2]; m[3] = h[3] & ~l[3];
 }
 
+// Two passes: (1) every piece lying inside one payload is a plain gather + store (the common case
+// even at 1 KiB frames: ~4 frame edges in 256 pieces); (2) the pieces holding a header or a frame
+// edge are compacted into lanes (LDS list, in window order) and assembled together -- one pass
+// of the costly header placement per window instead of one per 1 KiB slice (PMC: the slice-wise
+// version issued ~600 VALU per window at 1 KiB frames, past the HBM budget).
 template <int NT>
 __device__ __forceinline__ bool encode_window_lanes(const EncCopyArgs& a, uint32_t m, uint64_t wbase, uint64_t limit,
-                                                    uint32_t lane, const u32x4* __restrict__ pm) {
+                                                    uint32_t lane, const u32x4* __restrict__ pm,
+                                                    uint16_t* __restrict__ elist) {
     constexpr uint32_t P = ENC_WIN / 1024;
     constexpr int64_t WB = ENC_WIN;
     auto clip = [](int64_t x) -> int32_t { return (int32_t)(x < -(1ll << 30) ? -(1ll << 30) : (x > WB + 64 ? WB + 64 : x)); };
@@ -202,21 +208,53 @@ __device__ __forceinline__ bool encode_window_lanes(const EncCopyArgs& a, uint32
     if (nl == 64 && __shfl(re, 63) < (int32_t)WB && m + 64 < a.n_msgs) return false;
     const uint32_t so_lo = (uint32_t)so, so_hi = (uint32_t)((uint64_t)so >> 32);
 
-    // binary search: first step = the power of two with 2*st0 > nl (wave-uniform), as many steps
-    // as the window's frame count needs (3 for 1 KiB frames instead of 6)
+    // binary search: the last frame (lane) whose header starts at or before window byte pr; first
+    // step = the power of two with 2*st0 > nl (wave-uniform), as many steps as the window needs
     const int32_t st0 = nl == 0 ? 0 : (nl >= 32 ? 32 : (int32_t)((1u << (32 - __builtin_clz(nl))) >> 1));
-    int32_t ta[P];
-#pragma unroll
-    for (uint32_t k = 0; k < P; ++k) {
-        const int32_t pr = (int32_t)(k * 1024 + lane * 16);
+    auto find = [&](int32_t pr) -> int32_t {
         int32_t lo = -1;
         for (int32_t st = st0; st >= 1; st >>= 1) {
             const int32_t c = lo + st;
             const int32_t dv = __shfl(ro, c & 63);
             if (c < (int32_t)nl && dv <= pr) lo = c;
         }
-        ta[k] = lo < 0 ? 0 : lo;
+        return lo < 0 ? 0 : lo;
+    };
+    auto store_piece = [&](uint64_t pa, const uint4& v) {
+        if (pa + 16 <= limit) {
+            st16v<NT>(a.out + pa, u32x4{v.x, v.y, v.z, v.w});
+        } else {   // the tail piece: never write at or past the total / out_cap
+            const uint32_t d[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (uint32_t b = 0; b < 16; ++b)
+                if (pa + b < limit) a.out[pa + b] = (uint8_t)(d[b >> 2] >> (8 * (b & 3)));
+        }
+    };
+    // ---- pass 1: pieces inside one payload ----
+    uint32_t n_edge = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < P; ++k) {
+        const int32_t pr = (int32_t)(k * 1024 + lane * 16);
+        const uint64_t pa = wbase + (uint64_t)pr;
+        const int32_t t = find(pr);
+        const int32_t fp = __shfl(rp, t & 63), fe = __shfl(re, t & 63);
+        const uint32_t sl = __shfl(so_lo, t & 63), sh = __shfl(so_hi, t & 63);
+        const bool inside = t < (int32_t)nl && fp <= pr && pr + 16 <= fe && pa + 16 <= limit;
+        if (inside) {
+            const int64_t sof = (int64_t)((uint64_t)sh << 32 | sl) + (int64_t)pa;
+            const uint4 v = load16_unaligned(a.src, sof, a.src_bytes);
+            st16v<NT>(a.out + pa, u32x4{v.x, v.y, v.z, v.w});
+        }
+        const bool edge = !inside && pa < limit;
+        const uint64_t em = __ballot(edge);
+        if (edge)
+            elist[n_edge + __builtin_amdgcn_mbcnt_hi((uint32_t)(em >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)em, 0u))] =
+                (uint16_t)(k * 64 + lane);
+        n_edge += (uint32_t)__builtin_popcountll(em);
     }
+    if (n_edge == 0) return true;
+    __builtin_amdgcn_wave_barrier();
+    // ---- pass 2: pieces holding headers / frame edges, one per lane ----
     // one frame's contribution to a piece: header bytes from registers, payload by a gather
     auto part = [&](int32_t t, int32_t pr, uint4& acc, bool& ends_inside) {
         const int32_t fo = __shfl(ro, t & 63), fp = __shfl(rp, t & 63), fe = __shfl(re, t & 63);
@@ -241,46 +279,28 @@ __device__ __forceinline__ bool encode_window_lanes(const EncCopyArgs& a, uint32
         }
         ends_inside = fe < pr + 16;
     };
-    uint4 acc[P];
-    bool more = false;
-#pragma unroll
-    for (uint32_t k = 0; k < P; ++k) {
-        const int32_t pr = (int32_t)(k * 1024 + lane * 16);
-        acc[k] = make_uint4(0, 0, 0, 0);
+    for (uint32_t base = 0; base < n_edge; base += 64) {
+        const bool act = base + lane < n_edge;
+        const uint32_t pid = act ? elist[base + lane] : 0u;
+        const int32_t pr = (int32_t)((pid >> 6) * 1024 + (pid & 63) * 16);
+        const int32_t ta = find(pr);
+        uint4 acc = make_uint4(0, 0, 0, 0);
         bool ea, eb;
-        part(ta[k], pr, acc[k], ea);
-        part(ta[k] + 1, pr, acc[k], eb);
-        more |= ea && eb && ta[k] + 2 < (int32_t)nl;
-    }
-    if (__ballot(more)) {   // rare: frames shorter than 16 B -> a third, fourth ... frame in a piece
-#pragma unroll
-        for (uint32_t k = 0; k < P; ++k) {
-            const int32_t pr = (int32_t)(k * 1024 + lane * 16);
-            int32_t t = ta[k] + 2;
-            bool act = true;
-            while (__ballot(act && t < (int32_t)nl)) {
-                const int32_t fo = __shfl(ro, t & 63);
-                act = act && t < (int32_t)nl && fo < pr + 16;
-                uint4 tmp = make_uint4(0, 0, 0, 0);
-                bool e;
-                part(t, pr, tmp, e);
-                if (act) { acc[k].x |= tmp.x; acc[k].y |= tmp.y; acc[k].z |= tmp.z; acc[k].w |= tmp.w; }
-                ++t;
-            }
+        part(ta, pr, acc, ea);
+        part(ta + 1, pr, acc, eb);
+        // rare: frames shorter than 16 B -> a third, fourth ... frame in a piece
+        int32_t t = ta + 2;
+        bool more = act && ea && eb && t < (int32_t)nl;
+        while (__ballot(more)) {
+            const int32_t fo = __shfl(ro, t & 63);
+            more = more && t < (int32_t)nl && fo < pr + 16;
+            uint4 tmp = make_uint4(0, 0, 0, 0);
+            bool e;
+            part(t, pr, tmp, e);
+            if (more) { acc.x |= tmp.x; acc.y |= tmp.y; acc.z |= tmp.z; acc.w |= tmp.w; }
+            ++t;
         }
-    }
-#pragma unroll
-    for (uint32_t k = 0; k < P; ++k) {
-        const uint64_t pa = wbase + k * 1024u + lane * 16u;
-        if (pa >= limit) continue;
-        if (pa + 16 <= limit) {
-            st16v<NT>(a.out + pa, u32x4{acc[k].x, acc[k].y, acc[k].z, acc[k].w});
-        } else {   // the tail piece: never write at or past the total / out_cap
-            const uint32_t d[4] = {acc[k].x, acc[k].y, acc[k].z, acc[k].w};
-#pragma unroll
-            for (uint32_t b = 0; b < 16; ++b)
-                if (pa + b < limit) a.out[pa + b] = (uint8_t)(d[b >> 2] >> (8 * (b & 3)));
-        }
+        if (act) store_piece(wbase + (uint64_t)pr, acc);
     }
     return true;
 }
@@ -292,6 +312,7 @@ template <int NT>
 __global__ __launch_bounds__(256) void k_encode_copy(EncCopyArgs a) {
     constexpr uint32_t P = ENC_WIN / 1024;
     __shared__ u32x4 pm[17];
+    __shared__ uint16_t elist[4][ENC_WIN / 16];   // per wave: the window's edge pieces (pass 2)
     if (threadIdx.x < 17) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -328,7 +349,7 @@ __global__ __launch_bounds__(256) void k_encode_copy(EncCopyArgs a) {
     }
     // general path: frame edges in the window -> lane-parallel frame lookup (serial walk over the
     // frames only when more than 64 of them overlap the window)
-    if (encode_window_lanes<NT>(a, m, wbase, limit, lane, pm)) return;
+    if (encode_window_lanes<NT>(a, m, wbase, limit, lane, pm, elist[threadIdx.x >> 6])) return;
     uint4 acc[P];
 #pragma unroll
     for (uint32_t k = 0; k < P; ++k) acc[k] = make_uint4(0, 0, 0, 0);
