@@ -759,7 +759,7 @@ static int launch_encode(wsc_ctx* c, const wsc_out_msg* msgs, uint32_t n, const 
     ea.lb_agg = c->enc_lb_agg;
     ea.lb_incl = c->enc_lb_incl;
     ea.sticky = c->sticky;
-    const uint32_t sblocks = (n + 255) / 256;
+    const uint32_t sblocks = (n + 256 * ENC_IPT - 1) / (256 * ENC_IPT);
     hipLaunchKernelGGL(k_encode_scan, dim3(sblocks), dim3(256), 0, st, ea);
     HIP_TRY(hipGetLastError());
     EncCopyArgs ca{};

@@ -5,7 +5,7 @@
 // unmasked.  Called per message in the reference by Text/Binary (websocket.go:378-398), pong
 // (websocket_ctrl.go:140-143) and CloseCode (websocket_ctrl.go:108-109).  Here one launch pair
 // frames a whole batch of messages back to back:
-//   k_encode_scan  one lane per message: frame size, block scan + decoupled look-back -> out_off,
+//   k_encode_scan  16 consecutive messages per lane: frame sizes, block scan + look-back -> out_off,
 //                  and the output-window -> first-message index for the copy kernel.
 //   k_encode_copy  one 4 KiB output window per wave, 16 B per lane, 1 KiB per wave instruction:
 //                  a window inside one payload is a shifted stream copy (two aligned loads +
@@ -72,6 +72,8 @@ __device__ __forceinline__ void piece_mask(uint32_t bl, uint32_t bh, uint32_t (&
 // Scan: frame sizes -> out_off (exclusive), window index.  Same look-back protocol as the
 // decoder's walk (wsc_kernels.hip): ticket block ids, agent-scope payload stores drained with
 // vmcnt(0) before the agent-scope flag store, readers poll with agent-scope atomics, bounded spin.
+// ENC_IPT (16) consecutive messages per thread: 1 M messages in 256 blocks instead of 4,096 --
+// the scan went 68 -> 24 us (8 per thread: 28 us, 32: 30 us).
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_encode_scan(EncArgs a) {
     __shared__ uint32_t sh_bid;
@@ -81,14 +83,20 @@ __global__ __launch_bounds__(256) void k_encode_scan(EncArgs a) {
         sh_bid = __hip_atomic_fetch_add(a.lb_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     const uint32_t bid = sh_bid;
-    const uint32_t i = bid * 256 + threadIdx.x;
+    const uint64_t i0 = ((uint64_t)bid * 256 + threadIdx.x) * ENC_IPT;
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint64_t sz = 0;
-    if (i < a.n_msgs) {
-        const uint64_t len = a.msgs[i].len;
-        sz = enc_hlen(len) + len;
+    uint64_t sz[ENC_IPT];
+    uint64_t tsz = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < ENC_IPT; ++j) {
+        sz[j] = 0;
+        if (i0 + j < a.n_msgs) {
+            const uint64_t len = a.msgs[i0 + j].len;
+            sz[j] = enc_hlen(len) + len;
+        }
+        tsz += sz[j];
     }
-    uint64_t inc = sz;
+    uint64_t inc = tsz;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
         const uint64_t o = __shfl_up(inc, d);
@@ -146,16 +154,20 @@ __global__ __launch_bounds__(256) void k_encode_scan(EncArgs a) {
         }
     }
     __syncthreads();
-    const uint64_t off = sh_prefix + wpre + (inc - sz);
-    if (i < a.n_msgs) {
+    uint64_t off = sh_prefix + wpre + (inc - tsz);
+#pragma unroll
+    for (uint32_t j = 0; j < ENC_IPT; ++j) {
+        const uint64_t i = i0 + j;
+        if (i >= a.n_msgs) break;
         a.out_off[i] = off;
         // windows that start inside this frame: [ceil(off / W), floor((off + sz - 1) / W)]
         uint64_t w = (off + ENC_WIN - 1) >> ENC_WIN_SHIFT;
-        uint64_t w_end = ((off + sz - 1) >> ENC_WIN_SHIFT) + 1;
+        uint64_t w_end = ((off + sz[j] - 1) >> ENC_WIN_SHIFT) + 1;
         if (w_end > a.tile_entries) w_end = a.tile_entries;
-        for (; w < w_end; ++w) a.tile[w] = i;
+        for (; w < w_end; ++w) a.tile[w] = (uint32_t)i;
+        off += sz[j];
         if (i == a.n_msgs - 1) {
-            uint64_t total = off + sz;
+            uint64_t total = off;
             if (__hip_atomic_load(a.lb_err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
                 total = ~0ull;   // invalid
                 __hip_atomic_fetch_or(a.sticky, 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

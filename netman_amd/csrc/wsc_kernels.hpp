@@ -159,6 +159,7 @@ struct U8Win {
 // ---- encode (wsc_encode.hip) ----------------------------------------------------------------
 constexpr uint32_t ENC_WIN_SHIFT = 12;                 // 4 KiB output windows
 constexpr uint32_t ENC_WIN = 1u << ENC_WIN_SHIFT;
+constexpr uint32_t ENC_IPT = 16;                       // encode scan: consecutive messages per thread
 
 struct EncArgs {
     const wsc_out_msg* msgs;
