@@ -96,6 +96,54 @@ __global__ __launch_bounds__(256) void xor_pipe2(uint8_t* __restrict__ buf, uint
     }
 }
 
+// COMPACT store pattern: XOR-copy src -> dst + DOFS with 16 B per lane.  SRC_DRIVEN: aligned
+// loads, byte-aligned dwordx4 stores (what k_unmask<COMPACT> does inside a span); otherwise
+// aligned stores of byte-aligned loads (dst-driven).  ALIGN: aligned loads and stores, the
+// realignment done in registers -- each lane funnel-shifts its piece with the previous lane's
+// (DPP row/wave shift through __shfl_up) -- the cost of a register realignment.
+template <int P, int MODE>
+__global__ __launch_bounds__(256) void xor_compact(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                   uint64_t n_win, uint32_t key, uint32_t dofs) {
+    const uint64_t w = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (w >= n_win) return;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t base = w * (1024u * P) + lane * 16u;
+    u32x4 v[P];
+    if (MODE == 0) {   // source-driven: aligned loads, unaligned stores
+#pragma unroll
+        for (int k = 0; k < P; ++k) v[k] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + base + k * 1024u));
+#pragma unroll
+        for (int k = 0; k < P; ++k) {
+            v[k] ^= key;
+            uint8_t* d = dst + dofs + base + k * 1024u;
+            typedef unsigned int u32x4u __attribute__((ext_vector_type(4), aligned(1)));
+            __builtin_nontemporal_store(v[k], reinterpret_cast<u32x4u*>(d));
+        }
+    } else if (MODE == 1) {   // dst-driven: unaligned loads, aligned stores
+        typedef unsigned int u32x4u __attribute__((ext_vector_type(4), aligned(1)));
+#pragma unroll
+        for (int k = 0; k < P; ++k) v[k] = __builtin_nontemporal_load(reinterpret_cast<const u32x4u*>(src + dofs + base + k * 1024u));
+#pragma unroll
+        for (int k = 0; k < P; ++k) __builtin_nontemporal_store(v[k] ^ key, reinterpret_cast<u32x4*>(dst + base + k * 1024u));
+    } else {   // aligned loads and stores, byte shift by dofs & 15 in registers
+        const uint32_t bs = dofs & 3u;   // (a byte shift within a dword: the shape of the cost)
+#pragma unroll
+        for (int k = 0; k < P; ++k) v[k] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + base + k * 1024u));
+#pragma unroll
+        for (int k = 0; k < P; ++k) {
+            // out piece at dst + base (aligned) = src bytes [base - bs, base - bs + 16): the
+            // previous lane's last dword + this piece's first three
+            const uint32_t pw = __shfl_up(v[k].w, 1);
+            u32x4 o;
+            o.x = __builtin_amdgcn_alignbyte(v[k].x, pw, 4 - bs);
+            o.y = __builtin_amdgcn_alignbyte(v[k].y, v[k].x, 4 - bs);
+            o.z = __builtin_amdgcn_alignbyte(v[k].z, v[k].y, 4 - bs);
+            o.w = __builtin_amdgcn_alignbyte(v[k].w, v[k].z, 4 - bs);
+            __builtin_nontemporal_store(o ^ key, reinterpret_cast<u32x4*>(dst + base + k * 1024u));
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void copy16(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, uint64_t n16) {
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (i < n16) reinterpret_cast<float4*>(dst)[i] = reinterpret_cast<const float4*>(src)[i];
@@ -159,6 +207,24 @@ int main(int argc, char** argv) {
     CK(hipMemset(dst, 0, n));
     printf("buffer %llu bytes\n", (unsigned long long)n);
     const double rw = 2.0 * (double)n;
+    if (argc > 2 && argv[2][0] == 'c') {   // COMPACT store patterns: src -> dst at byte offsets
+        const uint64_t nw = n / 4096 - 1;   // (room for the offset)
+        const dim3 g((uint32_t)((nw + 3) / 4));
+        const double b2 = 2.0 * (double)nw * 4096;
+        for (uint32_t d : {0u, 1u, 5u, 13u}) {
+            char name[64];
+            snprintf(name, sizeof name, "src-driven +%u", d);
+            timeit(name, b2, [&] { hipLaunchKernelGGL((xor_compact<4, 0>), g, dim3(256), 0, 0, buf, dst, nw, 0x12345678u, d); });
+            snprintf(name, sizeof name, "dst-driven +%u", d);
+            timeit(name, b2, [&] { hipLaunchKernelGGL((xor_compact<4, 1>), g, dim3(256), 0, 0, buf, dst, nw, 0x12345678u, d); });
+            snprintf(name, sizeof name, "realign +%u", d);
+            timeit(name, b2, [&] { hipLaunchKernelGGL((xor_compact<4, 2>), g, dim3(256), 0, 0, buf, dst, nw, 0x12345678u, d); });
+        }
+        timeit("xor_inplace<4>", rw, [&] {
+            hipLaunchKernelGGL(xor_inplace<4>, dim3((uint32_t)((n / 4096 + 3) / 4)), dim3(256), 0, 0, buf, n / 4096, 0x12345678u);
+        });
+        return 0;
+    }
     if (argc > 2) {   // policy sweep only
         const uint64_t nw = n / 4096;
         const dim3 g((uint32_t)(((nw + 3) / 4 + 7) / 8 * 8));

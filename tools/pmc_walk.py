@@ -19,6 +19,7 @@ CONFIGS = {
     "c11": {"desc": "configs[1] 1 M x 1 KiB BIN, 1 frame/segment", "frames": 1 << 20, "payload": 1 << 30, "hdr": 8},
     "c4": {"desc": "configs[4] 64 Ki fragmented messages (2..16 fragments of 0..8 KiB), COMPACT", "frames": None,
            "payload": None, "hdr": None},
+    "c4i": {"desc": "configs[4]'s batch unmasked in place", "frames": None, "payload": None, "hdr": None},
 }
 SQ_QUAD = ("SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY")   # quad-cycles
 
