@@ -40,6 +40,18 @@ __device__ __forceinline__ uint4 load16_unaligned(const uint8_t* __restrict__ sr
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
+// load16_unaligned with the cache policy of NT bit 0 (non-temporal: a stream read once)
+template <int NT>
+__device__ __forceinline__ uint4 load16u(const uint8_t* __restrict__ src, int64_t off, uint64_t n) {
+    if constexpr ((NT & 1) != 0) {
+        if (off >= 0 && (uint64_t)off + 16 <= n) {
+            const u32x4u_ld t = __builtin_nontemporal_load(reinterpret_cast<const u32x4u_ld*>(src + off));
+            return make_uint4(t.x, t.y, t.z, t.w);
+        }
+    }
+    return load16_unaligned(src, off, n);
+}
+
 template <int NT>
 __device__ __forceinline__ u32x4 ld16v(const uint8_t* p) {
     if constexpr (NT & 1) return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
@@ -93,6 +105,20 @@ __device__ __forceinline__ u32x4 shr_bytes16(u32x4 x, uint32_t sh) {
         o[j] = __builtin_amdgcn_alignbyte(hi, lo, rb);
     }
     return o;
+}
+
+// bytes [g, g + 16) of the 32 bytes x then y, g in [0, 16]: two select levels and an alignbyte per
+// dword (named values, not an array: selects between array elements became a dynamically indexed
+// private array, which the compiler promoted to LDS)
+__device__ __forceinline__ u32x4 funnel16(u32x4 x, u32x4 y, uint32_t g) {
+    const bool c8 = (g & 8) != 0, c4 = (g & 4) != 0;
+    const uint32_t e0 = c8 ? x.z : x.x, e1 = c8 ? x.w : x.y, e2 = c8 ? y.x : x.z;
+    const uint32_t e3 = c8 ? y.y : x.w, e4 = c8 ? y.z : y.x, e5 = c8 ? y.w : y.y;
+    const uint32_t f0 = c4 ? e1 : e0, f1 = c4 ? e2 : e1, f2 = c4 ? e3 : e2, f3 = c4 ? e4 : e3, f4 = c4 ? e5 : e4;
+    const uint32_t b = g & 3;
+    const u32x4 o = {__builtin_amdgcn_alignbyte(f1, f0, b), __builtin_amdgcn_alignbyte(f2, f1, b),
+                     __builtin_amdgcn_alignbyte(f3, f2, b), __builtin_amdgcn_alignbyte(f4, f3, b)};
+    return g >= 16 ? y : o;
 }
 
 // Store bytes [lo, hi) of the 16-byte vector x at p (p = where byte lo goes; 0 <= lo < hi <= 16):

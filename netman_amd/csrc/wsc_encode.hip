@@ -36,22 +36,13 @@ __device__ __forceinline__ void enc_header(uint32_t first_byte, uint64_t len, ui
     h[3] = 0;
 }
 
-// 16 bytes b = 0..15 with b -> h[b - d] (zero outside h's 16 bytes), for d in (-16, 16).
+// 16 bytes b = 0..15 with b -> h[b - d] (zero outside h's 16 bytes), for d in (-16, 16): a funnel
+// of h with zeros (d >= 0: zeros then h from byte 16 - d; d < 0: h from byte -d then zeros)
 __device__ __forceinline__ uint4 enc_place(const uint32_t (&h)[4], int32_t d) {
-    const uint32_t z[12] = {0, 0, 0, 0, h[0], h[1], h[2], h[3], 0, 0, 0, 0};
-    const uint32_t s = (uint32_t)(16 - d);   // byte index in z of output byte 0: 1..31
-    const uint32_t q = s >> 2, rb = s & 3;
-    uint32_t w[5];
-#pragma unroll
-    for (int j = 0; j < 5; ++j) {           // w[j] = z[q + j] without dynamic register indexing
-        uint32_t v = z[j];
-#pragma unroll
-        for (uint32_t t = 1; t < 8; ++t)
-            if (q == t) v = z[t + j];
-        w[j] = v;
-    }
-    return make_uint4(__builtin_amdgcn_alignbyte(w[1], w[0], rb), __builtin_amdgcn_alignbyte(w[2], w[1], rb),
-                      __builtin_amdgcn_alignbyte(w[3], w[2], rb), __builtin_amdgcn_alignbyte(w[4], w[3], rb));
+    const u32x4 H = {h[0], h[1], h[2], h[3]}, Z = {0u, 0u, 0u, 0u};
+    const bool pos = d >= 0;
+    const u32x4 o = funnel16(pos ? Z : H, pos ? H : Z, pos ? (uint32_t)(16 - d) : (uint32_t)(-d));
+    return make_uint4(o.x, o.y, o.z, o.w);
 }
 
 __device__ __forceinline__ uint4 and4(const uint4& v, const uint32_t (&m)[4]) {
@@ -350,11 +341,14 @@ __global__ __launch_bounds__(256) void k_encode_copy(EncCopyArgs a) {
     const uint64_t o = a.out_off[m];
     const uint64_t p0 = o + enc_hlen(mm.len), p1 = p0 + mm.len;
     if (p0 <= wbase && p1 >= wbase + ENC_WIN && wbase + ENC_WIN <= limit) {
-        // fast path: the window lies inside one payload -> shifted stream copy
+        // fast path: the window lies inside one payload -> shifted stream copy, non-temporal loads
+        // (A/B, tools/lib_ab.py: 64 KiB echo batch 0.411 -> 0.396 ms; the lane-parallel windows
+        // keep default loads: their pieces at frame edges re-read lines a neighbour piece loaded,
+        // and nt loads made the 1 KiB batch 3.5 % slower)
         const int64_t so = (int64_t)mm.src_off - (int64_t)p0;
         uint4 v[P];
 #pragma unroll
-        for (uint32_t k = 0; k < P; ++k) v[k] = load16_unaligned(a.src, so + (int64_t)(wbase + k * 1024u + lofs), a.src_bytes);
+        for (uint32_t k = 0; k < P; ++k) v[k] = load16u<NT>(a.src, so + (int64_t)(wbase + k * 1024u + lofs), a.src_bytes);
 #pragma unroll
         for (uint32_t k = 0; k < P; ++k) st16v<NT>(a.out + wbase + k * 1024u + lofs, u32x4{v[k].x, v[k].y, v[k].z, v[k].w});
         return;
