@@ -411,9 +411,10 @@ def config3_dealt(a, torch, dist, K, synth, world, rank, dev, cdev):
     (16 frames per connection segment; 8 M frames = 32 GiB at N = 8) whose segments are dealt
     round-robin to the ranks (shard.assign_segments: segment g -> rank g mod N), so every rank
     decodes its own 1 M-frame, 4 GiB shard -- independent, no collective on the data path.  Each
-    rank runs the headline's pipeline (2 contexts, split walk/unmask streams); the step time is
-    the max over ranks; value = all ranks' payload x steps / that time.  Per-rank times are
-    reported.  torch.distributed is used for the barriers, the max and the gather only."""
+    rank decodes its shard back to back on one stream, two contexts in turn (below: the split
+    pipeline measured slower here); the step time is the max over ranks; value = all ranks'
+    payload x steps / that time.  Per-rank times are reported.  torch.distributed is used for
+    the barriers, the max and the gather only."""
     per_rank, size, fps = 1 << 20, 4096, 16
     cfg = synth.dealt_uniform_batch(per_rank * world, size, fps, seed=synth.SEED_BASE + 3, world=world, rank=rank)
     n_bytes, n_segs, nf = len(cfg["wire"]), len(cfg["seg_off"]) - 1, cfg["n_frames"]
@@ -430,13 +431,23 @@ def config3_dealt(a, torch, dist, K, synth, world, rank, dev, cdev):
         cs.append(c)
         ts.append(t)
         bs.append(c.make_batch(t["wire"], t["seg_off"], None, t["st"], t["so"], t["fr"], t["sm"]))
-    ws = cs[0].stream_create(K.cu_mask(range(min(n_cu // 2, max(16, (n_segs + 255) // 256))), n_cu))
+    # serial decodes on one stream (each context's walk + unmask in turn) by default: with 1 M
+    # frames the walk is 54 us on the whole chip, and beside the unmask (split pipeline) it took
+    # CUs and bandwidth from it -- tools/c3_ab.sh: serial 2,799 GiB/s, split with the walk on
+    # 128 / 48 / 16 CUs 2,685-2,710 / 2,438-2,444 / 2,112-2,129 (WSC_C3_SERIAL=0 and
+    # WSC_C3_WALK_CUS select the split form)
+    walk_cus = int(os.environ.get("WSC_C3_WALK_CUS", "0")) or min(n_cu // 2, max(16, (n_segs + 255) // 256))
+    serial = os.environ.get("WSC_C3_SERIAL", "1") == "1"
+    ws = cs[0].stream_create(K.cu_mask(range(walk_cus), n_cu))
     us = cs[0].stream_create(None)
     n_dec = [0, 0]
 
     def run(k):
         for i in range(k):
-            cs[i % 2].decode_split(bs[i % 2], ws, us)
+            if serial:
+                cs[i % 2].decode(bs[i % 2], us)
+            else:
+                cs[i % 2].decode_split(bs[i % 2], ws, us)
             n_dec[i % 2] += 1
 
     run(a.warmup)
@@ -481,7 +492,8 @@ def config3_dealt(a, torch, dist, K, synth, world, rank, dev, cdev):
             "gib_s": round(cfg["payload_bytes"] * world * a.steps / tmax / 2**30, 1),
             "ms_per_step": round(tmax / a.steps * 1e3, 4),
             "per_rank_ms_per_step": [round(x / a.steps * 1e3, 4) for x in times],
-            "n_gpus": world, "scaling": "weak", "parity_ok": ok}
+            "n_gpus": world, "scaling": "weak", "parity_ok": ok,
+            "mode": "serial decodes on one stream" if serial else f"split pipeline, walk on {walk_cus} CUs"}
 
 
 def other_configs(torch, K, synth, only=None):
