@@ -651,7 +651,8 @@ def other_configs(torch, K, synth, only=None):
 def encode_configs(torch, K, synth):
     """Batched server->client framing (wsc_encode, websocket_ctrl.go:23-70) of the decoded
     payloads of a batch -- the echo path's outbound half: device time (torch events on the launch
-    stream, median of 10) of k_encode_scan + k_encode_copy, algorithmic bytes = payload read +
+    stream around bursts of 20 back-to-back encodes, median of 5) of k_encode_scan +
+    k_encode_copy, algorithmic bytes = payload read +
     frames written + 24 B descriptor + 8 B offset per message."""
     dev = torch.device("cuda", torch.cuda.current_device())
     res = {}
@@ -674,14 +675,20 @@ def encode_configs(torch, K, synth):
         st = torch.cuda.Stream(device=dev)
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         times = []
-        for it in range(13):
+        # back-to-back encodes, as other_configs times decodes: 20 warm-up, then hipEvents around
+        # bursts of 20 (a launch-sync-launch loop left the chip idle between encodes and timed
+        # each one from a cold clock: ~30 us more than the kernel sum at 1 KiB)
+        with torch.cuda.stream(st):
+            for _ in range(20):
+                c.encode(d_msgs, n, src, len(cfg["wire"]), d_out, total + 4096, d_off, st.cuda_stream)
+        for it in range(5):
             with torch.cuda.stream(st):
                 ev[0].record(st)
-                c.encode(d_msgs, n, src, len(cfg["wire"]), d_out, total + 4096, d_off, st.cuda_stream)
+                for _ in range(20):
+                    c.encode(d_msgs, n, src, len(cfg["wire"]), d_out, total + 4096, d_off, st.cuda_stream)
                 ev[1].record(st)
             ev[1].synchronize()
-            if it >= 3:
-                times.append(ev[0].elapsed_time(ev[1]))
+            times.append(ev[0].elapsed_time(ev[1]) / 20)
         ok = int(d_off[-1].item()) == total
         # spot check: the first frame's header + payload and the last frame's payload end
         o = d_out[: 16].cpu().numpy()
