@@ -1613,7 +1613,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
                 u8_restage(sw, cur4, lane);
                 const uint32_t lim = b0 < g.hl ? g.hl : item.len;
                 bool plain;
-                const uint64_t pm = u8_chunk_map<NCH>(T, cur4, mask_at(item, b0), chunk_len(lim, b0 + lane * 64), plain);
+                const uint64_t pm = u8_chunk_map<NCH, U8P_WAVE>(T, cur4, mask_at(item, b0), chunk_len(lim, b0 + lane * 64), plain);
                 const uint64_t wm = u8_wave_map(pm, plain, lane);
                 if (b0 >= g.hl && !mids_in) {   // the first tail step: the windows come before it
                     acc = u8m_then(acc, mids);
@@ -1693,7 +1693,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
             u8_restage(sw, qc, lane);
             const uint32_t off = (lane & 15) * 64;
             bool plain;
-            const uint64_t pm = u8_chunk_map<NCH>(T, qc, a.unmasked ? 0u : rmask, chunk_len(rlen, off), plain);
+            const uint64_t pm = u8_chunk_map<NCH, U8P_LANE>(T, qc, a.unmasked ? 0u : rmask, chunk_len(rlen, off), plain);
             const uint64_t rm = u8_row_maps(pm, lane);
             if (un < n_units) {
                 nsmall = unit_small(xn);

@@ -129,7 +129,13 @@ __device__ __forceinline__ void u8_restage(uint4* sw, V (&q)[4], uint32_t lane) 
 // byte from the 8-byte rows of `tab`); every entry state that survives them is then in one state
 // X, which steps through the other 60 bytes one byte-table read each (`tab8[X][byte]`, state 8 =
 // reject, absorbing): two VALU ops and one LDS read per byte.
-template <uint32_t NCH, typename V>
+// How a wave folds chunks that end early (the last of an item):
+enum U8Part : uint32_t {
+    U8P_LANE = 0,   // the partial chunk's lane alone folds it byte by byte with full maps
+    U8P_WAVE = 1,   // the whole wave takes the chain steps predicated on each byte being valid
+    U8P_NONE = 2,   // the caller's chunks are always whole (the unmask's window fold)
+};
+template <uint32_t NCH, U8Part PART, typename V>
 __device__ __forceinline__ uint64_t u8_chunk_map(const U8Lds& t, const V (&v)[4], uint32_t mask, uint32_t nk,
                                                  bool& plain) {
     // byte i of the chunk, unmasked (i constant after unrolling)
@@ -147,19 +153,14 @@ __device__ __forceinline__ uint64_t u8_chunk_map(const U8Lds& t, const V (&v)[4]
             hib |= dw(j) & keep & 0x80808080u;
         }
     }
-    plain = true;
-    if (nk == 0) return u8m_id();
-    if (hib == 0) return u8m_ascii();
-    plain = false;
-    // Every entry state that survives the first 4 bytes is in ONE state X there: a survivor
-    // must be in state 0 just before the first lead byte (a lead in a non-zero state rejects),
-    // and 4 continuation bytes reject every state (at most 3 are owed).  So the first 4 bytes
-    // compose full maps, the others step the single state X, and the chunk's map is the
-    // prefix map with every surviving entry sent to the final state.  A partial chunk (the
-    // last of an item) folds its bytes with full maps instead: its map must leave a
-    // character that the item ends inside owed, not rejected by padding.
-    uint32_t lo = 0x03020100u, hi = 0x07060504u;
-    if (nk < 64) {   // (unrolled with a guard: a dynamic index into the chunk would go to scratch)
+    plain = nk == 0 || hib == 0;
+    // nothing to fold / ASCII only (a function: not kept live across the fold)
+    auto trivial = [nk]() -> uint64_t { return nk == 0 ? u8m_id() : u8m_ascii(); };
+    if (PART == U8P_LANE && plain) return trivial();
+    if (__ballot(!plain) == 0) return trivial();
+    if (PART == U8P_LANE && nk < 64) {
+        // (unrolled with a guard: a dynamic index into the chunk would go to scratch)
+        uint32_t lo = 0x03020100u, hi = 0x07060504u;
 #pragma unroll
         for (uint32_t i = 0; i < 64; ++i) {
             if (i < nk) {
@@ -171,9 +172,21 @@ __device__ __forceinline__ uint64_t u8_chunk_map(const U8Lds& t, const V (&v)[4]
         }
         return (uint64_t)hi << 32 | lo;
     }
-    // NCH independent chains of 64 / NCH bytes, interleaved byte by byte (latency: each chain
-    // is a dependent sequence of LDS reads), composed in order at the end
-    constexpr uint32_t CW = 16 / NCH;     // dwords per chain
+    // Every entry state that survives the first 4 bytes is in ONE state X there: a survivor
+    // must be in state 0 just before the first lead byte (a lead in a non-zero state rejects),
+    // and 4 continuation bytes reject every state (at most 3 are owed).  So the first 4 bytes
+    // compose full maps, the others step the single state X, and the chunk's map is the
+    // prefix map with every surviving entry sent to the final state.  NCH independent chains of
+    // 64 / NCH bytes, interleaved byte by byte (latency: each chain is a dependent sequence of
+    // LDS reads), are composed in order at the end.
+    // A partial chunk's map must leave a character that the item ends inside owed, not rejected
+    // by padding.  U8P_LANE: that lane folded it above, byte by byte, and the wave runs both
+    // forms.  U8P_WAVE: the wave folds all its chunks one way -- the chain steps predicated on
+    // the byte being valid as soon as one chunk is partial, a chain with at most 4 valid bytes
+    // keeping its full-map composition (cheaper where few waves hold a partial chunk: 64 KiB
+    // items; dearer where most do: 1 KiB items).
+    const bool part = PART == U8P_WAVE && __ballot(!plain && nk < 64) != 0;
+    constexpr uint32_t CW = 16 / NCH, CB = 4 * CW;   // dwords / bytes per chain
     uint32_t clo[NCH], chi[NCH], st[NCH];
 #pragma unroll
     for (uint32_t c = 0; c < NCH; ++c) {
@@ -183,8 +196,11 @@ __device__ __forceinline__ uint64_t u8_chunk_map(const U8Lds& t, const V (&v)[4]
         for (uint32_t i = 0; i < 4; ++i) {
             const uint64_t e = t.tab[(d0 >> (8 * i)) & 0xFFu];
             const uint32_t tl = (uint32_t)e, th = (uint32_t)(e >> 32);
-            l = (uint32_t)__builtin_amdgcn_perm(th, tl, l);
-            h = (uint32_t)__builtin_amdgcn_perm(th, tl, h);
+            const uint32_t l2 = (uint32_t)__builtin_amdgcn_perm(th, tl, l);
+            const uint32_t h2 = (uint32_t)__builtin_amdgcn_perm(th, tl, h);
+            const bool take = !part || c * CB + i < nk;
+            l = take ? l2 : l;
+            h = take ? h2 : h;
         }
         uint32_t x = l & h;             // non-rejected bytes all equal X, rejects are 0xFF
         x &= x >> 16;
@@ -201,19 +217,25 @@ __device__ __forceinline__ uint64_t u8_chunk_map(const U8Lds& t, const V (&v)[4]
 #pragma unroll
         for (uint32_t i = 0; i < 4; ++i) {
 #pragma unroll
-            for (uint32_t c = 0; c < NCH; ++c)
-                st[c] = t.tab8[__builtin_amdgcn_perm(st[c], dw(c * CW + j), i | 4u << 8 | 0x0Cu << 16 | 0x0Cu << 24)];
+            for (uint32_t c = 0; c < NCH; ++c) {
+                const uint32_t ns = t.tab8[__builtin_amdgcn_perm(st[c], dw(c * CW + j), i | 4u << 8 | 0x0Cu << 16 | 0x0Cu << 24)];
+                st[c] = (!part || c * CB + 4 * j + i < nk) ? ns : st[c];
+            }
         }
     }
     uint64_t m = u8m_id();
 #pragma unroll
     for (uint32_t c = 0; c < NCH; ++c) {
         const uint32_t fr = (st[c] > 7 ? 0xFFu : st[c]) * 0x01010101u;
-        const uint32_t l = (uint32_t)__builtin_amdgcn_perm(fr, fr, clo[c]);   // 0..7 -> final state
-        const uint32_t h = (uint32_t)__builtin_amdgcn_perm(fr, fr, chi[c]);
+        uint32_t l = (uint32_t)__builtin_amdgcn_perm(fr, fr, clo[c]);   // 0..7 -> final state
+        uint32_t h = (uint32_t)__builtin_amdgcn_perm(fr, fr, chi[c]);
+        if (part && nk <= c * CB + 4) {   // (at most 4 bytes: the composed map itself)
+            l = clo[c];
+            h = chi[c];
+        }
         m = c == 0 ? ((uint64_t)h << 32 | l) : u8m_then(m, (uint64_t)h << 32 | l);
     }
-    return m;
+    return plain ? trivial() : m;
 }
 
 }  // namespace wsc

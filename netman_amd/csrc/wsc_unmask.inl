@@ -374,7 +374,7 @@ __device__ __forceinline__ void fold_staged(const u32x4* v, uint32_t key, U8Win 
         }
         __builtin_amdgcn_wave_barrier();
         bool plain;
-        const uint64_t pm = u8_chunk_map<2>(b.t, q, 0u, 64u, plain);
+        const uint64_t pm = u8_chunk_map<2, U8P_NONE>(b.t, q, 0u, 64u, plain);
         m = u8m_then(m, u8_wave_map(pm, plain, lane));
     }
     if (lane == 0) {
