@@ -229,7 +229,10 @@ __device__ __forceinline__ uint4 rec_pack(const wsc_frame& fr, uint64_t seg_star
 // speculative header is used only when its address is the real next position, so results never
 // depend on the guess; frames that repeat their size (the common case on one connection) cost
 // one round trip per SPEC_D frames.  All loads of a round are waited together.
-template <bool EMIT, bool COMPACT, uint32_t LS = 64, int SPEC_D = 4, bool PURE = false>
+#ifndef WSC_WALK_SPEC
+#define WSC_WALK_SPEC 4
+#endif
+template <bool EMIT, bool COMPACT, uint32_t LS = 64, int SPEC_D = WSC_WALK_SPEC, bool PURE = false>
 __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, const SegCount& base,
                                                  const SegCount& own, uint4* lrec, WalkEnd* wend,
                                                  uint4* lrec2 = nullptr, uint32_t cap = 0, uint32_t tag = 0) {
