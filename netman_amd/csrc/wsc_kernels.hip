@@ -956,7 +956,7 @@ __global__ __launch_bounds__(256) void k_walk_emit(WalkArgs a) {
 // segments per walking lane), KR frame records per walking lane; every lane emits
 template <bool COMPACT, uint32_t KR, uint32_t NT, uint32_t G, uint32_t WL = NT>
 struct WalkLds {
-    static_assert(WL % 64 == 0 && WL <= NT && WL <= 256, "walking lanes: whole waves, owner is a byte");
+    static_assert(WL % 16 == 0 && WL <= NT && WL <= 256, "walking lanes: whole 16-lane rows, owner is a byte");
     SegCount prefix;
     SegCount wave[NT / 64];
     uint32_t wtot[NT / 64];
@@ -1761,6 +1761,10 @@ template __global__ void k_u8_check<4>(U8Args);
 // explicit instantiations used by the host code: 16 frame records per lane, one segment per
 // lane, blocks of 64 or 256 lanes; batches of more segments use the three-launch walk below
 template __global__ void k_walk_fused<false, 16, 64, 1, 64>(WalkArgs);
+template __global__ void k_walk_fused<false, 16, 64, 1, 16>(WalkArgs);
+template __global__ void k_walk_fused<true, 16, 64, 1, 16>(WalkArgs);
+template __global__ void k_walk_fused<false, 16, 64, 1, 32>(WalkArgs);
+template __global__ void k_walk_fused<true, 16, 64, 1, 32>(WalkArgs);
 template __global__ void k_walk_fused<true, 16, 64, 1, 64>(WalkArgs);
 template __global__ void k_walk_fused<false, 16, 256, 1, 256>(WalkArgs);
 template __global__ void k_walk_fused<true, 16, 256, 1, 256>(WalkArgs);
