@@ -15,7 +15,7 @@
 #include "wsc_kernels.hpp"
 
 namespace wsc {
-template <bool COMPACT, uint32_t KR, uint32_t NT, uint32_t G, uint32_t WL> __global__ void k_walk_fused(WalkArgs);
+template <bool COMPACT, uint32_t KR, uint32_t NT, uint32_t G, uint32_t WL, uint32_t SPREAD> __global__ void k_walk_fused(WalkArgs);
 template <bool COMPACT, uint32_t KR, uint32_t NT> __global__ void k_walk_tiled(WalkArgs, uint32_t);
 template <bool COMPACT> __global__ void k_walk_count(WalkArgs);
 __global__ void k_walk_scan(WalkArgs, uint32_t);
@@ -103,7 +103,7 @@ struct wsc_ctx {
     bool walk_tiled = true;             // WSC_WALK_TILED=0: the three-launch walk for mode 3 (A/B)
     bool ab_no_u8 = false;              // WSC_AB_NO_U8=1: A/B timing only -- binary unmask, no UTF-8 launches
                                         // (wrong for text batches; never set in tests or the bench)
-    int walk_mode = 0;                  // WSC_WALK_MODE: 16, 32, 64, 65, 256 or 3 pins the walk geometry (A/B, tests); 0 = auto
+    int walk_mode = 0;                  // WSC_WALK_MODE: 16, 32, 64, 65, 66, 256 or 3 pins the walk geometry (A/B, tests); 0 = auto
     uint32_t walk_used = 0;             // geometry (64 / 256 / 3) and block count of the last walk launched:
     uint32_t walk_blocks = 0;           // the staged unmask re-arms exactly that walk's look-back flags
     uint32_t max_walk_blocks = 0;       // look-back state allocated for this many walk blocks
@@ -315,9 +315,9 @@ int wsc_create(int device, const wsc_config* cfg_in, wsc_ctx** out) {
     if (const char* e = std::getenv("WSC_U8_GRID"); e && *e) c->u8_grid = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("WSC_AB_NO_U8"); e && e[0] == '1') c->ab_no_u8 = true;
     if (const char* e = std::getenv("WSC_WALK_TILED"); e && e[0] == '0') c->walk_tiled = false;
-    if (const char* e = std::getenv("WSC_WALK_MODE"); e && *e) {   // pin a walk geometry (tests, A/B): 16, 32, 64, 65, 256 or 3
+    if (const char* e = std::getenv("WSC_WALK_MODE"); e && *e) {   // pin a walk geometry (tests, A/B): 16, 32, 64, 65, 66, 256 or 3
         const int m = std::atoi(e);
-        c->walk_mode = (m == 16 || m == 32 || m == 64 || m == 65 || m == 256 || m == 3) ? m : 0;
+        c->walk_mode = (m == 16 || m == 32 || m == 64 || m == 65 || m == 66 || m == 256 || m == 3) ? m : 0;
     }
     if (const char* e = std::getenv("WSC_U8_INLINE_MAX"); e && *e)   // test knob: 0 sends all text chip-wide
         c->u8_inline_max = (uint32_t)std::strtoul(e, nullptr, 10);
@@ -445,7 +445,7 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     // fewer flags and leave stale inclusive prefixes for the next walk)
     const uint32_t mode = phase == 2 && c->walk_used ? c->walk_used : walk_mode(c, n, stream_cus(c, split ? sw : st));
     const uint32_t wnt = (mode == 64 || mode == 16 || mode == 32) ? 64u : 256u;
-    const uint32_t spb = mode == 65 ? 64u : (mode == 16 || mode == 32) ? mode : wnt;   // segments per walk block
+    const uint32_t spb = (mode == 65 || mode == 66) ? 64u : (mode == 16 || mode == 32) ? mode : wnt;   // segments per walk block
     const dim3 wblk(wnt), wgrid((n + spb - 1) / spb);
     if (phase != 2) {
         c->walk_used = mode;
@@ -484,17 +484,19 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
         if (compact) hipLaunchKernelGGL((k_walk_emit<true>), wgrid, wblk, 0, ws, wa);
         else hipLaunchKernelGGL((k_walk_emit<false>), wgrid, wblk, 0, ws, wa);
     } else if (compact) {
-        if (mode == 65) hipLaunchKernelGGL((k_walk_fused<true, 16, 256, 1, 64>), wgrid, wblk, 0, ws, wa);
-        else if (mode == 16) hipLaunchKernelGGL((k_walk_fused<true, 16, 64, 1, 16>), wgrid, wblk, 0, ws, wa);
-        else if (mode == 32) hipLaunchKernelGGL((k_walk_fused<true, 16, 64, 1, 32>), wgrid, wblk, 0, ws, wa);
-        else if (wnt == 64) hipLaunchKernelGGL((k_walk_fused<true, 16, 64, 1, 64>), wgrid, wblk, 0, ws, wa);
-        else hipLaunchKernelGGL((k_walk_fused<true, 16, 256, 1, 256>), wgrid, wblk, 0, ws, wa);
+        if (mode == 65) hipLaunchKernelGGL((k_walk_fused<true, 16, 256, 1, 64, 0>), wgrid, wblk, 0, ws, wa);
+        else if (mode == 66) hipLaunchKernelGGL((k_walk_fused<true, 16, 256, 1, 64, 16>), wgrid, wblk, 0, ws, wa);
+        else if (mode == 16) hipLaunchKernelGGL((k_walk_fused<true, 16, 64, 1, 16, 0>), wgrid, wblk, 0, ws, wa);
+        else if (mode == 32) hipLaunchKernelGGL((k_walk_fused<true, 16, 64, 1, 32, 0>), wgrid, wblk, 0, ws, wa);
+        else if (wnt == 64) hipLaunchKernelGGL((k_walk_fused<true, 16, 64, 1, 64, 0>), wgrid, wblk, 0, ws, wa);
+        else hipLaunchKernelGGL((k_walk_fused<true, 16, 256, 1, 256, 0>), wgrid, wblk, 0, ws, wa);
     } else {
-        if (mode == 65) hipLaunchKernelGGL((k_walk_fused<false, 16, 256, 1, 64>), wgrid, wblk, 0, ws, wa);
-        else if (mode == 16) hipLaunchKernelGGL((k_walk_fused<false, 16, 64, 1, 16>), wgrid, wblk, 0, ws, wa);
-        else if (mode == 32) hipLaunchKernelGGL((k_walk_fused<false, 16, 64, 1, 32>), wgrid, wblk, 0, ws, wa);
-        else if (wnt == 64) hipLaunchKernelGGL((k_walk_fused<false, 16, 64, 1, 64>), wgrid, wblk, 0, ws, wa);
-        else hipLaunchKernelGGL((k_walk_fused<false, 16, 256, 1, 256>), wgrid, wblk, 0, ws, wa);
+        if (mode == 65) hipLaunchKernelGGL((k_walk_fused<false, 16, 256, 1, 64, 0>), wgrid, wblk, 0, ws, wa);
+        else if (mode == 66) hipLaunchKernelGGL((k_walk_fused<false, 16, 256, 1, 64, 16>), wgrid, wblk, 0, ws, wa);
+        else if (mode == 16) hipLaunchKernelGGL((k_walk_fused<false, 16, 64, 1, 16, 0>), wgrid, wblk, 0, ws, wa);
+        else if (mode == 32) hipLaunchKernelGGL((k_walk_fused<false, 16, 64, 1, 32, 0>), wgrid, wblk, 0, ws, wa);
+        else if (wnt == 64) hipLaunchKernelGGL((k_walk_fused<false, 16, 64, 1, 64, 0>), wgrid, wblk, 0, ws, wa);
+        else hipLaunchKernelGGL((k_walk_fused<false, 16, 256, 1, 256, 0>), wgrid, wblk, 0, ws, wa);
     }
     HIP_TRY(hipGetLastError());
     if (split) HIP_TRY(hipEventRecord(c->ev_walked, ws));

@@ -1111,18 +1111,20 @@ __device__ __forceinline__ SegCount block_lookback(const WalkArgs& a, uint32_t b
 // seg0 + o * G; lanes from WL on only take part in the cooperative emit.
 template <bool COMPACT, uint32_t KR, uint32_t NT, uint32_t G, uint32_t WL>
 __device__ __forceinline__ void tile_emit(const WalkArgs& a, WalkLds<COMPACT, KR, NT, G, WL>& L, const SegCount& lb,
-                                          uint32_t nrec, uint32_t seg0, uint32_t seg_lim, uint32_t lane) {
+                                          uint32_t nrec, uint32_t seg0, uint32_t seg_lim, uint32_t lane,
+                                          uint32_t col = ~0u) {
     constexpr uint32_t NW = NT / 64;
     const uint32_t wl = lane & 63, wave = lane >> 6;
-    const uint32_t s0 = seg0 + lane * G;
-    const bool walker = lane < WL;
+    if (col == ~0u) col = lane;   // the walking lane's column (its segments, LDS records); physical lane by default
+    const uint32_t s0 = seg0 + col * G;
+    const bool walker = col < WL;
     const SegCount zero = {};
     // ---- per segment bases ----
     if (walker) {
         uint32_t fb = lb.frames, sb = lb.spans0 + lb.spans1;
         uint64_t ab = lb.bytes0 + lb.bytes1;
         for (uint32_t j = 0; j < G; ++j) {
-            const uint32_t q = j * WL + lane;
+            const uint32_t q = j * WL + col;
             const uint32_t s = s0 + j;
             const uint32_t fl = L.fbase[q];
             if (s < seg_lim && (fl & SEGF_U8DEFER)) {
@@ -1157,8 +1159,8 @@ __device__ __forceinline__ void tile_emit(const WalkArgs& a, WalkLds<COMPACT, KR
         if (w < wave) rpre += L.wtot[w];
         F += L.wtot[w];
     }
-    if (walker) L.rpre[lane] = rpre;
-    for (uint32_t k = 0; k < nrec; ++k) L.owner[rpre + k] = (uint8_t)lane;
+    if (walker) L.rpre[col] = rpre;
+    for (uint32_t k = 0; k < nrec; ++k) L.owner[rpre + k] = (uint8_t)col;
     __syncthreads();
     // ---- cooperative emit ----
     const uint32_t W = 1u << a.win_shift;
@@ -1224,7 +1226,7 @@ __device__ __forceinline__ void tile_emit(const WalkArgs& a, WalkLds<COMPACT, KR
     for (uint32_t j = 0; j < G && walker; ++j) {
         const uint32_t s = s0 + j;
         if (s >= seg_lim) break;
-        const uint32_t q = j * WL + lane;
+        const uint32_t q = j * WL + col;
         const uint64_t se = a.seg_off[s + 1];
         if (L.rep[q]) {
             const uint64_t Wd = W;   // windows that start after the last span, up to the segment end
@@ -1280,8 +1282,11 @@ __device__ __forceinline__ void write_summary(const WalkArgs& a, const SegCount&
 // come from a ticket counter in dispatch order, so every block a block waits for has already
 // started.  Flags and the ticket are zeroed by k_unmask (the next launch on the stream) of every
 // decode, and at context creation.
-template <bool COMPACT, uint32_t KR, uint32_t NT, uint32_t G, uint32_t WL>
+// SPREAD (> 0): the WL walking columns are spread SPREAD per wave over WL / SPREAD waves, so several
+// SIMDs issue the header chains (same blocks, same look-back as SPREAD = 0).
+template <bool COMPACT, uint32_t KR, uint32_t NT, uint32_t G, uint32_t WL, uint32_t SPREAD>
 __global__ __launch_bounds__(NT) void k_walk_fused(WalkArgs a) {
+    static_assert(SPREAD == 0 || (WL % SPREAD == 0 && WL / SPREAD <= NT / 64 && SPREAD <= 64), "spread geometry");
     __shared__ uint32_t sh_bid;
     __shared__ WalkLds<COMPACT, KR, NT, G, WL> L;
     const uint32_t lane = threadIdx.x, wl = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1292,7 +1297,9 @@ __global__ __launch_bounds__(NT) void k_walk_fused(WalkArgs a) {
     uint64_t t0 = 0, t1 = 0, t2 = 0;
     if (a.dbg && lane == 0) t0 = __builtin_amdgcn_s_memrealtime();
     uint32_t nrec;
-    const SegCount tot = tile_count<COMPACT, KR, NT, G>(a, L, (bid * WL + lane) * G, a.n_segs, lane, nrec);
+    // walking column: in lane order, so the block scan over physical lanes stays in segment order
+    const uint32_t col = SPREAD == 0 ? lane : (wl < SPREAD && wave < WL / (SPREAD ? SPREAD : 1)) ? wave * SPREAD + wl : WL + lane;
+    const SegCount tot = tile_count<COMPACT, KR, NT, G>(a, L, (bid * WL + col) * G, a.n_segs, col, nrec);
     SegCount btot;
     const SegCount excl = tile_scan<NT>(tot, L, wl, wave, btot);
     if (wave == 0) {
@@ -1302,7 +1309,7 @@ __global__ __launch_bounds__(NT) void k_walk_fused(WalkArgs a) {
     }
     __syncthreads();
     if (a.dbg && lane == 0) t2 = __builtin_amdgcn_s_memrealtime();
-    tile_emit<COMPACT, KR, NT, G>(a, L, sc_add(L.prefix, excl), nrec, bid * WL * G, a.n_segs, lane);
+    tile_emit<COMPACT, KR, NT, G>(a, L, sc_add(L.prefix, excl), nrec, bid * WL * G, a.n_segs, lane, col);
     if (a.dbg) {   // diagnostic timestamps (100 MHz s_memrealtime), written only to the dbg buffer
         __syncthreads();
         if (lane == 0) {
@@ -1760,16 +1767,18 @@ template __global__ void k_u8_check<4>(U8Args);
 
 // explicit instantiations used by the host code: 16 frame records per lane, one segment per
 // lane, blocks of 64 or 256 lanes; batches of more segments use the three-launch walk below
-template __global__ void k_walk_fused<false, 16, 64, 1, 64>(WalkArgs);
-template __global__ void k_walk_fused<false, 16, 64, 1, 16>(WalkArgs);
-template __global__ void k_walk_fused<true, 16, 64, 1, 16>(WalkArgs);
-template __global__ void k_walk_fused<false, 16, 64, 1, 32>(WalkArgs);
-template __global__ void k_walk_fused<true, 16, 64, 1, 32>(WalkArgs);
-template __global__ void k_walk_fused<true, 16, 64, 1, 64>(WalkArgs);
-template __global__ void k_walk_fused<false, 16, 256, 1, 256>(WalkArgs);
-template __global__ void k_walk_fused<true, 16, 256, 1, 256>(WalkArgs);
-template __global__ void k_walk_fused<false, 16, 256, 1, 64>(WalkArgs);
-template __global__ void k_walk_fused<true, 16, 256, 1, 64>(WalkArgs);
+template __global__ void k_walk_fused<false, 16, 64, 1, 64, 0>(WalkArgs);
+template __global__ void k_walk_fused<false, 16, 64, 1, 16, 0>(WalkArgs);
+template __global__ void k_walk_fused<true, 16, 64, 1, 16, 0>(WalkArgs);
+template __global__ void k_walk_fused<false, 16, 64, 1, 32, 0>(WalkArgs);
+template __global__ void k_walk_fused<true, 16, 64, 1, 32, 0>(WalkArgs);
+template __global__ void k_walk_fused<true, 16, 64, 1, 64, 0>(WalkArgs);
+template __global__ void k_walk_fused<false, 16, 256, 1, 256, 0>(WalkArgs);
+template __global__ void k_walk_fused<true, 16, 256, 1, 256, 0>(WalkArgs);
+template __global__ void k_walk_fused<false, 16, 256, 1, 64, 0>(WalkArgs);
+template __global__ void k_walk_fused<true, 16, 256, 1, 64, 0>(WalkArgs);
+template __global__ void k_walk_fused<false, 16, 256, 1, 64, 16>(WalkArgs);
+template __global__ void k_walk_fused<true, 16, 256, 1, 64, 16>(WalkArgs);
 template __global__ void k_walk_tiled<false, 4, 256>(WalkArgs, uint32_t);
 template __global__ void k_walk_tiled<true, 4, 256>(WalkArgs, uint32_t);
 template __global__ void k_walk_count<false>(WalkArgs);

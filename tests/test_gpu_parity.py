@@ -62,13 +62,15 @@ def test_fuzz_single_batch(codec, compact):
 
 
 @pytest.mark.parametrize("compact,mode", [(False, 3), (True, 3), (False, 256), (True, 256), (False, 64), (True, 64),
-                                          (False, 65), (True, 65), (False, 16), (True, 16), (False, 32), (True, 32)])
+                                          (False, 65), (True, 65), (False, 16), (True, 16), (False, 32), (True, 32),
+                                          (False, 66), (True, 66)])
 def test_fuzz_walk_geometries(codec_lib, monkeypatch, compact, mode):
     """Every walk geometry forced on the same fuzz batches (5..44 units with text and errors, and
     1..6 units): the fused walk with 64- and 256-lane blocks (16 LDS records per lane, longer
     segments re-walked, the rest emitted cooperatively), 256-lane blocks whose first wave walks and
     all four emit (mode 65), 64-lane blocks whose first 16 / 32 lanes walk (modes 16, 32: several
-    walking waves per CU), and the tiled walk for many segments (mode 3)."""
+    walking waves per CU), 256-lane blocks whose 64 walking columns are spread 16 per wave (mode
+    66), and the tiled walk for many segments (mode 3)."""
     monkeypatch.setenv("WSC_WALK_MODE", str(mode))
     c = K.Codec(0, max_batch_bytes=64 << 20, max_segs=1 << 14, max_frames=1 << 18)
     try:
