@@ -229,8 +229,12 @@ __device__ __forceinline__ uint4 rec_pack(const wsc_frame& fr, uint64_t seg_star
 // speculative header is used only when its address is the real next position, so results never
 // depend on the guess; frames that repeat their size (the common case on one connection) cost
 // one round trip per SPEC_D frames.  All loads of a round are waited together.
+// Depth 2 by default: the chain of one walking wave per CU is bound by its own instruction
+// latency (one wave per SIMD, nothing to interleave), and the header queue's register shifts grow
+// with the depth -- measured (profiles/r03_walk_spec_ab*.log): configs[4] walk 76 -> 61 us,
+// configs[2] 34.7 -> 33.7 us at depth 2 vs 4; 8 and 16 are slower still.
 #ifndef WSC_WALK_SPEC
-#define WSC_WALK_SPEC 4
+#define WSC_WALK_SPEC 2
 #endif
 template <bool EMIT, bool COMPACT, uint32_t LS = 64, int SPEC_D = WSC_WALK_SPEC, bool PURE = false>
 __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, const SegCount& base,
