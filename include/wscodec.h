@@ -28,8 +28,10 @@
 extern "C" {
 #endif
 
-#define WSC_ABI_VERSION 3   /* 2: wsc_frame.payload_len_hi (40-bit payload lengths), staged split;
-                               3: payloads streamed across batches (wsc_conn_state.frame_*, WSC_FK_PIECE) */
+#define WSC_ABI_VERSION 4   /* 2: wsc_frame.payload_len_hi (40-bit payload lengths), staged split;
+                               3: payloads streamed across batches (wsc_conn_state.frame_*, WSC_FK_PIECE);
+                               4: PONG payloads stream too (wsc_conn_state.frame_utf8), session EOF,
+                                  no-progress guard and per-connection message cap */
 
 /* ---- return codes --------------------------------------------------------------------------- */
 #define WSC_OK 0
@@ -53,6 +55,13 @@ extern "C" {
 #define WSC_ERR_TOO_LARGE 7              /* payload > max_frame_len (reference would panic, Q4) -> 1002 */
 #define WSC_ERR_DEVICE 8                 /* session only: the connection's batch hit a device error
                                             -> CloseCode(1011); see wsc_session_* below           */
+#define WSC_ERR_NO_PROGRESS 9            /* session only: a whole batch of the connection's bytes decoded
+                                            nothing (a header or PING/CLOSE frame longer than
+                                            max_batch_bytes, which must be >= 139 to rule it out)
+                                            -> CloseCode(1009) instead of re-sending it forever    */
+#define WSC_ERR_MSG_TOO_BIG 10           /* session only: the connection's buffered message passed the
+                                            cap set by wsc_session_set_max_message (off by default:
+                                            the reference has none, Q4) -> CloseCode(1009)          */
 
 /* ---- what the decoder did with a frame (websocket.go:136-208 / websocket_frame.go:52-102) --- */
 #define WSC_FK_FRAG 0        /* FIN=0 through nextFrame: payload appended to continueBuffer      */
@@ -63,20 +72,25 @@ extern "C" {
 #define WSC_FK_PONG_EMPTY 5  /* PONG without payload: Close() (websocket.go:198-201)             */
 #define WSC_FK_ERROR 6       /* sentinel `err` at this frame: CloseCode(1002|1007)               */
 #define WSC_FK_STALL 7       /* unmasked client frame: reference returns EAGAIN forever (Q3)     */
-#define WSC_FK_PIECE 8       /* the payload bytes of a data frame that is not complete at the end of
-                                its segment (nextFrame's partial read into rBuffer,
+#define WSC_FK_PIECE 8       /* the payload bytes of a data frame or PONG that is not complete at the
+                                end of its segment (nextFrame's partial read into rBuffer,
                                 websocket_frame.go:16-31): unmasked, nothing delivered yet.  The
                                 frame continues in the connection's next segment (state_out.frame_*);
-                                its last piece carries the frame's real kind (MESSAGE or FRAG) */
+                                its last piece carries the frame's real kind (MESSAGE, FRAG or PONG) */
 
-/* Streaming (ABI 3).  A data frame (opcode 0/1/2) whose header is complete is consumed as its
+/* Streaming (ABI 3; PONG since ABI 4).  A data frame (opcode 0/1/2) or a PONG -- the reference puts
+ * no size limit on a PONG and accumulates its payload over reads like any frame's
+ * (websocket.go:191-205, websocket_frame.go:16-31) -- whose header is complete is consumed as its
  * payload arrives: each batch unmasks the bytes it holds and records them (WSC_FK_PIECE, then the
  * final kind on the piece that completes the frame), and the connection carries only
  * {frame_rem, frame_mask, frame_hdr, frame_len} -- never the payload -- to its next segment, which
  * starts with the rest of that payload.  A record whose header lay in an earlier batch has
  * WSC_FF_HEAD_PREV, hdr_len 0 and hdr_off = its first payload byte; its `mask` is phased to that
- * byte.  The frame's data is the concatenation of its pieces' payloads, in order.  Control frames
- * (<= 125 B) and incomplete headers are still carried whole (seg_result.consumed stops before them). */
+ * byte.  The frame's data is the concatenation of its pieces' payloads, in order.  A PONG's pieces go
+ * to the control region in COMPACT mode; under messageMode TEXT the PONG payload alone is UTF-8
+ * checked when its last piece arrives (Q6), its DFA state carried in frame_utf8.  PING and CLOSE
+ * frames (<= 125 B by rule) and incomplete headers are still carried whole (seg_result.consumed
+ * stops before them: at most 139 bytes).                                                         */
 
 /* wsc_frame.flags */
 #define WSC_FF_UNMASKED 0x01  /* payload went through nextFrame and was XOR-unmasked             */
@@ -113,8 +127,11 @@ typedef struct wsc_conn_state {
                               byte starts a header (websocket_frame.go:16 rLen)                   */
     uint64_t frame_len;    /* its whole payload length (fragmentLength)                          */
     uint32_t frame_mask;   /* its mask, phased so that the next payload byte takes wire byte 0   */
-    uint32_t pad;
-} wsc_conn_state;          /* 40 B */
+    uint8_t frame_utf8;    /* an in-progress PONG under messageMode TEXT: utf8 DFA state after its
+                              bytes so far (its own check, Q6; cont_utf8 stays the message's)     */
+    uint8_t pad[3];
+} wsc_conn_state;          /* 40 B.  Once status is not OPEN only status is meaningful (a closed
+                              connection decodes nothing more); frame_* are then zero           */
 
 /* One record per frame whose header was parsed and acted on, in stream order.                  */
 typedef struct wsc_frame {
@@ -330,7 +347,23 @@ int wsc_debug_stamps(wsc_ctx* ctx, uint64_t* out, uint32_t max_blocks);
  * failed batch get WSC_EV_CLOSE with close_code 1011 and err WSC_ERR_DEVICE, keep their carried
  * bytes (wsc_session_state) and decode nothing more; other connections are untouched.  There is
  * no CPU fallback.  (The reference drops all of a poller's connections when epoll_wait fails,
- * eventloop/epoll.go:41-49.)                                                                      */
+ * eventloop/epoll.go:41-49.)
+ *
+ * EOF rule.  In the reference a read returning 0 becomes io.EOF (BaseConnect.Read,
+ * baseconnect.go:100-103) and the poller then calls Close() (epoll.go:108-110) -- but only after
+ * every frame read before it was delivered, since each DecodePacket consumes at most one frame and
+ * the EOF read comes once the socket buffer is empty.  A bulk reader must keep that order: on a
+ * zero-byte read call wsc_session_eof(conn) and keep draining wsc_session_next as usual.  The
+ * session decodes every byte read before the EOF (submit / complete as usual: wsc_session_pending
+ * stays non-zero while any is left), delivers their events, and then yields WSC_EV_CLOSE with
+ * close_code 1000 and err 0 -- Close() -- as the connection's last event; an incomplete frame at
+ * the EOF is dropped (the reference's next read of it returns io.EOF).  Do NOT close the socket on
+ * the zero-byte read itself: that loses the messages still queued or in flight.
+ *
+ * Livelock guard: a batch in which one connection's whole segment (max_batch_bytes of its bytes)
+ * decoded nothing -- possible only for a header or PING / CLOSE frame longer than the batch, i.e.
+ * max_batch_bytes < 139 -- closes that connection (WSC_EV_CLOSE 1009, WSC_ERR_NO_PROGRESS) instead
+ * of re-sending the same bytes forever.  PONG and data payloads of any length stream.            */
 typedef struct wsc_session wsc_session;
 
 /* events popped by wsc_session_next(); mirrors what DecodePacket + epoll.go:104-140 produce   */
@@ -372,6 +405,15 @@ int wsc_session_decode(wsc_session* s);    /* submit + complete until everything
  * spills): a double-buffered poller submits again while this is non-zero, new reads or not.   */
 int wsc_session_pending(wsc_session* s, uint64_t* bytes);
 int wsc_session_next(wsc_session* s, uint32_t conn, wsc_event* ev);  /* DecodePacket() */
+/* The peer closed: a read returned 0 (see the EOF rule above).  Reads for conn stop; its queued
+ * and still-undecoded bytes are delivered, then WSC_EV_CLOSE 1000 / err 0.                      */
+int wsc_session_eof(wsc_session* s, uint32_t conn);
+/* Optional per-connection memory cap: a message whose bytes (its fragments and streamed pieces
+ * so far included) pass `bytes` closes the connection with WSC_EV_CLOSE 1009 /
+ * WSC_ERR_MSG_TOO_BIG instead of being buffered.  0 (the default) = no cap, like the reference
+ * (Q4: it buffers any size until make() fails), so one peer can make the session buffer up to
+ * max_frame_len bytes per frame and any number of fragments.                                    */
+int wsc_session_set_max_message(wsc_session* s, uint64_t bytes);
 int wsc_session_state(wsc_session* s, uint32_t conn, wsc_conn_state* st, uint64_t* carry_bytes);
 /* Byte accounting since create: out[0] bytes read (committed / fed), out[1] bytes sent to the
  * device (H2D of batch wires), out[2] of those, bytes sent again (carried incomplete headers and

@@ -30,6 +30,8 @@ WSC_E_INTERNAL = -7
 ERR_NONE, ERR_OPCODE_FAIL, ERR_RSV_FAIL, ERR_PING_PAYLOAD_OVERSIZE = 0, 1, 2, 3
 ERR_CTRL_FRAGMENTED, ERR_MUST_UTF8, ERR_PROTOCOL_ERROR, ERR_TOO_LARGE = 4, 5, 6, 7
 ERR_DEVICE = 8   # session: the connection's batch hit a device error -> CloseCode(1011)
+ERR_NO_PROGRESS = 9   # session: a whole batch of a connection's bytes decoded nothing -> CloseCode(1009)
+ERR_MSG_TOO_BIG = 10  # session: a message passed wsc_session_set_max_message -> CloseCode(1009)
 
 FK_FRAG, FK_MESSAGE, FK_PING, FK_PONG, FK_CLOSE, FK_PONG_EMPTY, FK_ERROR, FK_STALL, FK_PIECE = range(9)
 FF_UNMASKED, FF_CONT_MSG, FF_CTRL_ARENA, FF_HEAD_PREV = 0x01, 0x02, 0x40, 0x80
@@ -42,7 +44,8 @@ EV_NONE, EV_MESSAGE, EV_PONG, EV_CLOSE, EV_STALL = 0, 1, 2, 3, 4
 # ---- numpy views of the ABI records ------------------------------------------------------------
 CONN_STATE_DTYPE = np.dtype([("cont_len", "<u8"), ("msg_id", "<u4"), ("message_mode", "u1"),
                              ("cont_utf8", "u1"), ("status", "u1"), ("frame_hdr", "u1"),
-                             ("frame_rem", "<u8"), ("frame_len", "<u8"), ("frame_mask", "<u4"), ("pad", "<u4")])
+                             ("frame_rem", "<u8"), ("frame_len", "<u8"), ("frame_mask", "<u4"),
+                             ("frame_utf8", "u1"), ("pad", "u1", (3,))])
 FRAME_DTYPE = np.dtype([("hdr_off", "<u8"), ("payload_len", "<u4"), ("mask", "<u4"), ("seg", "<u4"),
                         ("msg_id", "<u4"), ("opcode", "u1"), ("fin", "u1"), ("kind", "u1"),
                         ("mode", "u1"), ("err", "u1"), ("hdr_len", "u1"), ("flags", "u1"),
@@ -88,7 +91,7 @@ class WscConnState(C.Structure):
     _fields_ = [("cont_len", C.c_uint64), ("msg_id", C.c_uint32), ("message_mode", C.c_uint8),
                 ("cont_utf8", C.c_uint8), ("status", C.c_uint8), ("frame_hdr", C.c_uint8),
                 ("frame_rem", C.c_uint64), ("frame_len", C.c_uint64), ("frame_mask", C.c_uint32),
-                ("pad", C.c_uint32)]
+                ("frame_utf8", C.c_uint8), ("pad", C.c_uint8 * 3)]
 
 
 # every function include/wscodec.h declares, with its ctypes signature
@@ -130,12 +133,14 @@ SIGNATURES = {
     "wsc_session_decode": (_I, [_P]),
     "wsc_session_pending": (_I, [_P, C.POINTER(_U64)]),
     "wsc_session_next": (_I, [_P, _U32, C.POINTER(WscEvent)]),
+    "wsc_session_eof": (_I, [_P, _U32]),
+    "wsc_session_set_max_message": (_I, [_P, _U64]),
     "wsc_session_state": (_I, [_P, _U32, C.POINTER(WscConnState), C.POINTER(_U64)]),
     "wsc_session_stats": (_I, [_P, C.POINTER(_U64), _U32]),
 }
 
 _lib = None
-ABI_VERSION = 3   # include/wscodec.h WSC_ABI_VERSION: the record layouts above
+ABI_VERSION = 4   # include/wscodec.h WSC_ABI_VERSION: the record layouts above
 
 
 def load_library(path: str = LIB_PATH):
@@ -410,6 +415,8 @@ WebsocketMustUtf8 = NetmanError("websocket text message must utf-8")
 WebsocketProtocolError = NetmanError("websocket protocol error")
 WebsocketFrameTooLarge = NetmanError("websocket frame exceeds max_frame_len")  # Q4 divergence
 DeviceFailure = NetmanError("websocket decode device failure")                  # session policy -> 1011
+NoProgress = NetmanError("websocket frame header larger than the decode batch")  # session guard -> 1009
+MessageTooBig = NetmanError("websocket message exceeds the session cap")         # optional cap -> 1009
 EAGAIN = NetmanError("resource temporarily unavailable")
 
 SENTINELS = {
@@ -421,6 +428,8 @@ SENTINELS = {
     ERR_PROTOCOL_ERROR: WebsocketProtocolError,
     ERR_TOO_LARGE: WebsocketFrameTooLarge,
     ERR_DEVICE: DeviceFailure,
+    ERR_NO_PROGRESS: NoProgress,
+    ERR_MSG_TOO_BIG: MessageTooBig,
 }
 
 
@@ -433,6 +442,8 @@ def close_code_for(err) -> int | None:
         return 1007
     if err is DeviceFailure:
         return 1011
+    if err is NoProgress or err is MessageTooBig:
+        return 1009
     return None
 
 
@@ -500,6 +511,13 @@ class Session:
 
     def decode(self):
         _check(self.lib.wsc_session_decode(self.h), "wsc_session_decode")
+
+    def eof(self, conn: int):
+        """the peer closed (a read returned 0): wsc_session_eof -- queued events first, then Close()"""
+        _check(self.lib.wsc_session_eof(self.h, conn), "wsc_session_eof")
+
+    def set_max_message(self, nbytes: int):
+        _check(self.lib.wsc_session_set_max_message(self.h, int(nbytes)), "wsc_session_set_max_message")
 
     def pending(self) -> int:
         """bytes fed but not yet submitted (submit again while non-zero)"""

@@ -98,6 +98,8 @@ struct wsc_ctx {
     uint32_t* u8ctr = nullptr;          // UTF-8 item counters, one per decode parity ([0], [32]): a decode's walk
                                         // allocates from its own, its unmask zeroes the other (the next decode's)
     uint32_t u8par = 0;                 // parity of the decode the last walk belongs to
+    bool u8_dirty = false;              // a walk was launched whose unmask (which zeroes the next decode's item
+                                        // counter) was not: the next walk zeroes its counter itself
     uint32_t u8_inline_max = 256;
     uint32_t u8_grid = 0;               // WSC_U8_GRID: k_u8_check workgroups (A/B experiments; 0 = 5 per CU)
     bool walk_tiled = true;             // WSC_WALK_TILED=0: the three-launch walk for mode 3 (A/B)
@@ -428,8 +430,10 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     wa.summary = b->summary;
     wa.u8items = c->u8items;
     wa.u8items_cap = c->u8items_cap;
-    if (phase != 2) c->u8par ^= 1u;   // a new decode: the other item counter (zeroed by the last unmask)
-    wa.u8count = c->u8ctr + 32 * c->u8par;
+    // a new decode uses the other item counter (zeroed by the last decode's unmask); committed to
+    // the context only once every check below has passed (round-3 ADVICE medium)
+    const uint32_t par = phase != 2 ? c->u8par ^ 1u : c->u8par;
+    wa.u8count = c->u8ctr + 32 * par;
     wa.u8seg = c->u8seg;
     wa.u8_inline_max = c->u8_inline_max;
     wa.sticky = c->sticky;
@@ -447,12 +451,8 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     const uint32_t wnt = (mode == 64 || mode == 16 || mode == 32) ? 64u : 256u;
     const uint32_t spb = (mode == 65 || mode == 66) ? 64u : (mode == 16 || mode == 32) ? mode : wnt;   // segments per walk block
     const dim3 wblk(wnt), wgrid((n + spb - 1) / spb);
-    if (phase != 2) {
-        c->walk_used = mode;
-        c->walk_blocks = wgrid.x;
-        if (wgrid.x + 1 > c->max_walk_blocks)   // never index look-back state past its allocation
-            return fail(WSC_E_INTERNAL, "walk geometry needs more look-back blocks than allocated");
-    }
+    if (phase != 2 && wgrid.x + 1 > c->max_walk_blocks)   // never index look-back state past its allocation
+        return fail(WSC_E_INTERNAL, "walk geometry needs more look-back blocks than allocated");
     uint32_t rearm = 0;   // (after the launch below: the tiled walk sets walk_blocks)
     auto rec = [&](int i) {
         if (ev) (void)hipEventRecord(ev[i], st);
@@ -463,9 +463,19 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     const hipStream_t ws = split ? sw : st;
     if (phase != 2) {
     if (const int r = fin_wait(c)) return r;
+    // from here the decode's state is the context's: geometry, item-counter parity
+    c->walk_used = mode;
+    c->walk_blocks = wgrid.x;
+    c->u8par = par;
+    const bool stale = c->u8_dirty;   // the previous decode's unmask never launched: this counter is stale
+    c->u8_dirty = true;
     __atomic_store_n(&c->hflag[0], 0u, __ATOMIC_RELEASE);
     c->walk_waited = false;
     if (split) HIP_TRY(hipStreamWaitEvent(ws, c->ev_done, 0));
+    if (stale) {   // ... and its look-back ticket / flags were not re-armed either
+        HIP_TRY(hipMemsetAsync(c->u8ctr + 32 * par, 0, sizeof(uint32_t), ws));
+        HIP_TRY(hipMemsetAsync(c->lb_state, 0, (c->max_walk_blocks + 3) * sizeof(uint32_t), ws));
+    }
     // fused: 16 frame records per lane in LDS (segments with more frames re-walk their headers)
     if (mode == 3 && c->walk_tiled) {
         // tiled: a persistent grid (2 blocks per CU of the walk's stream), contiguous segment ranges
@@ -557,6 +567,7 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
                        c->lb_state, rearm,   // re-arms ticket, timeout, flags
                        sig_unmask ? c->fin_ctr : nullptr, sig_unmask ? c->hflag + 1 : nullptr, c->fin_seq + 1, uw);
     HIP_TRY(hipGetLastError());
+    c->u8_dirty = false;   // the next decode's counter is zeroed by this unmask
     rec(2);
     if (need_u8) {
         U8Args ua{};

@@ -171,6 +171,7 @@ struct WalkEnd {
     uint64_t frem, flen;     // the in-progress (streamed) data frame: payload still to come, length
     uint32_t fmask, fhdr;    // ... its mask phased to the next payload byte, FIN << 7 | opcode
     uint32_t msg, mode, status, close_code, err, u8dfa;
+    uint32_t pdfa;           // an in-progress PONG under TEXT mode: DFA state of its bytes so far
     bool replay;             // counting pass: the LDS records hold the whole segment
 };
 
@@ -186,7 +187,8 @@ __device__ __forceinline__ wsc_conn_state end_state(const WalkEnd& w) {
     o.frame_rem = w.frem;
     o.frame_len = w.frem ? w.flen : 0;
     o.frame_mask = w.frem ? w.fmask : 0;
-    o.pad = 0;
+    o.frame_utf8 = (w.frem && (w.fhdr & 0xFu) == 10u) ? (uint8_t)w.pdfa : 0;
+    o.pad[0] = o.pad[1] = o.pad[2] = 0;
     return o;
 }
 
@@ -254,6 +256,9 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
     // websocket_frame.go:16-31 -- nextFrame reads what is there into rBuffer, completes later
     uint64_t frem = st.frame_rem, flen = st.frame_len;
     uint32_t fmask = st.frame_mask, fhdr = st.frame_hdr;
+    // a streamed PONG under messageMode TEXT: the DFA state of its payload so far (its own utf8.Valid,
+    // websocket_frame.go:71 with Q6; the message's state u8dfa is untouched by it)
+    uint32_t pdfa = st.frame_utf8;
     uint32_t close_code = 0, err_out = 0;
     uint32_t nf = 0, ns0 = 0, ns1 = 0, sflags = 0;
     uint64_t nb0 = 0, nb1 = 0;
@@ -268,6 +273,7 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
     bool u8_pending = false;                      // a text chain has a deferred (chip-wide) part
     uint32_t u8_head = 0xFFFFFFFFu, u8_last = 0xFFFFFFFFu, u8_n = 0, u8_ncomp = 0;
     bool u8_comp = false;                         // an item whose verdict needs the segment's composition
+    bool p8_open = false;                         // the segment ends inside a PONG whose piece was deferred
     uint32_t pool_next = 0, pool_end = 0;         // the segment's unused item slots
     auto dead_fill = [&](uint32_t i, uint32_t e) {
         for (; i < e; ++i)
@@ -280,7 +286,8 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
     };
     if constexpr (EMIT) {
         u8fail = a.u8info[2 * s];
-        u8dfa = a.u8info[2 * s + 1];
+        u8dfa = a.u8info[2 * s + 1] & 0xFFu;
+        pdfa = a.u8info[2 * s + 1] >> 8;
     }
 
     uint64_t pos = seg_start;
@@ -301,16 +308,17 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
 
     // A text payload validated chip-wide (after the unmask): item slots from the segment's pool,
     // window flags for the unmask's fold, the segment's item list.  Counting pass only.
-    auto defer = [&](uint64_t src, uint64_t n, uint32_t mk, bool part, bool chain, uint32_t hl) {
+    // kind: U8K_*; PONG pieces (U8K_PONG / U8K_PONG_END) bring their own entry state p_in
+    auto defer = [&](uint64_t src, uint64_t n, uint32_t mk, uint8_t kind, uint32_t p_in, uint32_t hl) {
         // large text (or a chain already deferred): validated chip-wide by k_u8_check,
         // which also applies the verdict; the walk goes on as if it were valid
+        const bool part = kind == U8K_PART, chain = kind == U8K_CHAIN, pong = kind >= U8K_PONG;
         if constexpr (PURE) {   // a count without side effects: only the chain state the walk keys on
             if (part) u8_pending = true;
             if (chain) u8_pending = false;
             return;
         }
-        const uint8_t kind = part ? U8K_PART : (chain ? U8K_CHAIN : U8K_SELF);
-        const uint8_t s_in = (part || chain) ? (u8_pending ? 0xFF : (uint8_t)u8dfa) : 0;
+        const uint8_t s_in = pong ? (uint8_t)p_in : (part || chain) ? (u8_pending ? 0xFF : (uint8_t)u8dfa) : 0;
         // a payload up to U8_PIECE is one piece; longer ones are cut at absolute
         // U8_PIECE-aligned wire offsets.  Either way every unmask window that lies
         // inside a text payload lies inside one item (its map is folded by the unmask
@@ -385,10 +393,10 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
                 else u8_head = idx;
                 u8_last = idx;
                 u8_n += 1;
-                if (part || chain || pieces != 1) u8_ncomp += 1;   // counted by k_u8_check
+                if (part || chain || pong || pieces != 1) u8_ncomp += 1;   // counted by k_u8_check
             }
         }
-        if (part || chain || pieces != 1) u8_comp = true;
+        if (part || chain || pong || pieces != 1) u8_comp = true;
         if (part) u8_pending = true;
         if (chain) u8_pending = false;   // the message completes here
     };
@@ -413,7 +421,7 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
                     const bool skip = fr.mode == 1 && u8_run_masked(0, w, src, n, mk) != 0;
                     if (!skip && u8_run_masked(0, w, src + 2, n - 2, rotr32(mk, 16)) != 0) u8fail = nf;
                 } else if (n > a.u8_inline_max || ((part || chain) && u8_pending)) {
-                    defer(src, n, mk, part, chain, fr.hdr_len);
+                    defer(src, n, mk, part ? U8K_PART : (chain ? U8K_CHAIN : U8K_SELF), 0, fr.hdr_len);
                 } else {
                     bool ok = true;
                     if (part) u8dfa = u8_run_masked(u8dfa, w, src, n, mk);
@@ -422,6 +430,29 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
                     if (!ok) u8fail = nf;
                 }
             }
+        }
+        // a streamed PONG's piece under messageMode TEXT (Q6): its payload alone must be valid once
+        // complete; each piece continues the PONG's own DFA (carried in frame_utf8 across batches)
+        const bool pong_u8 = fr.opcode == 10 && fr.mode == 1 && (fr.kind == WSC_FK_PIECE || (fr.flags & WSC_FF_HEAD_PREV));
+        if (pong_u8) {
+            sflags |= SEGF_UTF8;
+            if constexpr (!EMIT) {
+                const bool end = fr.kind != WSC_FK_PIECE;
+                const uint32_t p_in = (fr.flags & WSC_FF_HEAD_PREV) ? pdfa : 0u;   // fresh at its header
+                const uint64_t src = fr.hdr_off + fr.hdr_len;
+                if (plen > a.u8_inline_max) {   // chip-wide: the check composes it (and carries it if open)
+                    defer(src, plen, fr.mask, end ? U8K_PONG_END : U8K_PONG, p_in, fr.hdr_len);
+                    p8_open = !end;
+                    pdfa = 0;
+                } else {
+                    pdfa = u8_run_masked(p_in, w, src, plen, fr.mask);
+                    p8_open = false;
+                    if (end && pdfa != 0) u8fail = nf;
+                }
+                if (end) pdfa = 0;
+            }
+        }
+        if ((fr.flags & (WSC_FF_U8_PART | WSC_FF_U8_SELF | WSC_FF_U8_CHAIN | WSC_FF_U8_REASON)) || pong_u8) {
             if (nf == u8fail) {   // -> CloseCode(1007) (epoll.go:126-127); nothing after it is read
                 fr.kind = WSC_FK_ERROR;
                 fr.err = WSC_ERR_MUST_UTF8;
@@ -437,7 +468,8 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
         else record(fr, have_span, region, plen);
         nf += 1;
         if (have_span) {
-            if (COMPACT && region) { ns1 += 1; nb1 += plen; }   // control payloads: <= 125 B
+            // (control payloads: <= 125 B, but a PONG's -- and its pieces' -- have no bound)
+            if (COMPACT && region) { ns1 += span_chunks(fr.hdr_off + fr.hdr_len, plen); nb1 += plen; }
             else { ns0 += span_chunks(fr.hdr_off + fr.hdr_len, plen); nb0 += plen; }
         }
     };
@@ -463,10 +495,13 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
         fr.err = 0;
         fr.hdr_len = 0;
         fr.flags = WSC_FF_UNMASKED | WSC_FF_HEAD_PREV;
-        const bool text = mode == 1;
+        const bool text = mode == 1 && op != 10;   // (a PONG's own check: finish, Q6)
         if (take < frem) {
             fr.kind = WSC_FK_PIECE;
             if (text) fr.flags |= WSC_FF_U8_PART;
+        } else if (op == 10) {   // the PONG is complete: read and discarded (websocket.go:203-205), Q5
+            fr.kind = WSC_FK_PONG;
+            msg += 1;
         } else if (fin) {
             fr.kind = WSC_FK_MESSAGE;
             if (op == 0 && cont >= 1) { fr.flags |= WSC_FF_CONT_MSG; cont = 0; }
@@ -480,7 +515,7 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
         }
         frem -= take;
         fmask = rotr32(fmask, 8u * (uint32_t)(take & 3));
-        finish(fr, take, take > 0, 0);
+        finish(fr, take, take > 0, op == 10 ? 1u : 0u);   // (COMPACT: a PONG's bytes in the control region)
         pos += take;
     };
 
@@ -582,8 +617,10 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
                 if (payload && !err) {
                     if (plen > a.max_frame_len) err = WSC_ERR_TOO_LARGE;        // Q4
                     else if (avail < hl + plen) {
-                        if (op > 2) return false;   // a control frame (<= 125 B) waits whole
-                        piece = true;               // websocket_frame.go:16-31 partial read
+                        // PING / CLOSE (<= 125 B by the rules above) wait whole; a data frame or a
+                        // PONG (no size limit, websocket.go:191-205) streams: websocket_frame.go:16-31
+                        if (op == 8 || op == 9) return false;
+                        piece = true;
                     }
                 }
                 if (piece) {
@@ -603,8 +640,12 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
                     // the payload is carried as state, never as bytes
                     fr.kind = WSC_FK_PIECE;
                     fr.flags |= WSC_FF_UNMASKED;
-                    if (mode_h == 1) fr.flags |= WSC_FF_U8_PART;
-                    mode = mode_h;
+                    if (op == 10) {
+                        region = 1;   // COMPACT: the control region (the payload is discarded)
+                    } else {
+                        if (mode_h == 1) fr.flags |= WSC_FF_U8_PART;
+                        mode = mode_h;
+                    }
                     frem = plen - take;
                     flen = plen;
                     fmask = rotr32(mask, 8u * (uint32_t)(take & 3));
@@ -761,14 +802,14 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
         replay = lrec && nf <= cap && seg_end - seg_start <= 0xFFFFFFFFull && !(sflags & SEGF_LONG);
         if (!replay && !PURE) {   // only a re-walking emit pass reads them back
             a.u8info[2 * s] = u8fail;
-            a.u8info[2 * s + 1] = u8dfa;
+            a.u8info[2 * s + 1] = u8dfa | pdfa << 8;
         }
         if (u8_n) {
             U8Seg g{};
             g.head = u8_head;
             g.n = u8_ncomp;   // the composite items (single-piece messages are never counted)
             g.done = 0;
-            g.pending_end = (u8_pending ? 1u : 0u) | (u8_comp ? 2u : 0u);
+            g.pending_end = (u8_pending ? 1u : 0u) | (u8_comp ? 2u : 0u) | (p8_open && frem ? 4u : 0u);
             g.minfail = 0xFFFFFFFFu;
             a.u8seg[s] = g;
             c.flags |= SEGF_U8DEFER;
@@ -776,7 +817,7 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
     }
     WalkEnd we;
     we.pos = pos; we.cont = cont; we.msg = msg; we.mode = mode; we.status = status;
-    we.close_code = close_code; we.err = err_out; we.u8dfa = u8dfa;
+    we.close_code = close_code; we.err = err_out; we.u8dfa = u8dfa; we.pdfa = pdfa;
     we.frem = status == WSC_SEG_OPEN ? frem : 0;
     we.flen = flen; we.fmask = fmask; we.fhdr = fhdr;
     we.last_dend = pend;
@@ -1371,6 +1412,17 @@ __global__ __launch_bounds__(NT) void k_walk_tiled(WalkArgs a, uint32_t per_bloc
         run = sc_add(run, ttot);
         __syncthreads();   // (the tile's LDS is reused by the next tile)
     }
+    // phase 2 emitted at the offsets phase 1 published: both passes must have counted the same
+    // frames, spans and bytes, or records and summary disagree -- flag it as an internal error
+    // (look-back timeout bit: the batch's results are invalid; sticky for wsc_error_flags)
+    if (lane == 0) {
+        const SegCount want = sc_add(block_prefix, btot);
+        if (run.frames != want.frames || run.spans0 != want.spans0 || run.spans1 != want.spans1 ||
+            run.bytes0 != want.bytes0 || run.bytes1 != want.bytes1) {
+            __hip_atomic_fetch_or(a.lb_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_or(a.sticky, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
     if (se == a.n_segs && sb < se && lane == 0) write_summary<COMPACT>(a, sc_add(block_prefix, btot));
 }
 
@@ -1416,6 +1468,7 @@ __device__ __forceinline__ void u8_count(const U8Args& a, uint32_t seg, uint32_t
 // SELF items never sit inside a chain and are skipped.
 __device__ __forceinline__ uint32_t u8_comp_verdict(const U8Args& a, uint32_t s, const U8Seg& g) {
     uint32_t cur = 0, start = 0;   // states 0..7, 0xFF = reject
+    uint32_t pcur = 0;             // an open streamed PONG's state (its own chain, Q6)
     uint64_t fm = u8m_id();
     uint32_t j = g.head;
     for (uint32_t c = 0; c < a.items_cap && j != 0xFFFFFFFFu; ++c) {
@@ -1423,7 +1476,8 @@ __device__ __forceinline__ uint32_t u8_comp_verdict(const U8Args& a, uint32_t s,
         if (x.kind == U8K_SELF && x.first && x.last) { j = x.next; continue; }
         const uint64_t m = __hip_atomic_fetch_add(a.maps + j, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (x.first) {
-            start = x.kind == U8K_SELF ? 0u : (x.s_in != 0xFF ? (x.s_in > 7 ? 0xFFu : (uint32_t)x.s_in) : cur);
+            if (x.kind >= U8K_PONG) start = x.s_in > 7 ? 0xFFu : (uint32_t)x.s_in;   // known at the walk
+            else start = x.kind == U8K_SELF ? 0u : (x.s_in != 0xFF ? (x.s_in > 7 ? 0xFFu : (uint32_t)x.s_in) : cur);
             fm = u8m_id();
         }
         fm = u8m_then(fm, m);
@@ -1431,6 +1485,8 @@ __device__ __forceinline__ uint32_t u8_comp_verdict(const U8Args& a, uint32_t s,
             const uint32_t end = u8m_get(fm, start);
             if (x.kind == U8K_PART) {
                 cur = end;
+            } else if (x.kind == U8K_PONG) {
+                pcur = end;
             } else {
                 if (end != 0) return x.ordinal;
                 if (x.kind == U8K_CHAIN) cur = 0;
@@ -1440,6 +1496,7 @@ __device__ __forceinline__ uint32_t u8_comp_verdict(const U8Args& a, uint32_t s,
     }
     if ((g.pending_end & 1u) && (a.state_out[s].cont_len || a.state_out[s].frame_rem))
         a.state_out[s].cont_utf8 = (uint8_t)(cur > 7 ? 8u : cur);
+    if (g.pending_end & 4u) a.state_out[s].frame_utf8 = (uint8_t)(pcur > 7 ? 8u : pcur);
     return 0xFFFFFFFFu;
 }
 
@@ -1469,7 +1526,14 @@ __device__ __forceinline__ void u8_fail(const U8Args& a, uint32_t s, uint32_t or
     r->status = WSC_SEG_ERROR;
     r->close_code = 1007;
     r->err = WSC_ERR_MUST_UTF8;
-    a.state_out[s].status = WSC_SEG_ERROR;
+    // a closed connection carries no frame in progress (as the walk's own terminal paths leave it)
+    wsc_conn_state* so = a.state_out + s;
+    so->status = WSC_SEG_ERROR;
+    so->frame_rem = 0;
+    so->frame_len = 0;
+    so->frame_mask = 0;
+    so->frame_hdr = 0;
+    so->frame_utf8 = 0;
     lo = fend;
     hi = old == 0xFFFFFFFFu ? ~0ull : frame_end(old);
 }

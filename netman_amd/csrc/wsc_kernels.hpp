@@ -39,7 +39,10 @@ enum : uint32_t { SEGF_UTF8 = 1u, SEGF_U8DEFER = 2u, SEGF_LONG = 4u };
 // at most U8_PIECE bytes (one per frame below 1 GiB), validated chip-wide: the unmask folds the
 // maps of the windows inside them, k_u8_check the partial windows at their ends (after the unmask).
 constexpr uint32_t U8_PIECE = 1u << 30;
-enum : uint8_t { U8K_SELF = 0, U8K_PART = 1, U8K_CHAIN = 2 };   // close reasons are SELF items
+// close reasons are SELF items; a streamed PONG's piece under TEXT mode (Q6) is a PONG item (the
+// PONG continues in the next batch: its end state is carried) or PONG_END (its verdict), entry state
+// known at the walk (0 at its header, else the carried frame_utf8)
+enum : uint8_t { U8K_SELF = 0, U8K_PART = 1, U8K_CHAIN = 2, U8K_PONG = 3, U8K_PONG_END = 4 };
 constexpr uint32_t U8_DEAD = 0xFFFFFFFFu;   // U8Item.seg of an unused walk-pool slot
 struct U8Item {
     uint64_t src;       // wire offset of the first (masked) byte
@@ -55,7 +58,8 @@ struct U8Item {
 static_assert(sizeof(U8Item) == 32, "U8Item layout");
 struct U8Seg {          // per segment with deferred items (written by the walk)
     uint32_t head, n, done;
-    uint32_t pending_end;  // bit 0: a text chain with a deferred part is still open; bit 1: composite items
+    uint32_t pending_end;  // bit 0: a text chain with a deferred part is still open; bit 1: composite items;
+                           // bit 2: a deferred PONG piece is still open (its state -> frame_utf8)
     uint32_t sbase, nspans, fbase;         // the segment's span and frame ranges (emit pass)
     uint32_t minfail;      // first failing single-piece SELF frame (ordinal), 0xFFFFFFFF = none
 };

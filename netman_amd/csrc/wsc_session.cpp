@@ -90,6 +90,9 @@ struct Conn {
     bool failed = false;          // its batch hit a device error (WSC_ERR_DEVICE)
     bool in_flight = false;       // has a segment in the submitted batch: new bytes wait in the
                                   // spill until complete() has set the carry they must follow
+    bool eof = false;             // the peer closed (a read returned 0): once every byte read before it
+                                  // is decoded, the last event is Close() (baseconnect.go:100-103,
+                                  // epoll.go:108-110)
 };
 
 struct Stage {                    // one staging set: pinned host buffers, device buffers, context
@@ -128,6 +131,15 @@ uint32_t close_code_for(uint32_t err) {   // eventloop/epoll.go:106-129
     return err == WSC_ERR_MUST_UTF8 ? 1007u : 1002u;
 }
 
+void push_close(Conn& c, uint32_t code, uint32_t err) {
+    Event e;
+    std::memset(&e.ev, 0, sizeof(e.ev));
+    e.ev.type = WSC_EV_CLOSE;
+    e.ev.close_code = code;
+    e.ev.err = err;
+    c.pending.push_back(std::move(e));
+}
+
 double now_s() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -157,6 +169,7 @@ struct wsc_session {
     // wsc_session_stats: bytes read, sent to the device, of those sent again (carried), batches,
     // streamed payload bytes collected into messages
     uint64_t st_read = 0, st_h2d = 0, st_resent = 0, st_batches = 0, st_pieces = 0;
+    uint64_t max_message = 0;     // wsc_session_set_max_message: 0 = no cap (the reference has none, Q4)
 };
 
 namespace {
@@ -253,7 +266,16 @@ void harvest(wsc_session* s, int set, Conn& c, uint32_t slot, const uint8_t* in_
              const wsc_frame* frames, const uint64_t* frame_dst, uint64_t arena_base) {
     const bool compact = (s->flags & WSC_F_COMPACT) != 0;
     bool views = false;
-    for (uint32_t i = r.frame_begin; i < r.frame_begin + r.frame_count; ++i) {
+    // wsc_session_set_max_message: a message (or the fragments / pieces of one) past the cap closes
+    // the connection with 1009 instead of buffering it (off by default: the reference buffers any size)
+    bool capped = false;
+    auto over = [&](uint64_t more) {
+        if (!s->max_message || c.cont.size() + c.rbuf.size() + more <= s->max_message) return false;
+        push_close(c, 1009, WSC_ERR_MSG_TOO_BIG);
+        capped = true;
+        return true;
+    };
+    for (uint32_t i = r.frame_begin; i < r.frame_begin + r.frame_count && !capped; ++i) {
         const wsc_frame& f = frames[i];
         const uint64_t flen = f.payload_len | (uint64_t)f.payload_len_hi << 32;   // 40-bit length
         const uint8_t* p = compact ? res_base + arena_base + frame_dst[i] : res_base + f.hdr_off + f.hdr_len;
@@ -261,10 +283,13 @@ void harvest(wsc_session* s, int set, Conn& c, uint32_t slot, const uint8_t* in_
         std::memset(&e.ev, 0, sizeof(e.ev));
         switch (f.kind) {
         case WSC_FK_PIECE:                                    // websocket_frame.go:16-31 (rBuffer)
+            if (f.opcode == 10) continue;                     // a PONG's bytes: discarded when complete
+            if (over(flen)) continue;
             c.rbuf.insert(c.rbuf.end(), p, p + flen);
             s->st_pieces += flen;
             continue;
         case WSC_FK_FRAG:                                     // websocket_frame.go:95-98
+            if (over(flen)) continue;
             if (!c.rbuf.empty()) {                            // a streamed fragment's earlier pieces
                 c.cont.insert(c.cont.end(), c.rbuf.begin(), c.rbuf.end());
                 c.rbuf.clear();
@@ -272,6 +297,7 @@ void harvest(wsc_session* s, int set, Conn& c, uint32_t slot, const uint8_t* in_
             c.cont.insert(c.cont.end(), p, p + flen);
             continue;
         case WSC_FK_MESSAGE:                                  // websocket_frame.go:62-91
+            if (over(flen)) continue;
             if (f.flags & WSC_FF_CONT_MSG) {
                 e.data.swap(c.cont);
                 e.data.insert(e.data.end(), c.rbuf.begin(), c.rbuf.end());
@@ -318,7 +344,13 @@ void harvest(wsc_session* s, int set, Conn& c, uint32_t slot, const uint8_t* in_
     }
     if (views) s->st[set].view_conns.push_back(slot);
     c.st = so;
-    if (r.status == WSC_SEG_OPEN) {   // the undecoded tail (still masked) goes in front of the next bytes
+    // no-progress guard: a whole batch of this connection's bytes decoded nothing (only a header or a
+    // PING / CLOSE frame longer than max_batch_bytes can do that): re-sending it would never end
+    const bool stuck = r.status == WSC_SEG_OPEN && r.consumed == 0 && r.frame_count == 0 &&
+                       seg_len >= s->cfg.max_batch_bytes;
+    if (stuck) push_close(c, 1009, WSC_ERR_NO_PROGRESS);
+    if (capped || stuck) c.st.status = WSC_SEG_ERROR;
+    if (c.st.status == WSC_SEG_OPEN) {   // the undecoded tail (still masked) goes in front of the next bytes
         c.carry.assign(in_seg + r.consumed, in_seg + seg_len);   // (placing a segment emptied the carry)
     } else {
         c.carry.clear();
@@ -326,6 +358,20 @@ void harvest(wsc_session* s, int set, Conn& c, uint32_t slot, const uint8_t* in_
         c.cont.clear();
         c.rbuf.clear();
     }
+}
+
+// EOF (wsc_session_eof): once nothing of the connection is left to decode -- no bytes in a batch
+// being filled or in flight, none waiting in its spill -- its last event is Close() with code 1000
+// (epoll.go:108-110), after every event its earlier bytes produced; an incomplete frame left in
+// its carry is dropped, as the reference's next read returns io.EOF inside nextFrame or the header
+void maybe_eof(wsc_session* s, Conn& c) {
+    if (!c.eof || !c.live || c.failed || c.st.status != WSC_SEG_OPEN) return;
+    if (c.in_flight || c.fill_epoch == s->fill_epoch || !c.spill.empty()) return;
+    push_close(c, 1000, 0);
+    c.st.status = WSC_SEG_CLOSED;
+    c.carry.clear();
+    c.cont.clear();
+    c.rbuf.clear();
 }
 
 void fail_conn(wsc_session* s, Conn& c) {
@@ -405,6 +451,7 @@ int decode_sync_part(wsc_session* s, int set, uint32_t a, uint32_t b, uint64_t p
             std::vector<uint8_t> tail(g.h_wire + base + end, g.h_wire + base + g.seg_len[a]);
             if (c->st.status == WSC_SEG_OPEN) c->spill.insert(c->spill.begin(), tail.begin(), tail.end());
         }
+        maybe_eof(s, *c);
     }
     // views handed out above point into res (in place) / the arena copy region: both in h_res
     return WSC_OK;
@@ -587,7 +634,7 @@ int wsc_session_reserve(wsc_session* s, uint32_t conn, uint64_t max_bytes, uint8
     *ptr = nullptr;
     *avail = 0;
     c->reserved = 0;
-    if (c->st.status != WSC_SEG_OPEN || c->failed || max_bytes == 0) return WSC_OK;   // closed: nothing to read into
+    if (c->st.status != WSC_SEG_OPEN || c->failed || c->eof || max_bytes == 0) return WSC_OK;   // closed: nothing to read into
     Stage& f = s->st[s->fill];
     const uint64_t cap = s->cfg.max_batch_bytes;
     // straight into the staging being filled, right behind the connection's segment there (its
@@ -769,6 +816,7 @@ int wsc_session_complete(wsc_session* s) {
             harvest(s, set, *c, h & SLOT_MASK, g.h_wire + g.seg_start[q], g.h_res, g.seg_len[q],
                     g.h_seg_out[q], g.h_state_out[q], g.h_frames, compact ? g.h_frame_dst : nullptr, 0);
             g.done[q] = 1;
+            maybe_eof(s, *c);
         }
     }
     if (rc != WSC_OK && rc != WSC_E_CAPACITY) {
@@ -820,6 +868,24 @@ int wsc_session_pending(wsc_session* s, uint64_t* bytes) {
     for (const Conn& c : s->conns)
         if (c.live && !c.failed && c.st.status == WSC_SEG_OPEN) n += c.spill.size();
     *bytes = n;
+    return WSC_OK;
+}
+
+// The peer closed its side: a read returned 0 (BaseConnect.Read -> io.EOF, baseconnect.go:100-103).
+// Every event of the bytes read before it is delivered first; then Close() (epoll.go:108-110).
+int wsc_session_eof(wsc_session* s, uint32_t conn) {
+    if (!s) return WSC_E_INVAL;
+    apply_removes(s);
+    Conn* c = lookup(s, conn);
+    if (!c) return WSC_E_STATE;
+    c->eof = true;
+    maybe_eof(s, *c);
+    return WSC_OK;
+}
+
+int wsc_session_set_max_message(wsc_session* s, uint64_t bytes) {
+    if (!s) return WSC_E_INVAL;
+    s->max_message = bytes;
     return WSC_OK;
 }
 

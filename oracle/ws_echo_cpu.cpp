@@ -20,6 +20,7 @@ struct Conn {
     std::vector<uint8_t> buf;                 // bytes read, not yet decoded (the socket buffer)
     std::deque<std::vector<uint8_t>> msgs;    // delivered messages
     std::vector<uint8_t> cur;                 // the message last returned by next()
+    bool eof = false, closed = false;         // read() returned 0 (io.EOF) / Close() handed out
 };
 
 struct CpuDecoder : echo::Decoder {
@@ -64,15 +65,24 @@ struct CpuDecoder : echo::Decoder {
         }
         dirty.clear();
     }
-    bool next(int id, const uint8_t** data, size_t* len) override {
+    int next(int id, const uint8_t** data, size_t* len) override {
         Conn& c = conns[id];
-        if (c.msgs.empty()) return false;
+        if (c.msgs.empty()) {
+            // io.EOF -> Close() (epoll.go:108-110), once every frame read before it is delivered
+            // (decode() ran over every read already: the EOF read comes in a later round)
+            if (c.eof && !c.closed) {
+                c.closed = true;
+                return echo::EV_CLOSE;
+            }
+            return echo::EV_NONE;
+        }
         c.cur = std::move(c.msgs.front());
         c.msgs.pop_front();
         *data = c.cur.data();
         *len = c.cur.size();
-        return true;
+        return echo::EV_MESSAGE;
     }
+    void eof(int id) override { conns[id].eof = true; }
 };
 
 }  // namespace
@@ -81,9 +91,10 @@ int main(int argc, char** argv) {
     int conns = 1, frames = 4000, threads = 1, pollers = 1;
     size_t size = 65536;
     echo::parse_args(argc, argv, conns, frames, size, threads, pollers);
-    const echo::Result r = echo::run([](int) { return std::unique_ptr<echo::Decoder>(new CpuDecoder()); }, pollers,
-                                     conns, frames, size, threads);
+    const bool shut = echo::has_flag(argc, argv, "--shutdown");
+    const echo::Result r = echo::run([](int, int) { return std::unique_ptr<echo::Decoder>(new CpuDecoder()); },
+                                     pollers, conns, frames, size, threads, 60, shut);
     echo::print_json("cpu port: reference frame-at-a-time decode (websocket.go / websocket_frame.go), one per poller",
-                     r, pollers, conns, frames, size);
+                     r, pollers, conns, frames, size, 0, shut);
     return r.ok ? 0 : 1;
 }

@@ -71,12 +71,12 @@ static void buf_free(buf_t* b) { free(b->p); b->p = NULL; b->n = b->cap = 0; }
 
 /* --- simulated non-blocking socket + BaseConnect.Read (baseconnect.go:84-106) ------------------- */
 enum { E_NIL = 0, E_EAGAIN = 100, E_EOF = 101 };
-typedef struct { const uint8_t* s; uint64_t avail, rpos; } sock_t;
-/* unix.Read: -1/EAGAIN when nothing is buffered, 0 for a zero-length read; BaseConnect.Read maps
- * n<0 -> (0, err) and n==0 -> (0, io.EOF). */
+typedef struct { const uint8_t* s; uint64_t avail, rpos; int eof; } sock_t;
+/* unix.Read: -1/EAGAIN when nothing is buffered, 0 for a zero-length read or once the peer has
+ * closed and nothing is buffered; BaseConnect.Read maps n<0 -> (0, err) and n==0 -> (0, io.EOF). */
 static int64_t conn_read(sock_t* k, uint8_t* dst, uint64_t n, int* err) {
     if (n == 0) { *err = E_EOF; return 0; }
-    if (k->rpos >= k->avail) { *err = E_EAGAIN; return 0; }
+    if (k->rpos >= k->avail) { *err = k->eof ? E_EOF : E_EAGAIN; return 0; }
     uint64_t m = k->avail - k->rpos;
     if (m > n) m = n;
     memcpy(dst, k->s + k->rpos, m);
@@ -480,6 +480,14 @@ int wso_run(const uint8_t* stream, uint64_t len, const uint64_t* chunk_ends, uin
             uint64_t max_frame_len, uint8_t* inplace,
             wso_event* ev, uint32_t ev_cap, wso_frame* fr, uint32_t fr_cap,
             uint8_t* arena, uint64_t arena_cap, wso_result* res) {
+    return wso_run_ex(stream, len, chunk_ends, n_chunks, max_frame_len, inplace, ev, ev_cap, fr, fr_cap, arena,
+                      arena_cap, res, 0);
+}
+
+int wso_run_ex(const uint8_t* stream, uint64_t len, const uint64_t* chunk_ends, uint32_t n_chunks,
+               uint64_t max_frame_len, uint8_t* inplace,
+               wso_event* ev, uint32_t ev_cap, wso_frame* fr, uint32_t fr_cap,
+               uint8_t* arena, uint64_t arena_cap, wso_result* res, uint32_t flags) {
     run_t r;
     memset(&r, 0, sizeof(r));
     r.k.s = stream;
@@ -502,6 +510,21 @@ int wso_run(const uint8_t* stream, uint64_t len, const uint64_t* chunk_ends, uin
             decode_packet(&r);
             if (unmasked_stall(&r.c) || (r.k.rpos == before && r.n_ev == ev_before && !r.c.closed)) {
                 stalled = 1;   /* Q3: EAGAIN without reading anything: epoll would spin forever */
+                break;
+            }
+        }
+    }
+    if ((flags & WSO_RUN_EOF) && !r.c.closed && !stalled) {
+        /* the peer closed: epoll keeps reporting the fd readable and each DecodePacket reads
+         * what is left, until a read returns 0 -> io.EOF -> Close() (epoll.go:108-110) */
+        r.k.avail = len;
+        r.k.eof = 1;
+        while (!r.c.closed) {
+            uint64_t before = r.k.rpos;
+            uint32_t ev_before = r.n_ev;
+            decode_packet(&r);
+            if (unmasked_stall(&r.c) || (r.k.rpos == before && r.n_ev == ev_before && !r.c.closed)) {
+                stalled = 1;
                 break;
             }
         }

@@ -110,6 +110,16 @@ int wso_run(const uint8_t* stream, uint64_t len, const uint64_t* chunk_ends, uin
             wso_event* ev, uint32_t ev_cap, wso_frame* fr, uint32_t fr_cap,
             uint8_t* arena, uint64_t arena_cap, wso_result* res);
 
+/* wso_run with flags: WSO_RUN_EOF -- after the last chunk the peer closes: the next read returns
+ * 0, which BaseConnect.Read maps to io.EOF (baseconnect.go:100-103) and the poller answers with
+ * Close() = CloseCode(1000, "") (epoll.go:108-110, websocket.go:401-404).  Level-triggered epoll
+ * reports the EOF as readable, so DecodePacket is called until it returns that error. */
+#define WSO_RUN_EOF 1u
+int wso_run_ex(const uint8_t* stream, uint64_t len, const uint64_t* chunk_ends, uint32_t n_chunks,
+               uint64_t max_frame_len, uint8_t* inplace,
+               wso_event* ev, uint32_t ev_cap, wso_frame* fr, uint32_t fr_cap,
+               uint8_t* arena, uint64_t arena_cap, wso_result* res, uint32_t flags);
+
 /* Go 1.16 utf8.Valid restated */
 int wso_utf8_valid(const uint8_t* p, uint64_t n);
 

@@ -62,8 +62,19 @@ def _ext_for(rng, n):
     return None
 
 
+def _big_pong(rng):
+    """a PONG payload of any size (the reference has no limit, websocket.go:191-205): ASCII (valid
+    UTF-8 under a TEXT message, Q6) or random bytes (almost surely invalid there -> 1007)"""
+    n = int(rng.choice([126, 300, 4095, 4096, 9000, 70000]))
+    if rng.random() < 0.7:
+        return bytes(rng.integers(0x20, 0x7F, n, dtype=np.uint8))
+    return rng.bytes(n)
+
+
 def random_stream(seed: int, n_units: int = 20, err_p: float = 0.03, big_p: float = 0.02,
-                  text_p: float = 0.3) -> bytes:
+                  text_p: float = 0.3, pong_big_p: float = 0.0) -> bytes:
+    """pong_big_p: chance per unit of a large PONG (and between fragments of a message) -- 0 keeps
+    the streams of earlier rounds byte for byte (no extra draws)"""
     rng = np.random.default_rng(seed)
     out = bytearray()
 
@@ -92,6 +103,9 @@ def random_stream(seed: int, n_units: int = 20, err_p: float = 0.03, big_p: floa
             elif kind == 10: F(OP_PONG, b"")
             else: F(OP_PONG, b"x", fin=False)
             continue
+        if pong_big_p and rng.random() < pong_big_p:
+            F(OP_PONG, _big_pong(rng))
+            continue
         if r < 0.10:
             F(OP_PING, _ctrl_payload(rng, 126))
         elif r < 0.15:
@@ -112,6 +126,8 @@ def random_stream(seed: int, n_units: int = 20, err_p: float = 0.03, big_p: floa
                   fin=(i == len(pieces) - 1))
                 if i < len(pieces) - 1 and rng.random() < 0.15:
                     F(OP_PING, _ctrl_payload(rng, 20))
+                if pong_big_p and i < len(pieces) - 1 and rng.random() < pong_big_p:
+                    F(OP_PONG, _big_pong(rng))       # Q6: checked alone under a TEXT message
                 if i < len(pieces) - 1 and rng.random() < 0.01:
                     F(OP_CLOSE, (1000).to_bytes(2, "big") + b"frag", fin=False)   # Q7 quirk
         else:

@@ -52,6 +52,8 @@ def lib():
         _lib.wso_run.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint32, C.c_uint64,
                                  C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32,
                                  C.c_void_p, C.c_uint64, C.POINTER(WsoResult)]
+        _lib.wso_run_ex.restype = C.c_int
+        _lib.wso_run_ex.argtypes = _lib.wso_run.argtypes + [C.c_uint32]
         _lib.wso_utf8_valid.restype = C.c_int
         _lib.wso_utf8_valid.argtypes = [C.c_void_p, C.c_uint64]
         _lib.wso_encode.restype = C.c_uint64
@@ -86,9 +88,10 @@ class OracleOut:
 MAX_FRAME_LEN = (1 << 40) - 1   # wsc_config_default's max_frame_len (the 40-bit record, Q4)
 
 
-def run(stream: bytes, chunk_ends=None, max_frame_len=MAX_FRAME_LEN, cap=None) -> OracleOut:
+def run(stream: bytes, chunk_ends=None, max_frame_len=MAX_FRAME_LEN, cap=None, eof=False) -> OracleOut:
     """cap: room for that many events / frame log lines (default: enough for any stream of
-    this length -- n / 2; pass a bound for streams of a few large frames)"""
+    this length -- n / 2; pass a bound for streams of a few large frames).
+    eof: the peer closes after the stream (a read returns 0 -> io.EOF -> Close(), epoll.go:108-110)"""
     L = lib()
     s = np.frombuffer(stream, dtype=np.uint8) if stream else np.zeros(1, np.uint8)
     n = len(stream)
@@ -104,9 +107,9 @@ def run(stream: bytes, chunk_ends=None, max_frame_len=MAX_FRAME_LEN, cap=None) -
     if chunk_ends is not None:
         ce = np.ascontiguousarray(chunk_ends, dtype=np.uint64)
         nc = len(ce)
-    rc = L.wso_run(s.ctypes.data, n, ce.ctypes.data if ce is not None else None, nc, max_frame_len,
-                   inplace.ctypes.data, C.cast(ev, C.c_void_p), ev_cap, fr.ctypes.data, fr_cap,
-                   arena.ctypes.data, len(arena), C.byref(res))
+    rc = L.wso_run_ex(s.ctypes.data, n, ce.ctypes.data if ce is not None else None, nc, max_frame_len,
+                      inplace.ctypes.data, C.cast(ev, C.c_void_p), ev_cap, fr.ctypes.data, fr_cap,
+                      arena.ctypes.data, len(arena), C.byref(res), 1 if eof else 0)
     assert rc == 0, "oracle output overflow"
     events = []
     for i in range(res.n_events):

@@ -38,6 +38,8 @@ struct Conn {
     std::vector<std::vector<uint8_t>> got;
     size_t fed = 0;
     bool removed = false;
+    bool eof = false;      // wsc_session_eof after its last byte: Close() must come last, after every message
+    bool closed = false;
 };
 
 Conn make_conn(size_t n_msgs, size_t max_len) {
@@ -54,6 +56,11 @@ Conn make_conn(size_t n_msgs, size_t max_len) {
             if (rnd(2)) { uint8_t pp[3] = {1, 2, 3}; put_frame(c.wire, 0x89, pp, rnd(4)); }
             put_frame(c.wire, 0x80, msg.data() + cut, msg.size() - cut);
         }
+        if (rnd(4) == 0) {   // a PONG of any size (up to 3x the largest message): streamed like data (ABI 4)
+            std::vector<uint8_t> pong(1 + rnd(3 * max_len));
+            for (auto& x : pong) x = (uint8_t)rng();
+            put_frame(c.wire, 0x8A, pong.data(), pong.size());
+        }
         c.sent.push_back(std::move(msg));
     }
     return c;
@@ -69,8 +76,14 @@ void drain(wsc_session* s, Conn& c) {
         if (rc == WSC_E_STATE) { CHECK(c.removed); return; }
         CHECK(rc == WSC_OK);
         if (ev.type == WSC_EV_NONE) return;
-        if (ev.type == WSC_EV_MESSAGE) c.got.emplace_back(ev.data, ev.data + ev.len);
-        CHECK(ev.type != WSC_EV_CLOSE || c.removed);
+        if (ev.type == WSC_EV_MESSAGE) {
+            CHECK(!c.closed);
+            c.got.emplace_back(ev.data, ev.data + ev.len);
+        }
+        if (ev.type == WSC_EV_CLOSE) {   // only the EOF's Close(), once, after every message
+            CHECK(c.removed || (c.eof && ev.close_code == 1000 && ev.err == 0 && !c.closed));
+            c.closed = true;
+        }
     }
 }
 
@@ -132,6 +145,11 @@ void phase(uint64_t batch_bytes, uint32_t max_frames, int mode, size_t n_conns, 
                 }
             }
             c.fed += n;
+            if (c.fed == c.wire.size() && i % 2 == 1 && !c.removed) {   // the peer closes after its last byte
+                const int rc = wsc_session_eof(s, c.h);
+                CHECK(rc == WSC_OK);
+                c.eof = true;
+            }
             fed.push_back(i);
             any = true;
         }
@@ -171,6 +189,7 @@ void phase(uint64_t batch_bytes, uint32_t max_frames, int mode, size_t n_conns, 
                              (unsigned long long)batch_bytes, max_frames, c.got.size(), c.sent.size(), c.fed, c.wire.size());
             CHECK(c.got.size() == c.sent.size());
             for (size_t i = 0; i < c.got.size() && i < c.sent.size(); ++i) CHECK(c.got[i] == c.sent[i]);
+            CHECK(c.closed == c.eof);
         }
     }
     CHECK(wsc_session_destroy(s) == WSC_OK);

@@ -86,6 +86,9 @@ static void walk(const wsc_ctx* c, uint8_t* w, uint64_t a, uint64_t b, uint32_t 
         xor_run(w + pos, take, st.frame_mask);
         if (take < st.frame_rem) {
             f.kind = WSC_FK_PIECE;
+        } else if (op == 10) {   // a streamed PONG completes: discarded
+            f.kind = WSC_FK_PONG;
+            st.msg_id += 1;
         } else if (fin) {
             f.kind = WSC_FK_MESSAGE;
             if (op == 0 && st.cont_len) f.flags |= WSC_FF_CONT_MSG;
@@ -144,7 +147,7 @@ static void walk(const wsc_ctx* c, uint8_t* w, uint64_t a, uint64_t b, uint32_t 
         uint64_t take = plen;
         bool piece = false;
         if (b - pos < hl + plen) {
-            if (!data || bad) break;   // control frames wait whole (the stand-in checks errors first)
+            if ((!data && op != 10) || bad) break;   // PING / CLOSE wait whole (errors checked first)
             take = b - pos - hl;
             piece = true;
         }
@@ -189,6 +192,12 @@ static void walk(const wsc_ctx* c, uint8_t* w, uint64_t a, uint64_t b, uint32_t 
         } else if (op == 9) {
             f.kind = WSC_FK_PING;
             st.msg_id += 1;
+        } else if (op == 10 && piece) {   // a PONG streams like a data frame (ABI 4)
+            f.kind = WSC_FK_PIECE;
+            st.frame_rem = plen - take;
+            st.frame_len = plen;
+            st.frame_mask = rotr(mask, 8 * (uint32_t)(take & 3));
+            st.frame_hdr = (uint8_t)(fin << 7 | op);
         } else if (op == 10) {
             f.kind = plen ? WSC_FK_PONG : WSC_FK_PONG_EMPTY;
             if (plen) st.msg_id += 1;

@@ -28,11 +28,12 @@ def test_struct_sizes_match_header(codec_lib):
     assert C.sizeof(K.WscConfig) == 40
     assert C.sizeof(K.WscBatch) == 96
     assert C.sizeof(K.WscEvent) == 40
+    assert C.sizeof(K.WscConnState) == 40 and K.CONN_STATE_DTYPE.itemsize == 40
     assert K.FRAME_DTYPE.itemsize == 32 and K.SEG_RESULT_DTYPE.itemsize == 32
 
 
 def test_config_default_and_version(codec_lib):
-    assert codec_lib.wsc_abi_version() == K.ABI_VERSION == 3
+    assert codec_lib.wsc_abi_version() == K.ABI_VERSION == 4
     cfg = K.default_config()
     assert cfg.max_frame_len == (1 << 40) - 1 and cfg.unmask_window == 4096
 

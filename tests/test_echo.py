@@ -34,6 +34,15 @@ def test_cpu_echo_roundtrip(cpu_echo, args):
     assert d["messages"] == int(args[1]) * int(args[3])
 
 
+@pytest.mark.parametrize("pollers", ["1", "4"])
+def test_cpu_echo_shutdown(cpu_echo, pollers):
+    """clients half-close after their last frame: every echo, then the close frame, then FIN"""
+    rc, d = _run(cpu_echo, "--conns", "16", "--frames", "40", "--size", "5000", "--client-threads", "4",
+                 "--pollers", pollers, "--shutdown")
+    assert rc == 0 and d["ok"] and d["shutdown"], d
+    assert d["messages"] == 16 * 40
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("args", [("--conns", "1", "--frames", "200", "--size", "65536"),
                                   ("--conns", "32", "--frames", "50", "--size", "70000", "--client-threads", "4"),
@@ -51,3 +60,23 @@ def test_gpu_echo_roundtrip(codec_lib, args):
     assert rc == 0 and d["ok"], d
     assert d["messages"] == int(args[1]) * int(args[3])
     assert d["pollers"] == (int(args[args.index("--pollers") + 1]) if "--pollers" in args else 1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("args", [("--pollers", "1"), ("--pollers", "4"), ("--pollers", "4", "--sync"),
+                                  ("--pollers", "1", "--conns", "1", "--frames", "300", "--size", "65536")])
+def test_gpu_echo_shutdown_delivers_before_close(codec_lib, args):
+    """clients send N messages then shutdown(SHUT_WR); the server's read returns 0
+    (io.EOF) while messages are still queued or in flight -- every one is echoed, then Close():
+    the close frame 88 02 03 E8, then the server's FIN (the client checks all of it)"""
+    from netman_amd import _build
+    exe = _build.build_tools()
+    base = {"--conns": "16", "--frames": "60", "--size": "20000", "--client-threads": "4"}
+    a = list(args)
+    for k, v in base.items():
+        if k not in a:
+            a += [k, v]
+    rc, d = _run(exe, *a, "--shutdown", "--devices", "1")
+    assert rc == 0 and d["ok"] and d["shutdown"], d
+    assert d["messages"] == int(a[a.index("--conns") + 1]) * int(a[a.index("--frames") + 1])
+    assert d["devices"] == 1

@@ -184,3 +184,29 @@ def test_text_1k_several_failures_per_connection(codec_lib, compact):
         assert int((res.seg["status"] == K.SEG_ERROR).sum()) > 0
     finally:
         c.close()
+
+
+def test_rejected_geometry_leaves_utf8_counters_consistent(codec_lib, monkeypatch):
+    """round-3 ADVICE (medium): a decode refused by the walk-geometry guard (WSC_WALK_MODE=16 with
+    more segments than the look-back state holds) must not flip the UTF-8 item-counter parity nor
+    commit its geometry -- the next decodes' chip-wide 1007 verdicts must stay exact"""
+    monkeypatch.setenv("WSC_WALK_MODE", "16")
+    monkeypatch.setenv("WSC_U8_INLINE_MAX", "0")
+    c = K.Codec(0, max_batch_bytes=8 << 20, max_segs=1 << 15, max_frames=1 << 17)
+    try:
+        many = [synth.frame(2, b"x", mask=i) for i in range(1 << 15)]
+        wire, off = pack_streams(many)
+        with pytest.raises(K.WscError) as ei:
+            c.decode_host(wire, off)
+        assert ei.value.rc == K.WSC_E_INTERNAL
+        rng = np.random.default_rng(5)
+        for rnd in range(3):
+            streams = [random_stream(9100 + 37 * rnd + i, n_units=20, text_p=0.9, err_p=0.05) for i in range(64)]
+            bad = bytearray(synth.utf8_units(rng, 300)) + b"\xff"
+            streams += [synth.frame(1, bytes(bad), mask=3) + synth.frame(2, b"after")] * 4
+            _check(c, streams)
+            if rnd == 0:   # a second refusal between good decodes
+                with pytest.raises(K.WscError):
+                    c.decode_host(wire, off)
+    finally:
+        c.close()

@@ -153,3 +153,36 @@ def test_inplace_unmask_matches_restatement():
     s = frame(2, data, mask=0xA1B2C3D4)
     out = O.run(s)
     assert out.inplace[8:] == data and out.inplace[:8] == s[:8]
+
+
+# ---- round 4: PONG payloads of any size, and EOF ordering (oracle semantics, no GPU) -----------
+def test_pong_any_size_accumulates_over_reads():
+    """websocket.go:191-205 has no length check for PONG; nextFrame accumulates it over reads
+    (websocket_frame.go:16-31): a 300 B and a 70 kB PONG read in 1000-byte chunks are consumed,
+    count in msgID (Q5), and the next message follows; under an open TEXT message the PONG's
+    payload alone must be valid UTF-8 (Q6)"""
+    rng = np.random.default_rng(4)
+    s = (frame(10, bytes(300), mask=1) + frame(10, rng.bytes(70_000), mask=2) + frame(2, b"next", mask=3))
+    chunks = list(range(1000, len(s), 1000)) + [len(s)]
+    out = O.run(s, chunk_ends=chunks)
+    assert [(e.type, e.msg_id, e.data) for e in out.events] == [(O.EV_MESSAGE, 2, b"next")]
+    assert [int(f["kind"]) for f in out.frames] == [3, 3, 1]
+    bad = frame(1, b"a", fin=False, mask=1) + frame(10, b"ok" * 100 + b"\xff", mask=2) + frame(0, b"b", mask=3)
+    assert [(e.type, e.close_code, e.err) for e in O.run(bad, chunk_ends=[50, len(bad)]).events] == [(O.EV_CLOSE, 1007, 5)]
+
+
+@pytest.mark.parametrize("tail,closes", [(b"", True), (b"\x82", True), (frame(2, bytes(5000), mask=9)[:3000], True),
+                                         (frame(8, b"\x03\xe8", mask=4), False)])
+def test_eof_after_every_earlier_frame(tail, closes):
+    """BaseConnect.Read: n == 0 -> io.EOF (baseconnect.go:100-103) -> Close() (epoll.go:108-110),
+    reached only once every earlier frame is delivered; a torn frame or header at the EOF is dropped;
+    after a CLOSE frame the connection is already closed and no EOF is seen"""
+    s = frame(2, b"one", mask=1) + frame(1, "zwei ✓".encode(), mask=2) + tail
+    plain = O.run(s).events
+    out = O.run(s, eof=True).events
+    if closes:
+        assert [e.key() for e in out[:-1]] == [e.key() for e in plain]
+        assert (out[-1].type, out[-1].close_code, out[-1].err) == (O.EV_CLOSE, 1000, 0)
+    else:
+        assert [e.key() for e in out] == [e.key() for e in plain]
+    assert [e.data for e in out if e.type == O.EV_MESSAGE] == [b"one", "zwei ✓".encode()]

@@ -11,7 +11,11 @@
 // examples/websocket handler's connect.Binary(message.Bytes()) (examples/websocket/server.go:30-44,
 // encode at server/websocket_ctrl.go:23-70; the handler's fmt.Println is left out).  Client
 // threads send `frames` masked 0x82 frames of `frame_bytes` per connection and check every echoed
-// byte.
+// byte.  With `shutdown` set each client half-closes its socket (shutdown(SHUT_WR)) right after its
+// last frame: the server reads 0 bytes (BaseConnect.Read -> io.EOF, baseconnect.go:100-103), must
+// still echo every message read before it, and only then Close()s -- CloseCode(1000, "") sends a
+// close frame 88 02 03 E8 and closes the fd (epoll.go:108-110, websocket_ctrl.go:99-119); the client
+// checks all of it.
 //
 // The Decoder is what the two binaries differ in:
 //   tools/ws_echo.cpp       product path: libwscodec's wsc_session, one batched device decode per round
@@ -42,12 +46,17 @@
 
 namespace echo {
 
+enum : int { EV_NONE = 0, EV_MESSAGE = 1, EV_CLOSE = 2 };
+
 struct Decoder {
     virtual ~Decoder() = default;
     virtual int open() = 0;                                               // newWebsocketProtocol
     virtual void feed(int conn, const uint8_t* p, size_t n) = 0;          // one bulk read
     virtual void decode() = 0;                                            // once per poller round
-    virtual bool next(int conn, const uint8_t** data, size_t* len) = 0;   // DecodePacket() -> message
+    // DecodePacket(): EV_MESSAGE (data/len), EV_CLOSE (Close(): send the close frame, close the fd)
+    // or EV_NONE (EAGAIN)
+    virtual int next(int conn, const uint8_t** data, size_t* len) = 0;
+    virtual void eof(int conn) = 0;                                       // a read returned 0
     // optional zero-copy read: room for the connection's next read (recv straight into it)
     virtual bool reserve(int, size_t, uint8_t**, size_t*) { return false; }
     virtual void commit(int, size_t) {}
@@ -91,12 +100,19 @@ struct ServerConn {
     std::vector<uint8_t> out;   // echo bytes not yet written
     size_t out_pos = 0;
     bool want_out = false;
+    bool read_eof = false;      // recv() returned 0: the decoder was told, EPOLLIN dropped
+    bool closing = false;       // Close(): the close frame is queued, the fd closes once it is sent
+    bool closed = false;
 };
 
-using DecoderFactory = std::function<std::unique_ptr<Decoder>(int conns_of_poller)>;
+// the close frame CloseCode(1000, "") sends: 0x88, length 2, code 1000 big-endian
+constexpr uint8_t CLOSE_1000[4] = {0x88, 0x02, 0x03, 0xE8};
+
+// decoder for poller p of P, serving `conns_of_poller` connections
+using DecoderFactory = std::function<std::unique_ptr<Decoder>(int poller, int conns_of_poller)>;
 
 inline Result run(const DecoderFactory& make_decoder, int pollers, int conns, int frames, size_t frame_bytes,
-                  int client_threads, int timeout_s = 60) {
+                  int client_threads, int timeout_s = 60, bool shutdown_wr = false) {
     Result res;
     const int lfd = socket(AF_INET, SOCK_STREAM, 0);
     int one = 1;
@@ -169,6 +185,7 @@ inline Result run(const DecoderFactory& make_decoder, int pollers, int conns, in
             std::vector<size_t> sent(fds.size(), 0);
             std::vector<std::vector<uint8_t>> inbuf(fds.size());
             std::vector<int> got(fds.size(), 0);
+            std::vector<char> peer_eof(fds.size(), 0), fin(fds.size(), 0);
             size_t done = 0;
             std::vector<uint8_t> rb(1 << 20);
             epoll_event evs[256];
@@ -194,16 +211,18 @@ inline Result run(const DecoderFactory& make_decoder, int pollers, int conns, in
                             e.events = EPOLLIN;
                             e.data.u64 = i;
                             epoll_ctl(ep, EPOLL_CTL_MOD, fds[i], &e);
+                            if (shutdown_wr) shutdown(fds[i], SHUT_WR);   // the peer is done sending
                         }
                     }
                     if (evs[k].events & EPOLLIN) {
                         while (true) {
                             const ssize_t r = recv(fds[i], rb.data(), rb.size(), 0);
+                            if (r == 0) peer_eof[i] = 1;
                             if (r <= 0) break;
                             inbuf[i].insert(inbuf[i].end(), rb.data(), rb.data() + r);
                         }
                         size_t p = 0;   // every complete echoed frame must equal header + payload
-                        while (inbuf[i].size() - p >= frame_out) {
+                        while (got[i] < frames && inbuf[i].size() - p >= frame_out) {
                             const uint8_t* f = inbuf[i].data() + p;
                             if (std::memcmp(f, want_h, want_hl) || std::memcmp(f + want_hl, payload.data(), frame_bytes)) {
                                 client_fail++;
@@ -211,9 +230,20 @@ inline Result run(const DecoderFactory& make_decoder, int pollers, int conns, in
                             }
                             p += frame_out;
                             client_msgs++;
-                            if (++got[i] == frames) done++;
+                            if (++got[i] == frames && !shutdown_wr) done++;
                         }
                         inbuf[i].erase(inbuf[i].begin(), inbuf[i].begin() + (long)p);
+                        if (shutdown_wr && !fin[i] && peer_eof[i]) {
+                            // all echoes, then exactly the close frame, then the server's FIN
+                            if (got[i] != frames || inbuf[i].size() != sizeof(CLOSE_1000) ||
+                                std::memcmp(inbuf[i].data(), CLOSE_1000, sizeof(CLOSE_1000))) {
+                                client_fail++;
+                            } else {
+                                fin[i] = 1;
+                                done++;
+                                epoll_ctl(ep, EPOLL_CTL_DEL, fds[i], nullptr);
+                            }
+                        }
                     }
                 }
             }
@@ -234,7 +264,7 @@ inline Result run(const DecoderFactory& make_decoder, int pollers, int conns, in
     if (pollers > conns) pollers = conns;
     std::vector<Poller> pl(pollers);
     for (int p = 0; p < pollers; ++p) {
-        pl[p].dec = make_decoder(conns / pollers + (p < conns % pollers ? 1 : 0));
+        pl[p].dec = make_decoder(p, conns / pollers + (p < conns % pollers ? 1 : 0));
         pl[p].ep = epoll_create1(0);
     }
     for (int i = 0; i < conns && client_fail.load() == 0; ++i) {
@@ -272,12 +302,21 @@ inline Result run(const DecoderFactory& make_decoder, int pollers, int conns, in
         // messages are echoed, so the device decodes while this thread builds and sends the replies
         const bool pipe = dec.pipelined();
         std::vector<size_t> drain;   // connections whose messages are ready to echo (previous round)
+        std::vector<size_t> eofs;    // read side closed, Close() not yet delivered: drained every round
+        size_t n_closed = 0;
         auto echo_round = [&](const std::vector<size_t>& conns_ready) {
             for (size_t q : conns_ready) {   // every delivered message is echoed
                 ServerConn& c = sc[q];
+                if (c.closing) continue;
                 const uint8_t* d;
                 size_t len;
-                while (dec.next(c.id, &d, &len)) {
+                int k;
+                while ((k = dec.next(c.id, &d, &len)) != EV_NONE) {
+                    if (k == EV_CLOSE) {      // Close() -> CloseCode(1000, ""): close frame, then the fd
+                        c.out.insert(c.out.end(), CLOSE_1000, CLOSE_1000 + sizeof(CLOSE_1000));
+                        c.closing = true;
+                        break;
+                    }
                     uint8_t h[10];
                     const size_t hl = put_header(h, 0x82, len);
                     c.out.insert(c.out.end(), h, h + hl);
@@ -287,7 +326,8 @@ inline Result run(const DecoderFactory& make_decoder, int pollers, int conns, in
                 }
             }
         };
-        while (P.error.empty() && P.served < want && client_fail.load() == 0) {
+        auto all_done = [&] { return shutdown_wr ? n_closed == sc.size() : P.served >= want; };
+        while (P.error.empty() && !all_done() && client_fail.load() == 0) {
             if (std::chrono::steady_clock::now() > deadline) {
                 P.error = "server timeout";
                 break;
@@ -295,24 +335,39 @@ inline Result run(const DecoderFactory& make_decoder, int pollers, int conns, in
             const int n = epoll_wait(P.ep, evs, 1024, pipe && !drain.empty() ? 0 : 100);
             fed.clear();
             for (int k = 0; k < n; ++k) {
-                ServerConn& c = sc[evs[k].data.u64];
-                if (evs[k].events & EPOLLIN) {
+                const size_t q = evs[k].data.u64;
+                ServerConn& c = sc[q];
+                if ((evs[k].events & EPOLLIN) && !c.read_eof && !c.closed) {
                     uint8_t* p = nullptr;
                     size_t avail = 0;
+                    ssize_t r;
                     if (dec.reserve(c.id, rb.size(), &p, &avail)) {   // ONE bulk read per event, into pinned staging
-                        const ssize_t r = recv(c.fd, p, avail, 0);
+                        r = recv(c.fd, p, avail, 0);
                         dec.commit(c.id, r > 0 ? (size_t)r : 0);
-                        if (r > 0) fed.push_back(evs[k].data.u64);
+                        if (r > 0) fed.push_back(q);
                     } else {
-                        const ssize_t r = recv(c.fd, rb.data(), rb.size(), 0);   // ONE bulk read per event
+                        r = recv(c.fd, rb.data(), rb.size(), 0);   // ONE bulk read per event
                         if (r > 0) {
                             dec.feed(c.id, rb.data(), (size_t)r);
-                            fed.push_back(evs[k].data.u64);
+                            fed.push_back(q);
                         }
+                    }
+                    if (r == 0) {   // io.EOF: the decoder delivers what was read, then Close()
+                        dec.eof(c.id);
+                        c.read_eof = true;
+                        eofs.push_back(q);
+                        epoll_event e{};   // level-triggered EOF would fire forever: stop reading
+                        e.events = c.want_out ? EPOLLOUT : 0u;
+                        e.data.u64 = q;
+                        epoll_ctl(P.ep, EPOLL_CTL_MOD, c.fd, &e);
                     }
                 }
             }
-            if (pipe) {
+            // pipelined decoders pipeline only rounds of several connections: a round of one
+            // connection waits for its own batch either way, and the synchronous call saves the
+            // second staging set's hand-off
+            const bool pipe_round = pipe && fed.size() > 1;
+            if (pipe_round) {
                 if (!fed.empty() || dec.pending()) {
                     dec.submit();          // round r+1 on the device ...
                     P.rounds++;
@@ -321,14 +376,24 @@ inline Result run(const DecoderFactory& make_decoder, int pollers, int conns, in
                 dec.complete();
                 drain = fed;
             } else {
-                if (!fed.empty()) {
-                    dec.decode();
+                if (!fed.empty() || dec.pending()) {
+                    dec.decode();          // (an earlier pipelined batch completes first)
                     P.rounds++;
                 }
+                echo_round(drain);
+                drain.clear();
                 echo_round(fed);
+            }
+            if (!eofs.empty()) {
+                echo_round(eofs);
+                size_t w = 0;
+                for (size_t q : eofs)
+                    if (!sc[q].closing) eofs[w++] = q;
+                eofs.resize(w);
             }
             for (size_t i = 0; i < sc.size(); ++i) {
                 ServerConn& c = sc[i];
+                if (c.closed) continue;
                 while (c.out_pos < c.out.size()) {   // until the socket buffer is full
                     const ssize_t w = send(c.fd, c.out.data() + c.out_pos, c.out.size() - c.out_pos, MSG_NOSIGNAL);
                     if (w <= 0) break;
@@ -339,9 +404,17 @@ inline Result run(const DecoderFactory& make_decoder, int pollers, int conns, in
                     c.out_pos = 0;
                 }
                 const bool need = c.out_pos < c.out.size();
+                if (c.closing && !need) {   // the close frame is out: unix.Close(fd) (websocket_ctrl.go:117)
+                    epoll_ctl(P.ep, EPOLL_CTL_DEL, c.fd, nullptr);
+                    close(c.fd);
+                    c.fd = -1;
+                    c.closed = true;
+                    ++n_closed;
+                    continue;
+                }
                 if (need != c.want_out) {
                     epoll_event e{};
-                    e.events = EPOLLIN | (need ? EPOLLOUT : 0u);
+                    e.events = (c.read_eof ? 0u : EPOLLIN) | (need ? EPOLLOUT : 0u);
                     e.data.u64 = i;
                     epoll_ctl(P.ep, EPOLL_CTL_MOD, c.fd, &e);
                     c.want_out = need;
@@ -350,7 +423,7 @@ inline Result run(const DecoderFactory& make_decoder, int pollers, int conns, in
         }
         // flush what is left (the clients check every echo)
         for (auto& c : sc) {
-            while (c.out_pos < c.out.size() && client_fail.load() == 0 && P.error.empty()) {
+            while (!c.closed && c.out_pos < c.out.size() && client_fail.load() == 0 && P.error.empty()) {
                 const ssize_t w = send(c.fd, c.out.data() + c.out_pos, c.out.size() - c.out_pos, MSG_NOSIGNAL);
                 if (w > 0) c.out_pos += (size_t)w;
                 else std::this_thread::yield();
@@ -372,7 +445,8 @@ inline Result run(const DecoderFactory& make_decoder, int pollers, int conns, in
         res.payload_bytes += P.payload;
         res.rounds += P.rounds;
         if (res.error.empty() && !P.error.empty()) res.error = P.error;
-        for (auto& c : P.sc) close(c.fd);
+        for (auto& c : P.sc)
+            if (c.fd >= 0) close(c.fd);
         close(P.ep);
         P.dec.reset();
     }
@@ -383,14 +457,22 @@ inline Result run(const DecoderFactory& make_decoder, int pollers, int conns, in
     return res;
 }
 
-inline void print_json(const char* codec, const Result& r, int pollers, int conns, int frames, size_t frame_bytes) {
-    printf("{\"codec\": \"%s\", \"ok\": %s, \"pollers\": %d, \"connections\": %d, \"frames_per_conn\": %d, \"frame_bytes\": %zu, "
+inline void print_json(const char* codec, const Result& r, int pollers, int conns, int frames, size_t frame_bytes,
+                       int devices = 0, bool shutdown_wr = false) {
+    printf("{\"codec\": \"%s\", \"devices\": %d, \"shutdown\": %s, \"ok\": %s, \"pollers\": %d, \"connections\": %d, \"frames_per_conn\": %d, \"frame_bytes\": %zu, "
            "\"seconds\": %.4f, \"messages\": %llu, \"msgs_per_s\": %.1f, \"gib_s\": %.3f, \"rounds\": %llu, "
            "\"error\": \"%s\"}\n",
-           codec, r.ok ? "true" : "false", pollers, conns, frames, frame_bytes, r.seconds, (unsigned long long)r.messages,
+           codec, devices, shutdown_wr ? "true" : "false", r.ok ? "true" : "false", pollers, conns, frames, frame_bytes,
+           r.seconds, (unsigned long long)r.messages,
            r.seconds > 0 ? (double)r.messages / r.seconds : 0.0,
            r.seconds > 0 ? (double)r.payload_bytes / r.seconds / 1073741824.0 : 0.0, (unsigned long long)r.rounds,
            r.error.c_str());
+}
+
+inline bool has_flag(int argc, char** argv, const char* flag) {
+    for (int i = 1; i < argc; ++i)
+        if (std::string(argv[i]) == flag) return true;
+    return false;
 }
 
 inline void parse_args(int argc, char** argv, int& conns, int& frames, size_t& frame_bytes, int& threads,

@@ -2,9 +2,14 @@
 // (the DecodePacket mirror above the C ABI) decodes every round's bulk reads in ONE batched device
 // pass on the MI355X.  Harness: tools/echo_harness.hpp.  The CPU baseline twin is
 // oracle/ws_echo_cpu.cpp.  Prints one JSON line.
-//   ws_echo [--pollers P] [--conns C] [--frames N] [--size BYTES] [--client-threads T] [--sync]
-// --pollers P: P poller threads, each with its own wsc_session on the same device (netman runs
-// NumCPU pollers, eventloop/event.go:33-37); connection i belongs to poller i % P.
+//   ws_echo [--pollers P] [--devices G] [--conns C] [--frames N] [--size BYTES] [--client-threads T]
+//           [--sync] [--shutdown]
+// --pollers P: P poller threads, each with its own wsc_session (netman runs NumCPU pollers,
+// eventloop/event.go:33-37); connection i belongs to poller i % P.
+// --devices G: poller p's session lives on device p % G (one host thread, stream and
+// pinned staging per GPU; connections never move between devices).  Default 1.
+// --shutdown: clients half-close after their last frame; the server must echo everything, then
+// Close() (wsc_session_eof, the EOF rule in include/wscodec.h).
 #include "../include/wscodec.h"
 #include "echo_harness.hpp"
 
@@ -13,14 +18,14 @@ namespace {
 struct GpuDecoder : echo::Decoder {
     wsc_session* s = nullptr;
     wsc_event ev{};
-    GpuDecoder(int conns, bool pipelined) : pipe(pipelined) {
+    GpuDecoder(int device, int conns, bool pipelined) : pipe(pipelined) {
         wsc_config cfg;
         wsc_config_default(&cfg);
         // one device batch per poller round: its connections' 4 MiB reads (+ a margin)
         cfg.max_batch_bytes = (uint64_t)(conns < 4 ? 4 : conns) * (5ull << 20);
         cfg.max_segs = (uint32_t)conns + 16;
         cfg.max_frames = 1u << 18;
-        if (wsc_session_create(0, &cfg, 0, &s) != WSC_OK) {
+        if (wsc_session_create(device, &cfg, 0, &s) != WSC_OK) {
             fprintf(stderr, "wsc_session_create: %s\n", wsc_last_error());
             exit(2);
         }
@@ -55,17 +60,19 @@ struct GpuDecoder : echo::Decoder {
         }
     }
     bool pipe;
-    bool next(int conn, const uint8_t** data, size_t* len) override {
+    int next(int conn, const uint8_t** data, size_t* len) override {
         while (true) {
-            wsc_session_next(s, (uint32_t)conn, &ev);
-            if (ev.type == WSC_EV_NONE) return false;
+            if (wsc_session_next(s, (uint32_t)conn, &ev) != WSC_OK) return echo::EV_NONE;
+            if (ev.type == WSC_EV_NONE) return echo::EV_NONE;
             if (ev.type == WSC_EV_MESSAGE) {
                 *data = ev.data;
                 *len = ev.len;
-                return true;
+                return echo::EV_MESSAGE;
             }
+            if (ev.type == WSC_EV_CLOSE || ev.type == WSC_EV_STALL) return echo::EV_CLOSE;
         }
     }
+    void eof(int conn) override { check(wsc_session_eof(s, (uint32_t)conn), "wsc_session_eof"); }
 };
 
 }  // namespace
@@ -74,14 +81,19 @@ int main(int argc, char** argv) {
     int conns = 1, frames = 4000, threads = 1, pollers = 1;
     size_t size = 65536;
     echo::parse_args(argc, argv, conns, frames, size, threads, pollers);
-    bool pipe = true;
-    for (int i = 1; i < argc; ++i)
-        if (std::string(argv[i]) == "--sync") pipe = false;   // one synchronous decode per round
+    const bool pipe = !echo::has_flag(argc, argv, "--sync");   // --sync: one synchronous decode per round
+    const bool shut = echo::has_flag(argc, argv, "--shutdown");
+    int devices = 1;
+    for (int i = 1; i + 1 < argc; ++i)
+        if (std::string(argv[i]) == "--devices") devices = atoi(argv[i + 1]);
+    if (devices < 1) devices = 1;   // (more than visible: wsc_session_create fails, exit 2)
     const echo::Result r = echo::run(
-        [pipe](int n) { return std::unique_ptr<echo::Decoder>(new GpuDecoder(n, pipe)); }, pollers, conns, frames,
-        size, threads);
+        [pipe, devices](int poller, int n) {
+            return std::unique_ptr<echo::Decoder>(new GpuDecoder(poller % devices, n, pipe));   // poller p -> device p % G
+        },
+        pollers, conns, frames, size, threads, 60, shut);
     echo::print_json(pipe ? "gpu: libwscodec wsc_session per poller, recv into pinned staging, submit r+1 / echo r / complete"
                           : "gpu: libwscodec wsc_session per poller, one synchronous device decode per poller round",
-                     r, pollers, conns, frames, size);
+                     r, pollers, conns, frames, size, devices, shut);
     return r.ok ? 0 : 1;
 }
