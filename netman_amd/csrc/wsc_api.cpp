@@ -103,6 +103,7 @@ struct wsc_ctx {
     uint32_t u8_inline_max = 256;
     uint32_t u8_grid = 0;               // WSC_U8_GRID: k_u8_check workgroups (A/B experiments; 0 = 5 per CU)
     bool walk_tiled = true;             // WSC_WALK_TILED=0: the three-launch walk for mode 3 (A/B)
+    bool quad_pre = true;               // WSC_QUAD_PRE=0: the fused walk without its quad pre-pass (A/B)
     bool ab_no_u8 = false;              // WSC_AB_NO_U8=1: A/B timing only -- binary unmask, no UTF-8 launches
                                         // (wrong for text batches; never set in tests or the bench)
     int walk_mode = 0;                  // WSC_WALK_MODE: 16, 32, 64, 65, 66, 256 or 3 pins the walk geometry (A/B, tests); 0 = auto
@@ -317,6 +318,7 @@ int wsc_create(int device, const wsc_config* cfg_in, wsc_ctx** out) {
     if (const char* e = std::getenv("WSC_U8_GRID"); e && *e) c->u8_grid = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("WSC_AB_NO_U8"); e && e[0] == '1') c->ab_no_u8 = true;
     if (const char* e = std::getenv("WSC_WALK_TILED"); e && e[0] == '0') c->walk_tiled = false;
+    if (const char* e = std::getenv("WSC_QUAD_PRE"); e && e[0] == '0') c->quad_pre = false;
     if (const char* e = std::getenv("WSC_WALK_MODE"); e && *e) {   // pin a walk geometry (tests, A/B): 16, 32, 64, 65, 66, 256 or 3
         const int m = std::atoi(e);
         c->walk_mode = (m == 16 || m == 32 || m == 64 || m == 65 || m == 66 || m == 256 || m == 3) ? m : 0;
@@ -440,6 +442,7 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     wa.u8host = c->hflag;
     wa.win_flag = c->win_flag;
     wa.compact = compact ? 1u : 0u;
+    wa.quad_pre = c->quad_pre ? 1u : 0u;
 
     // walk geometry: the fused walk with blocks that fill the CUs once (64 lanes for up to 64
     // segments per CU, else 256), or -- for more segments than the chip holds lanes at once -- the

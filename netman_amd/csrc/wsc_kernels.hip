@@ -238,10 +238,20 @@ __device__ __forceinline__ uint4 rec_pack(const wsc_frame& fr, uint64_t seg_star
 #ifndef WSC_WALK_SPEC
 #define WSC_WALK_SPEC 2
 #endif
+
+// What the quad pre-pass (quad_prefix, below) already walked of a segment: its leading run of
+// plain complete BIN messages, recorded in LDS.  The serial walk continues after it.  Offsets are
+// relative to the segment start (the pre-pass runs only on segments < 4 GiB).
+struct PreState {
+    uint32_t nf, ns, nb;   // frames recorded, spans, payload bytes (region 0)
+    uint32_t pos, pend;    // where the walk continues; wire end of the last span
+    uint32_t msg, stride;  // msgID after the run; the last frame's size (the next speculation)
+};
 template <bool EMIT, bool COMPACT, uint32_t LS = 64, int SPEC_D = WSC_WALK_SPEC, bool PURE = false>
 __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, const SegCount& base,
                                                  const SegCount& own, uint4* lrec, WalkEnd* wend,
-                                                 uint4* lrec2 = nullptr, uint32_t cap = 0, uint32_t tag = 0) {
+                                                 uint4* lrec2 = nullptr, uint32_t cap = 0, uint32_t tag = 0,
+                                                 const PreState* pre = nullptr) {
     const uint8_t* __restrict__ w = a.wire;
     const uint64_t seg_start = a.seg_off[s];
     const uint64_t seg_end = a.seg_off[s + 1];
@@ -759,6 +769,20 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
 
     uint64_t stride = 0;
     bool go = status == WSC_SEG_OPEN;
+    if constexpr (!EMIT) {
+        // the quad pre-pass walked (and recorded) the segment's leading plain BIN messages: continue
+        // after them with the state they leave (websocket_frame.go:84-89: mode 0, msgID + 1 each)
+        if (pre && pre->nf) {
+            pos = seg_start + pre->pos;
+            pend = seg_start + pre->pend;
+            msg = pre->msg;
+            mode = 0;
+            nf = pre->nf;
+            ns0 = pre->ns;
+            nb0 = pre->nb;
+            stride = pre->stride;
+        }
+    }
     if (go && frem && seg_end > pos) resume();   // (a rest longer than the segment: nothing else)
     go = go && status == WSC_SEG_OPEN && frem == 0;
     while (go) {
@@ -997,6 +1021,162 @@ __global__ __launch_bounds__(256) void k_walk_emit(WalkArgs a) {
     walk_segment<true, COMPACT, 256>(a, s, base, own, nullptr, nullptr);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Quad pre-pass of the fused walk (one segment per 4 lanes, every wave of the block).  The serial
+// walk spends its time on the header chain: one lane walks its segment's frames one after another,
+// each a dependent memory round trip plus the state machine's instructions on one wave per SIMD
+// (the configs[2] walk waits 85 % of its cycles).  Most frames are plain complete BIN messages
+// (0x82, masked, no fragmented message open: websocket.go:142-146 then websocket_frame.go:52-91 --
+// Message{MsgID: msg, Opcode: 2}, messageMode 0, msgID + 1), so a quad speculates: its 16
+// candidates (4 per lane) sit at pos + k * stride, stride = the size of the last frame found, all
+// loaded in ONE round trip and parsed in parallel; the leading run of candidates that are plain BIN
+// messages of exactly that size are real frames -- plus the first one that breaks the stride, if
+// it is one.  Their LDS records (the serial walk's format) are written at once, with MsgIDs, span
+// ordinals and arena offsets from quad prefix sums.  The run stops at the first frame that is not a
+// plain BIN message (or is incomplete, or at the record capacity); the serial walk then continues
+// from there with the state the run leaves.  Results never depend on the guess: a candidate is used
+// only when the previous real frame ends exactly at it.
+// ---------------------------------------------------------------------------------------------
+template <uint32_t LS>
+__device__ __forceinline__ void quad_prefix(const WalkArgs& a, uint32_t s, uint32_t q, uint32_t qbase,
+                                            uint4* lrec, uint4* lrec2, PreState* out, uint32_t cap) {
+    const uint8_t* __restrict__ w = a.wire;
+    bool ok = s < a.n_segs;
+    uint64_t seg_start = 0, seg_end = 0;
+    uint32_t msg = 0;
+    if (ok) {
+        seg_start = a.seg_off[s];
+        seg_end = a.seg_off[s + 1];
+        if (a.state_in) {
+            const wsc_conn_state st = a.state_in[s];
+            ok = st.status == WSC_SEG_OPEN && st.cont_len == 0 && st.frame_rem == 0;
+            msg = st.msg_id;
+        }
+        ok = ok && seg_end - seg_start <= 0xFFFFFFFFull;
+    }
+    auto quad = [&](uint32_t v, uint32_t k) { return (uint32_t)__shfl((int)v, (int)(qbase + k)); };
+    uint64_t pos = seg_start, pend = seg_start;
+    uint32_t stride = 0, nf = 0, ns = 0, nb = 0;
+    bool go = ok && seg_end - pos >= 2 && cap > 0;
+    while (go) {
+        // one round trip: candidates 4q .. 4q+3 (candidate 0 is the real next frame)
+        uint4 hd[4];
+        uint64_t hp[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t idx = 4 * q + j;
+            hp[j] = pos + (uint64_t)idx * stride;
+            const bool ld = idx == 0 || (stride != 0 && hp[j] + 2 <= seg_end);
+            hd[j] = ld ? hdr_load(w, a.n_bytes, hp[j]) : make_uint4(0, 0, 0, 0);
+            if (!ld) hp[j] = ~0ull;
+        }
+        uint32_t fbits = 0, lbits = 0;
+        uint32_t sz[4], pl[4], hlj[4], mk[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t b0 = hd[j].x & 0xFFu, b1 = (hd[j].x >> 8) & 0xFFu, len7 = b1 & 0x7Fu;
+            uint64_t plen;
+            uint32_t mask, hl;
+            if (len7 < 126) {
+                plen = len7;
+                mask = __builtin_amdgcn_alignbyte(hd[j].y, hd[j].x, 2);
+                hl = 6;
+            } else if (len7 == 126) {
+                plen = ((hd[j].x >> 8) & 0xFF00u) | (hd[j].x >> 24);
+                mask = hd[j].y;
+                hl = 8;
+            } else {
+                const uint64_t x = (uint64_t)__builtin_amdgcn_alignbyte(hd[j].y, hd[j].x, 2) |
+                                   (uint64_t)__builtin_amdgcn_alignbyte(hd[j].z, hd[j].y, 2) << 32;
+                plen = __builtin_bswap64(x);
+                mask = __builtin_amdgcn_alignbyte(hd[j].w, hd[j].z, 2);
+                hl = 14;
+            }
+            // a plain complete BIN message (the serial walk's `fast` path, binary case)
+            const bool f = hp[j] != ~0ull && b0 == 0x82u && (b1 & 0x80u) && plen <= a.max_frame_len &&
+                           hp[j] + hl + plen <= seg_end;
+            sz[j] = f ? hl + (uint32_t)plen : 0u;   // (the segment is < 4 GiB)
+            pl[j] = f ? (uint32_t)plen : 0u;
+            hlj[j] = hl;
+            mk[j] = mask;
+            fbits |= (f ? 1u : 0u) << j;
+            lbits |= (f && sz[j] == stride ? 1u : 0u) << j;
+        }
+        const uint32_t F16 = quad(fbits, 0) | quad(fbits, 1) << 4 | quad(fbits, 2) << 8 | quad(fbits, 3) << 12;
+        const uint32_t L16 = quad(lbits, 0) | quad(lbits, 1) << 4 | quad(lbits, 2) << 8 | quad(lbits, 3) << 12;
+        const uint32_t lead = (uint32_t)__builtin_ctz(~L16 | 0x10000u);   // linked candidates in front
+        uint32_t r;
+        bool stop;
+        if (lead >= 16) {
+            r = 16;
+            stop = false;
+        } else {
+            const bool fl = (F16 >> lead) & 1u;   // the candidate at `lead` is real: taken if plain
+            r = fl ? lead + 1 : lead;
+            stop = !fl;
+        }
+        if (nf + r > cap) {   // LDS records of this segment: the serial walk counts the rest
+            r = cap - nf;
+            stop = true;
+        }
+        if (r == 0) break;
+        // exclusive prefix over the taken candidates: spans, payload bytes, last span end
+        uint32_t cnt = 0, bytes = 0;
+        uint64_t lend = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (4 * q + j < r && pl[j]) { cnt += 1; bytes += pl[j]; lend = hp[j] + sz[j]; }
+        uint32_t cnt_x = 0, bytes_x = 0, cnt_t = 0, bytes_t = 0;
+        uint64_t lend_x = pend, lend_t = pend;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+            const uint32_t c = quad(cnt, k), b = quad(bytes, k);
+            const uint64_t e = (uint64_t)quad((uint32_t)lend, k) | (uint64_t)quad((uint32_t)(lend >> 32), k) << 32;
+            if (k < q) { cnt_x += c; bytes_x += b; if (e > lend_x) lend_x = e; }
+            cnt_t += c; bytes_t += b;
+            if (e > lend_t) lend_t = e;
+        }
+        // the records, in the serial walk's LDS format (rec_pack / record)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t idx = 4 * q + j;
+            if (idx < r) {
+                const uint32_t bits = 2u | 1u << 4 | (uint32_t)WSC_FK_MESSAGE << 5 | 2u << 9 | hlj[j] << 14 |
+                                      (uint32_t)WSC_FF_UNMASKED << 18 | (pl[j] ? 1u : 0u) << 27;
+                lrec[(nf + idx) * LS] = make_uint4((uint32_t)(hp[j] - seg_start), pl[j], mk[j], bits);
+                lrec2[(nf + idx) * LS] = make_uint4(msg + idx, ns + cnt_x, nb + bytes_x, (uint32_t)(lend_x - seg_start));
+                if (pl[j]) {
+                    cnt_x += 1;
+                    bytes_x += pl[j];
+                    lend_x = hp[j] + sz[j];
+                }
+            }
+        }
+        // the quad's state after the run: the last taken candidate's end and size
+        const uint32_t last = r - 1, lj = last & 3;
+        const uint32_t lsz = quad(lj == 0 ? sz[0] : lj == 1 ? sz[1] : lj == 2 ? sz[2] : sz[3], last >> 2);
+        pos = pos + (uint64_t)last * stride + lsz;
+        stride = lsz;
+        msg += r;
+        nf += r;
+        ns += cnt_t;
+        nb += bytes_t;
+        pend = lend_t;
+        go = !stop && nf < cap && seg_end - pos >= 2;
+    }
+    if (q == 0 && s < a.n_segs) {
+        PreState p;
+        p.nf = ok ? nf : 0;
+        p.ns = ns;
+        p.nb = nb;
+        p.pos = (uint32_t)(pos - seg_start);
+        p.pend = (uint32_t)(pend - seg_start);
+        p.msg = msg;
+        p.stride = stride;
+        *out = p;
+    }
+}
+
 // LDS of one tile of the walk: NT lanes of which the first WL walk segments (G consecutive
 // segments per walking lane), KR frame records per walking lane; every lane emits
 template <bool COMPACT, uint32_t KR, uint32_t NT, uint32_t G, uint32_t WL = NT>
@@ -1018,6 +1198,7 @@ struct WalkLds {
     uint32_t cons[G * WL], endst[G * WL];
     uint64_t abase[COMPACT ? G * WL : 1], ob0[COMPACT ? G * WL : 1];
     uint8_t rep[G * WL], r0[G * WL];   // (r0: the segment's first record in the lane's list)
+    PreState pre[(G == 1 && (4 * WL) % NT == 0) ? WL : 1];   // quad pre-pass results (one quad per segment)
 };
 
 // Count phase of a tile: each lane walks its G segments (first one s0; segments from seg_lim on
@@ -1025,7 +1206,7 @@ struct WalkLds {
 // state.  Returns the lane's total (lanes from WL on walk nothing).
 template <bool COMPACT, uint32_t KR, uint32_t NT, uint32_t G, uint32_t WL>
 __device__ __forceinline__ SegCount tile_count(const WalkArgs& a, WalkLds<COMPACT, KR, NT, G, WL>& L, uint32_t s0,
-                                               uint32_t seg_lim, uint32_t lane, uint32_t& nrec) {
+                                               uint32_t seg_lim, uint32_t lane, uint32_t& nrec, bool pre = false) {
     const SegCount zero = {};
     SegCount tot = zero;
     nrec = 0;
@@ -1042,7 +1223,8 @@ __device__ __forceinline__ SegCount tile_count(const WalkArgs& a, WalkLds<COMPAC
         WalkEnd we;
         const uint32_t cap = KR - nrec;
         const SegCount c = walk_segment<false, COMPACT, WL>(a, s, zero, zero, L.rec + nrec * WL + lane, &we,
-                                                            L.rec2 + nrec * WL + lane, cap, j);
+                                                            L.rec2 + nrec * WL + lane, cap, j,
+                                                            pre && j == 0 ? L.pre + (lane < WL ? lane : 0) : nullptr);
         const uint64_t ss = a.seg_off[s];
         const bool rep = we.replay;
         L.r0[q] = (uint8_t)nrec;
@@ -1342,9 +1524,32 @@ __global__ __launch_bounds__(NT) void k_walk_fused(WalkArgs a) {
     uint64_t t0 = 0, t1 = 0, t2 = 0;
     if (a.dbg && lane == 0) t0 = __builtin_amdgcn_s_memrealtime();
     uint32_t nrec;
+    // quad pre-pass (one segment per 4 lanes, all waves): the leading plain BIN messages of each
+    // segment, recorded in LDS; the walking lane continues after them
+    // (more walking lanes than quads: the quads take the block's segments NT / 4 at a time; if the
+    // first pass found no plain BIN message at all -- fragmented or text traffic -- the rest are skipped)
+    constexpr bool PRE = G == 1 && SPREAD == 0 && (4 * WL) % NT == 0;
+    if constexpr (PRE) {
+        constexpr uint32_t NQ = NT / 4, PASSES = WL / NQ;
+        __shared__ uint32_t sh_found;
+        if (lane == 0) sh_found = 0;
+        if (lane < WL) L.pre[lane].nf = 0;
+        __syncthreads();
+        if (a.quad_pre) {
+            for (uint32_t g = 0; g < PASSES; ++g) {
+                const uint32_t qc = g * NQ + (lane >> 2);
+                quad_prefix<WL>(a, bid * WL + qc, lane & 3u, wl & ~3u, L.rec + qc, L.rec2 + qc, L.pre + qc, KR);
+                if (g + 1 == PASSES) break;
+                if ((lane & 3u) == 0 && L.pre[qc].nf) sh_found = 1;   // (benign race: any writer sets 1)
+                __syncthreads();
+                if (g == 0 && sh_found == 0) break;
+            }
+        }
+        __syncthreads();
+    }
     // walking column: in lane order, so the block scan over physical lanes stays in segment order
     const uint32_t col = SPREAD == 0 ? lane : (wl < SPREAD && wave < WL / (SPREAD ? SPREAD : 1)) ? wave * SPREAD + wl : WL + lane;
-    const SegCount tot = tile_count<COMPACT, KR, NT, G>(a, L, (bid * WL + col) * G, a.n_segs, col, nrec);
+    const SegCount tot = tile_count<COMPACT, KR, NT, G>(a, L, (bid * WL + col) * G, a.n_segs, col, nrec, PRE);
     SegCount btot;
     const SegCount excl = tile_scan<NT>(tot, L, wl, wave, btot);
     if (wave == 0) {

@@ -118,6 +118,7 @@ struct WalkArgs {
     uint32_t* u8host;            // host-visible word set when any UTF-8 item is deferred (cleared by the host)
     uint32_t* win_flag;          // per unmask window: 1 = inside a deferred text item (k_unmask folds its map)
     uint32_t compact;            // WSC_F_COMPACT (k_walk_scan: the other kernels are templated on it)
+    uint32_t quad_pre;           // fused walk with one walking wave per 4: the quad pre-pass (WSC_QUAD_PRE=0: off, A/B)
 };
 
 // k_u8_check runs AFTER the unmask: the unmask has already folded every text window that lies
