@@ -311,7 +311,8 @@ int wsc_encode_host(wsc_ctx* ctx, const wsc_out_msg* msgs, uint32_t n_msgs, cons
 int wsc_profile(wsc_ctx* ctx, const wsc_batch* batch, int iters, double* out_ms);
 
 /* Diagnostics: with WSC_DEBUG_STAMPS=1 in the environment at wsc_create, the header-walk kernel
- * records per block 4 s_memrealtime stamps (100 MHz): start, counted, look-back done, emitted. */
+ * records per block 8 u64 slots of s_memrealtime stamps (100 MHz): start, counted, look-back done,
+ * emitted, quad pre-pass done (0 if none), 3 reserved.  `out` has room for 8 * max_blocks.     */
 int wsc_debug_stamps(wsc_ctx* ctx, uint64_t* out, uint32_t max_blocks);
 
 /* ---- session: the per-connection DecodePacket() mirror (C++ host side above the ABI) ---------

@@ -104,6 +104,8 @@ struct wsc_ctx {
     uint32_t u8_grid = 0;               // WSC_U8_GRID: k_u8_check workgroups (A/B experiments; 0 = 5 per CU)
     bool walk_tiled = true;             // WSC_WALK_TILED=0: the three-launch walk for mode 3 (A/B)
     bool quad_pre = true;               // WSC_QUAD_PRE=0: the fused walk without its quad pre-pass (A/B)
+    int xcd_map = 0;                    // WSC_XCD_MAP=1: unmask windows XCD-contiguous (A/B; measured slower:
+                                        // configs[4] COMPACT 0.945-0.955 -> 0.971 ms, headline 0.347 -> 0.359 ms)
     bool ab_no_u8 = false;              // WSC_AB_NO_U8=1: A/B timing only -- binary unmask, no UTF-8 launches
                                         // (wrong for text batches; never set in tests or the bench)
     int walk_mode = 0;                  // WSC_WALK_MODE: 16, 32, 64, 65, 66, 256 or 3 pins the walk geometry (A/B, tests); 0 = auto
@@ -111,6 +113,8 @@ struct wsc_ctx {
     uint32_t walk_blocks = 0;           // the staged unmask re-arms exactly that walk's look-back flags
     uint32_t max_walk_blocks = 0;       // look-back state allocated for this many walk blocks
     SegCount* counts = nullptr;         // three-launch walk: per-segment counts
+    uint4* hdr_cache = nullptr;         // tiled walk: per segment, its first 16 header bytes (WSC_HDR_CACHE=0: off)
+    uint32_t* stride_hint = nullptr;    // quad pre-pass: the frame stride the last decode ended with
     uint64_t tile_entries = 0;
     // host-staged path buffers (lazily allocated)
     uint8_t* d_wire = nullptr;
@@ -278,7 +282,11 @@ int wsc_create(int device, const wsc_config* cfg_in, wsc_ctx** out) {
         chk(hipMemsetAsync(c->fin_ctr, 0, 257 * 32 * sizeof(uint32_t), c->stream), "hipMemset fin_ctr");
     }
     chk(hipMalloc(&c->sticky, sizeof(uint32_t)), "hipMalloc sticky");
+    chk(hipMalloc(&c->stride_hint, sizeof(uint32_t)), "hipMalloc stride_hint");
+    if (rc == WSC_OK) chk(hipMemsetAsync(c->stride_hint, 0, sizeof(uint32_t), c->stream), "hipMemset stride_hint");
     chk(hipMalloc(&c->counts, (uint64_t)cfg.max_segs * sizeof(SegCount)), "hipMalloc counts");
+    if (const char* e = std::getenv("WSC_HDR_CACHE"); !(e && e[0] == '0'))
+        chk(hipMalloc(&c->hdr_cache, (uint64_t)cfg.max_segs * sizeof(uint4)), "hipMalloc hdr_cache");
     if (rc == WSC_OK) chk(hipMemsetAsync(c->sticky, 0, sizeof(uint32_t), c->stream), "hipMemset sticky");
     // the most walk blocks (64 segments per block; 16 per block for up to 64 segments per CU); the
     // look-back flags, aggregates and prefixes are indexed by block
@@ -290,7 +298,7 @@ int wsc_create(int device, const wsc_config* cfg_in, wsc_ctx** out) {
     chk(hipMalloc(&c->lb_agg, max_blocks * 4 * sizeof(uint64_t)), "hipMalloc lb_agg");
     chk(hipMalloc(&c->lb_incl, max_blocks * 4 * sizeof(uint64_t)), "hipMalloc lb_incl");
     if (const char* e = std::getenv("WSC_DEBUG_STAMPS"); e && e[0] == '1')
-        chk(hipMalloc(&c->dbg, max_blocks * 4 * sizeof(uint64_t)), "hipMalloc dbg");
+        chk(hipMalloc(&c->dbg, max_blocks * 8 * sizeof(uint64_t)), "hipMalloc dbg");
     if (rc == WSC_OK) {
         chk(hipMemsetAsync(c->lb_state, 0, (max_blocks + 3) * sizeof(uint32_t), c->stream), "hipMemset lb_state");
         chk(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
@@ -319,6 +327,7 @@ int wsc_create(int device, const wsc_config* cfg_in, wsc_ctx** out) {
     if (const char* e = std::getenv("WSC_AB_NO_U8"); e && e[0] == '1') c->ab_no_u8 = true;
     if (const char* e = std::getenv("WSC_WALK_TILED"); e && e[0] == '0') c->walk_tiled = false;
     if (const char* e = std::getenv("WSC_QUAD_PRE"); e && e[0] == '0') c->quad_pre = false;
+    if (const char* e = std::getenv("WSC_XCD_MAP"); e && *e) c->xcd_map = std::atoi(e) ? 1 : 0;
     if (const char* e = std::getenv("WSC_WALK_MODE"); e && *e) {   // pin a walk geometry (tests, A/B): 16, 32, 64, 65, 66, 256 or 3
         const int m = std::atoi(e);
         c->walk_mode = (m == 16 || m == 32 || m == 64 || m == 65 || m == 66 || m == 256 || m == 3) ? m : 0;
@@ -350,7 +359,7 @@ int wsc_destroy(wsc_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     (void)fin_wait(c);
-    void* ptrs[] = {c->fin_ctr, c->dbg, c->sticky, c->counts, c->lb_state, c->u8info, c->lb_agg, c->lb_incl, c->spans, c->tile, c->d_wire, c->d_arena,
+    void* ptrs[] = {c->fin_ctr, c->dbg, c->sticky, c->counts, c->hdr_cache, c->stride_hint, c->lb_state, c->u8info, c->lb_agg, c->lb_incl, c->spans, c->tile, c->d_wire, c->d_arena,
                     c->d_seg_off, c->d_state_in, c->d_state_out, c->d_seg_out, c->d_frames,
                     c->d_frame_dst, c->d_summary, c->enc_lb_state, c->enc_lb_agg, c->enc_lb_incl, c->enc_tile,
                     c->d_enc_msgs, c->d_enc_src, c->d_enc_out, c->d_enc_off, c->u8items, c->u8maps, c->u8seg,
@@ -443,6 +452,8 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     wa.win_flag = c->win_flag;
     wa.compact = compact ? 1u : 0u;
     wa.quad_pre = c->quad_pre ? 1u : 0u;
+    wa.hdr_cache = c->hdr_cache;
+    wa.stride_hint = c->stride_hint;
 
     // walk geometry: the fused walk with blocks that fill the CUs once (64 lanes for up to 64
     // segments per CU, else 256), or -- for more segments than the chip holds lanes at once -- the
@@ -560,6 +571,7 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     const bool sig_unmask = signal && !need_u8;
     U8Win uw{};
     uw.rearm = c->u8ctr + 32 * (c->u8par ^ 1u);
+    uw.grid_map = c->xcd_map == 1 ? 1u : 0u;
     if (need_u8) {
         uw.flag = c->win_flag;
         uw.map = c->win_map;
@@ -870,7 +882,8 @@ int wsc_debug_stamps(wsc_ctx* c, uint64_t* out, uint32_t max_blocks) {
     if (!c->dbg) return fail(WSC_E_STATE, "context created without WSC_DEBUG_STAMPS=1");
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipDeviceSynchronize());
-    HIP_TRY(hipMemcpy(out, c->dbg, (uint64_t)max_blocks * 4 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    if (max_blocks > c->max_walk_blocks) max_blocks = c->max_walk_blocks;
+    HIP_TRY(hipMemcpy(out, c->dbg, (uint64_t)max_blocks * 8 * sizeof(uint64_t), hipMemcpyDeviceToHost));
     return WSC_OK;
 }
 

@@ -245,13 +245,18 @@ __device__ __forceinline__ uint4 rec_pack(const wsc_frame& fr, uint64_t seg_star
 struct PreState {
     uint32_t nf, ns, nb;   // frames recorded, spans, payload bytes (region 0)
     uint32_t pos, pend;    // where the walk continues; wire end of the last span
-    uint32_t msg, stride;  // msgID after the run; the last frame's size (the next speculation)
+    uint32_t msg, stride;  // msgID after the run; the stride it speculated with last
+    bool full;             // the run reached the segment's end (< 2 bytes left): no serial walk
 };
 template <bool EMIT, bool COMPACT, uint32_t LS = 64, int SPEC_D = WSC_WALK_SPEC, bool PURE = false>
 __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, const SegCount& base,
                                                  const SegCount& own, uint4* lrec, WalkEnd* wend,
                                                  uint4* lrec2 = nullptr, uint32_t cap = 0, uint32_t tag = 0,
-                                                 const PreState* pre = nullptr) {
+                                                 const PreState* pre = nullptr, const uint4* hc_in = nullptr,
+                                                 uint4* hc_out = nullptr) {
+    // hc_out / hc_in: the tiled walk's header cache -- its counting pass stores the 16 bytes at the
+    // segment's first frame (one coalesced 16 B store per lane), the emitting pass takes them from
+    // there instead of re-reading a scattered wire line per segment
     const uint8_t* __restrict__ w = a.wire;
     const uint64_t seg_start = a.seg_off[s];
     const uint64_t seg_end = a.seg_off[s + 1];
@@ -796,9 +801,11 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
         for (int k = 0; k < SPEC_D; ++k) {
             hp[k] = pos + (uint64_t)k * stride;
             hc[k] = make_uint4(0, 0, 0, 0);
-            if (k == 0 || (stride != 0 && hp[k] + 2 <= seg_end)) hc[k] = hdr_load(w, a.n_bytes, hp[k]);
+            if (k == 0 && hc_in && pos == seg_start) hc[k] = hc_in[s];
+            else if (k == 0 || (stride != 0 && hp[k] + 2 <= seg_end)) hc[k] = hdr_load(w, a.n_bytes, hp[k]);
             else hp[k] = ~0ull;
         }
+        if (hc_out && pos == seg_start) hc_out[s] = hc[0];
         // consume the round's headers in order from the front of the queue; one copy of `step`
         // in the code (an unrolled consumer made the walk ~20k instructions: instruction-cache bound)
 #pragma unroll 1
@@ -1037,8 +1044,18 @@ __global__ __launch_bounds__(256) void k_walk_emit(WalkArgs a) {
 // from there with the state the run leaves.  Results never depend on the guess: a candidate is used
 // only when the previous real frame ends exactly at it.
 // ---------------------------------------------------------------------------------------------
+// broadcast lane K of each quad to the quad's 4 lanes (DPP quad_perm: a VALU op, no LDS round trip)
+template <int K>
+__device__ __forceinline__ uint32_t qb(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, K * 0x55, 0xF, 0xF, false);
+}
+__device__ __forceinline__ uint32_t qb_dyn(uint32_t v, uint32_t k) {   // k quad-uniform
+    const uint32_t v0 = qb<0>(v), v1 = qb<1>(v), v2 = qb<2>(v), v3 = qb<3>(v);
+    return k == 0 ? v0 : k == 1 ? v1 : k == 2 ? v2 : v3;
+}
+
 template <uint32_t LS>
-__device__ __forceinline__ void quad_prefix(const WalkArgs& a, uint32_t s, uint32_t q, uint32_t qbase,
+__device__ __forceinline__ void quad_prefix(const WalkArgs& a, uint32_t s, uint32_t q, uint32_t stride_hint,
                                             uint4* lrec, uint4* lrec2, PreState* out, uint32_t cap) {
     const uint8_t* __restrict__ w = a.wire;
     bool ok = s < a.n_segs;
@@ -1054,9 +1071,12 @@ __device__ __forceinline__ void quad_prefix(const WalkArgs& a, uint32_t s, uint3
         }
         ok = ok && seg_end - seg_start <= 0xFFFFFFFFull;
     }
-    auto quad = [&](uint32_t v, uint32_t k) { return (uint32_t)__shfl((int)v, (int)(qbase + k)); };
     uint64_t pos = seg_start, pend = seg_start;
-    uint32_t stride = 0, nf = 0, ns = 0, nb = 0;
+    // the first round speculates with the stride the previous decode on this context ended with (a
+    // hint only: any value is safe); later rounds keep the stride that linked, so a single frame of
+    // another size (a 64 KiB frame among 125 B ones) costs one round, not two
+    uint32_t stride = stride_hint, nf = 0, ns = 0, nb = 0;
+    bool first = true;
     bool go = ok && seg_end - pos >= 2 && cap > 0;
     while (go) {
         // one round trip: candidates 4q .. 4q+3 (candidate 0 is the real next frame)
@@ -1102,8 +1122,8 @@ __device__ __forceinline__ void quad_prefix(const WalkArgs& a, uint32_t s, uint3
             fbits |= (f ? 1u : 0u) << j;
             lbits |= (f && sz[j] == stride ? 1u : 0u) << j;
         }
-        const uint32_t F16 = quad(fbits, 0) | quad(fbits, 1) << 4 | quad(fbits, 2) << 8 | quad(fbits, 3) << 12;
-        const uint32_t L16 = quad(lbits, 0) | quad(lbits, 1) << 4 | quad(lbits, 2) << 8 | quad(lbits, 3) << 12;
+        const uint32_t F16 = qb<0>(fbits) | qb<1>(fbits) << 4 | qb<2>(fbits) << 8 | qb<3>(fbits) << 12;
+        const uint32_t L16 = qb<0>(lbits) | qb<1>(lbits) << 4 | qb<2>(lbits) << 8 | qb<3>(lbits) << 12;
         const uint32_t lead = (uint32_t)__builtin_ctz(~L16 | 0x10000u);   // linked candidates in front
         uint32_t r;
         bool stop;
@@ -1126,16 +1146,23 @@ __device__ __forceinline__ void quad_prefix(const WalkArgs& a, uint32_t s, uint3
 #pragma unroll
         for (int j = 0; j < 4; ++j)
             if (4 * q + j < r && pl[j]) { cnt += 1; bytes += pl[j]; lend = hp[j] + sz[j]; }
-        uint32_t cnt_x = 0, bytes_x = 0, cnt_t = 0, bytes_t = 0;
+        const uint32_t lend_lo = (uint32_t)lend, lend_hi = (uint32_t)(lend >> 32);
+        const uint32_t c4[4] = {qb<0>(cnt), qb<1>(cnt), qb<2>(cnt), qb<3>(cnt)};
+        const uint32_t b4[4] = {qb<0>(bytes), qb<1>(bytes), qb<2>(bytes), qb<3>(bytes)};
+        const uint64_t e4[4] = {(uint64_t)qb<0>(lend_hi) << 32 | qb<0>(lend_lo), (uint64_t)qb<1>(lend_hi) << 32 | qb<1>(lend_lo),
+                                (uint64_t)qb<2>(lend_hi) << 32 | qb<2>(lend_lo), (uint64_t)qb<3>(lend_hi) << 32 | qb<3>(lend_lo)};
+        uint32_t cnt_x = 0, bytes_x = 0;
         uint64_t lend_x = pend, lend_t = pend;
 #pragma unroll
         for (uint32_t k = 0; k < 4; ++k) {
-            const uint32_t c = quad(cnt, k), b = quad(bytes, k);
-            const uint64_t e = (uint64_t)quad((uint32_t)lend, k) | (uint64_t)quad((uint32_t)(lend >> 32), k) << 32;
-            if (k < q) { cnt_x += c; bytes_x += b; if (e > lend_x) lend_x = e; }
-            cnt_t += c; bytes_t += b;
-            if (e > lend_t) lend_t = e;
+            if (k < q) {
+                cnt_x += c4[k];
+                bytes_x += b4[k];
+                if (e4[k] > lend_x) lend_x = e4[k];
+            }
+            if (e4[k] > lend_t) lend_t = e4[k];
         }
+        const uint32_t cnt_t = c4[0] + c4[1] + c4[2] + c4[3], bytes_t = b4[0] + b4[1] + b4[2] + b4[3];
         // the records, in the serial walk's LDS format (rec_pack / record)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -1154,9 +1181,12 @@ __device__ __forceinline__ void quad_prefix(const WalkArgs& a, uint32_t s, uint3
         }
         // the quad's state after the run: the last taken candidate's end and size
         const uint32_t last = r - 1, lj = last & 3;
-        const uint32_t lsz = quad(lj == 0 ? sz[0] : lj == 1 ? sz[1] : lj == 2 ? sz[2] : sz[3], last >> 2);
+        const uint32_t lsz = qb_dyn(lj == 0 ? sz[0] : lj == 1 ? sz[1] : lj == 2 ? sz[2] : sz[3], last >> 2);
         pos = pos + (uint64_t)last * stride + lsz;
-        stride = lsz;
+        // a run that linked keeps its stride (the frame that broke it, taken, is a one-off); one that
+        // linked nothing -- a stale hint, or the first frame of another size -- follows that frame
+        if (lead == 0) stride = lsz;
+        first = false;
         msg += r;
         nf += r;
         ns += cnt_t;
@@ -1164,6 +1194,7 @@ __device__ __forceinline__ void quad_prefix(const WalkArgs& a, uint32_t s, uint3
         pend = lend_t;
         go = !stop && nf < cap && seg_end - pos >= 2;
     }
+    (void)first;
     if (q == 0 && s < a.n_segs) {
         PreState p;
         p.nf = ok ? nf : 0;
@@ -1173,6 +1204,7 @@ __device__ __forceinline__ void quad_prefix(const WalkArgs& a, uint32_t s, uint3
         p.pend = (uint32_t)(pend - seg_start);
         p.msg = msg;
         p.stride = stride;
+        p.full = ok && nf > 0 && seg_end - pos < 2;   // nothing left for the serial walk
         *out = p;
     }
 }
@@ -1206,7 +1238,8 @@ struct WalkLds {
 // state.  Returns the lane's total (lanes from WL on walk nothing).
 template <bool COMPACT, uint32_t KR, uint32_t NT, uint32_t G, uint32_t WL>
 __device__ __forceinline__ SegCount tile_count(const WalkArgs& a, WalkLds<COMPACT, KR, NT, G, WL>& L, uint32_t s0,
-                                               uint32_t seg_lim, uint32_t lane, uint32_t& nrec, bool pre = false) {
+                                               uint32_t seg_lim, uint32_t lane, uint32_t& nrec, bool pre = false,
+                                               const uint4* hcache = nullptr) {
     const SegCount zero = {};
     SegCount tot = zero;
     nrec = 0;
@@ -1222,10 +1255,33 @@ __device__ __forceinline__ SegCount tile_count(const WalkArgs& a, WalkLds<COMPAC
         }
         WalkEnd we;
         const uint32_t cap = KR - nrec;
-        const SegCount c = walk_segment<false, COMPACT, WL>(a, s, zero, zero, L.rec + nrec * WL + lane, &we,
-                                                            L.rec2 + nrec * WL + lane, cap, j,
-                                                            pre && j == 0 ? L.pre + (lane < WL ? lane : 0) : nullptr);
+        const PreState* ps = pre && j == 0 ? L.pre + (lane < WL ? lane : 0) : nullptr;
         const uint64_t ss = a.seg_off[s];
+        SegCount c;
+        if (ps && ps->full) {
+            // the quad pre-pass walked the whole segment (plain BIN messages from a connection with
+            // no fragmented message or frame open): its end state, without a serial walk -- what
+            // walk_segment would return after those frames (mode 0, msgID advanced, no text)
+            const wsc_conn_state st0 = a.state_in ? a.state_in[s] : wsc_conn_state{};
+            c = zero;
+            c.frames = ps->nf;
+            c.spans0 = ps->ns;
+            c.bytes0 = ps->nb;
+            we.pos = ss + ps->pos;
+            we.cont = 0;
+            we.last_dend = ss + ps->pend;
+            we.frem = we.flen = 0;
+            we.fmask = we.fhdr = 0;
+            we.msg = ps->msg;
+            we.mode = 0;
+            we.status = st0.status;   // (OPEN: the pre-pass runs only then)
+            we.close_code = we.err = 0;
+            we.u8dfa = we.pdfa = 0;
+            we.replay = true;         // (nf <= cap and the segment is < 4 GiB)
+        } else {
+            c = walk_segment<false, COMPACT, WL>(a, s, zero, zero, L.rec + nrec * WL + lane, &we,
+                                                 L.rec2 + nrec * WL + lane, cap, j, ps, hcache);
+        }
         const bool rep = we.replay;
         L.r0[q] = (uint8_t)nrec;
         if (rep) nrec += c.frames;
@@ -1536,9 +1592,10 @@ __global__ __launch_bounds__(NT) void k_walk_fused(WalkArgs a) {
         if (lane < WL) L.pre[lane].nf = 0;
         __syncthreads();
         if (a.quad_pre) {
+            const uint32_t hint = a.stride_hint ? *a.stride_hint : 0u;
             for (uint32_t g = 0; g < PASSES; ++g) {
                 const uint32_t qc = g * NQ + (lane >> 2);
-                quad_prefix<WL>(a, bid * WL + qc, lane & 3u, wl & ~3u, L.rec + qc, L.rec2 + qc, L.pre + qc, KR);
+                quad_prefix<WL>(a, bid * WL + qc, lane & 3u, hint, L.rec + qc, L.rec2 + qc, L.pre + qc, KR);
                 if (g + 1 == PASSES) break;
                 if ((lane & 3u) == 0 && L.pre[qc].nf) sh_found = 1;   // (benign race: any writer sets 1)
                 __syncthreads();
@@ -1546,6 +1603,9 @@ __global__ __launch_bounds__(NT) void k_walk_fused(WalkArgs a) {
             }
         }
         __syncthreads();
+        if (a.dbg && lane == 0) a.dbg[8 * bid + 4] = __builtin_amdgcn_s_memrealtime();   // pre-pass done
+        // the next decode's first speculation (a hint: any value is safe)
+        if (bid == 0 && lane == 0 && a.stride_hint && L.pre[0].nf) *a.stride_hint = L.pre[0].stride;
     }
     // walking column: in lane order, so the block scan over physical lanes stays in segment order
     const uint32_t col = SPREAD == 0 ? lane : (wl < SPREAD && wave < WL / (SPREAD ? SPREAD : 1)) ? wave * SPREAD + wl : WL + lane;
@@ -1563,10 +1623,10 @@ __global__ __launch_bounds__(NT) void k_walk_fused(WalkArgs a) {
     if (a.dbg) {   // diagnostic timestamps (100 MHz s_memrealtime), written only to the dbg buffer
         __syncthreads();
         if (lane == 0) {
-            a.dbg[4 * bid + 0] = t0;
-            a.dbg[4 * bid + 1] = t1;
-            a.dbg[4 * bid + 2] = t2;
-            a.dbg[4 * bid + 3] = __builtin_amdgcn_s_memrealtime();
+            a.dbg[8 * bid + 0] = t0;
+            a.dbg[8 * bid + 1] = t1;
+            a.dbg[8 * bid + 2] = t2;
+            a.dbg[8 * bid + 3] = __builtin_amdgcn_s_memrealtime();
         }
     }
     if (bid == n_blocks - 1 && lane == 0) write_summary<COMPACT>(a, sc_add(L.prefix, btot));
@@ -1597,7 +1657,9 @@ __global__ __launch_bounds__(NT) void k_walk_tiled(WalkArgs a, uint32_t per_bloc
     // ---- phase 1: the block's total ----
     SegCount tot = zero;
     for (uint32_t t = sb; t < se; t += NT)
-        if (t + lane < se) tot = sc_add(tot, walk_segment<false, COMPACT, NT, 4, true>(a, t + lane, zero, zero, nullptr, nullptr));
+        if (t + lane < se)
+            tot = sc_add(tot, walk_segment<false, COMPACT, NT, 4, true>(a, t + lane, zero, zero, nullptr, nullptr, nullptr, 0,
+                                                                        0, nullptr, nullptr, a.hdr_cache));
     SegCount btot;
     (void)tile_scan<NT>(tot, L, wl, wave, btot);
     if (wave == 0) {
@@ -1610,7 +1672,7 @@ __global__ __launch_bounds__(NT) void k_walk_tiled(WalkArgs a, uint32_t per_bloc
     SegCount run = block_prefix;
     for (uint32_t t = sb; t < se; t += NT) {
         uint32_t nrec;   // (lanes past the block's last segment count nothing)
-        const SegCount c = tile_count<COMPACT, KR, NT, 1>(a, L, t + lane, se, lane, nrec);
+        const SegCount c = tile_count<COMPACT, KR, NT, 1>(a, L, t + lane, se, lane, nrec, false, a.hdr_cache);
         SegCount ttot;
         const SegCount excl = tile_scan<NT>(c, L, wl, wave, ttot);
         tile_emit<COMPACT, KR, NT, 1>(a, L, sc_add(run, excl), nrec, t, se, lane);

@@ -119,6 +119,8 @@ struct WalkArgs {
     uint32_t* win_flag;          // per unmask window: 1 = inside a deferred text item (k_unmask folds its map)
     uint32_t compact;            // WSC_F_COMPACT (k_walk_scan: the other kernels are templated on it)
     uint32_t quad_pre;           // fused walk with one walking wave per 4: the quad pre-pass (WSC_QUAD_PRE=0: off, A/B)
+    uint4* hdr_cache;            // tiled walk: per segment, the 16 bytes at its first frame (null: off)
+    uint32_t* stride_hint;       // quad pre-pass: the stride the last decode ended with (first speculation)
 };
 
 // k_u8_check runs AFTER the unmask: the unmask has already folded every text window that lies
@@ -158,6 +160,8 @@ struct U8Win {
     uint64_t* map;
     const uint32_t* count;
     uint32_t* rearm;             // the next decode's item counter (zeroed by the unmask: always launched)
+    uint32_t grid_map;           // bit 0: XCD-contiguous windows (block b -> logical block so that the
+                                 // blocks sharing an XCD, b mod 8, take one contiguous run of windows)
 };
 
 

@@ -414,7 +414,18 @@ __device__ __forceinline__ void unmask_all(uint8_t* __restrict__ dst, const uint
     if (blockIdx.x == 0 && threadIdx.x == 0 && u8w.rearm) *u8w.rearm = 0;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t waves_per_block = blockDim.x >> 6;
-    const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * waves_per_block + (threadIdx.x >> 6));
+    // XCD-contiguous windows (grid_map bit 0): blocks are dealt round-robin over the 8 XCDs
+    // (MI355X_MICROARCH.md, workgroup dispatch), so window w and w + 1 of neighbouring blocks sit in
+    // two XCDs' L2s.  In COMPACT mode the arena line holding a window's last bytes also holds the
+    // next window's first ones: written from two L2s it leaves as two partial lines.  Remapped,
+    // the blocks of one XCD (b mod 8 = x) take one contiguous run of windows.  A bijection for any
+    // grid size; placement affects speed only, never results.
+    uint32_t bid = blockIdx.x;
+    if (u8w.grid_map & 1u) {
+        const uint32_t q = gridDim.x >> 3, rr = gridDim.x & 7u, x = bid & 7u;
+        bid = x * q + (x < rr ? x : rr) + (bid >> 3);
+    }
+    const uint32_t gw = __builtin_amdgcn_readfirstlane(bid * waves_per_block + (threadIdx.x >> 6));
     const uint32_t nw = gridDim.x * waves_per_block;
     const uint32_t n_spans = summary->n_spans;
     const uint64_t n_win = (total + WB - 1) / WB;

@@ -34,6 +34,19 @@ def test_cpu_echo_roundtrip(cpu_echo, args):
     assert d["messages"] == int(args[1]) * int(args[3])
 
 
+def test_poller_device_mapping():
+    """SURVEY §8(e) / VERDICT r3 #7: ws_echo --devices G puts poller p's session on device p mod G
+    (one host thread, stream and pinned staging per GPU; a connection never moves) -- checked
+    without a device (--print-map exits before any session is created)"""
+    from netman_amd import _build
+    exe = _build.build_tools()
+    for pollers, devices in ((8, 8), (8, 3), (5, 1), (16, 8)):
+        p = subprocess.run([exe, "--pollers", str(pollers), "--conns", "64", "--devices", str(devices), "--print-map"],
+                           capture_output=True, text=True, timeout=60)
+        d = json.loads(p.stdout)
+        assert p.returncode == 0 and d["device_of_poller"] == [i % devices for i in range(pollers)], d
+
+
 @pytest.mark.parametrize("pollers", ["1", "4"])
 def test_cpu_echo_shutdown(cpu_echo, pollers):
     """clients half-close after their last frame: every echo, then the close frame, then FIN"""

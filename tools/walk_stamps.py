@@ -37,11 +37,14 @@ nb = (n + 63) // 64 if mode in (64, 65) else (n + 255) // 256
 for it in range(3):
     c.decode(b)
     c.sync()
-    out = np.zeros(nb * 4, np.uint64)
+    out = np.zeros(nb * 8, np.uint64)
     assert c.lib.wsc_debug_stamps(c.h, out.ctypes.data, nb) == 0
-    st = out.reshape(nb, 4).astype(np.int64)
+    st = out.reshape(nb, 8).astype(np.int64)
     t0 = st[:, 0].min()
     rel = (st - t0) / 100.0   # us
+    if st[:, 4].min() > 0:
+        pre = rel[:, 4] - rel[:, 0]
+        print(f"{wl} iter {it}: quad pre-pass med {np.median(pre):.1f} max {pre.max():.1f} us")
     cnt = rel[:, 1] - rel[:, 0]
     lb = rel[:, 2] - rel[:, 1]
     em = rel[:, 3] - rel[:, 2]

@@ -87,9 +87,16 @@ int main(int argc, char** argv) {
     for (int i = 1; i + 1 < argc; ++i)
         if (std::string(argv[i]) == "--devices") devices = atoi(argv[i + 1]);
     if (devices < 1) devices = 1;   // (more than visible: wsc_session_create fails, exit 2)
+    auto device_of = [devices](int poller) { return poller % devices; };   // poller p -> device p mod G
+    if (echo::has_flag(argc, argv, "--print-map")) {   // the mapping alone (no device touched)
+        printf("{\"pollers\": %d, \"devices\": %d, \"device_of_poller\": [", pollers, devices);
+        for (int p = 0; p < pollers; ++p) printf("%s%d", p ? ", " : "", device_of(p));
+        printf("]}\n");
+        return 0;
+    }
     const echo::Result r = echo::run(
-        [pipe, devices](int poller, int n) {
-            return std::unique_ptr<echo::Decoder>(new GpuDecoder(poller % devices, n, pipe));   // poller p -> device p % G
+        [pipe, device_of](int poller, int n) {
+            return std::unique_ptr<echo::Decoder>(new GpuDecoder(device_of(poller), n, pipe));
         },
         pollers, conns, frames, size, threads, 60, shut);
     echo::print_json(pipe ? "gpu: libwscodec wsc_session per poller, recv into pinned staging, submit r+1 / echo r / complete"
