@@ -1230,7 +1230,7 @@ struct WalkLds {
     uint32_t cons[G * WL], endst[G * WL];
     uint64_t abase[COMPACT ? G * WL : 1], ob0[COMPACT ? G * WL : 1];
     uint8_t rep[G * WL], r0[G * WL];   // (r0: the segment's first record in the lane's list)
-    PreState pre[(G == 1 && (4 * WL) % NT == 0) ? WL : 1];   // quad pre-pass results (one quad per segment)
+    PreState pre[(G == 1 && NT == 4 * WL) ? WL : 1];   // quad pre-pass results (one quad per segment)
 };
 
 // Count phase of a tile: each lane walks its G segments (first one s0; segments from seg_lim on
@@ -1258,7 +1258,7 @@ __device__ __forceinline__ SegCount tile_count(const WalkArgs& a, WalkLds<COMPAC
         const PreState* ps = pre && j == 0 ? L.pre + (lane < WL ? lane : 0) : nullptr;
         const uint64_t ss = a.seg_off[s];
         SegCount c;
-        if (ps && ps->full) {
+        if (ps && ps->full && ps->nf) {
             // the quad pre-pass walked the whole segment (plain BIN messages from a connection with
             // no fragmented message or frame open): its end state, without a serial walk -- what
             // walk_segment would return after those frames (mode 0, msgID advanced, no text)
@@ -1582,14 +1582,21 @@ __global__ __launch_bounds__(NT) void k_walk_fused(WalkArgs a) {
     uint32_t nrec;
     // quad pre-pass (one segment per 4 lanes, all waves): the leading plain BIN messages of each
     // segment, recorded in LDS; the walking lane continues after them
-    // (more walking lanes than quads: the quads take the block's segments NT / 4 at a time; if the
-    // first pass found no plain BIN message at all -- fragmented or text traffic -- the rest are skipped)
-    constexpr bool PRE = G == 1 && SPREAD == 0 && (4 * WL) % NT == 0;
+    // Only where the block has a quad per walking lane (one walking wave in four: modes 65, 16).
+    // With more walking lanes than quads (modes 64, 256) the quads would take the segments NT / 4
+    // at a time, one pass after another: measured slower there (the pipelined configs[2] walk on
+    // 16 CUs: 0.0618 -> 0.0648 ms per batch) or neutral (configs[1] 16 frames/segment).
+    // (The pass loop below also serves PASSES > 1; a pass finding no plain BIN message at all --
+    // fragmented or text traffic -- skips the rest.)
+    constexpr bool PRE = G == 1 && SPREAD == 0 && NT == 4 * WL;
     if constexpr (PRE) {
         constexpr uint32_t NQ = NT / 4, PASSES = WL / NQ;
         __shared__ uint32_t sh_found;
         if (lane == 0) sh_found = 0;
-        if (lane < WL) L.pre[lane].nf = 0;
+        if (lane < WL) {   // (segments no pass reaches -- skipped passes -- keep these)
+            L.pre[lane].nf = 0;
+            L.pre[lane].full = false;
+        }
         __syncthreads();
         if (a.quad_pre) {
             const uint32_t hint = a.stride_hint ? *a.stride_hint : 0u;
