@@ -729,6 +729,10 @@ def echo_configs(with_cpu=True):
         runs.append((f"64 conns x 2000 x 1 KiB, {P} poller(s)", ["--conns", "64", "--frames", "2000", "--size", "1024",
                                                                  "--client-threads", "4", "--pollers", str(P)],
                      ["gpu", "gpu_sync", "cpu_port"]))
+    # clients half-close after their last frame (the EOF rule: every message echoed before Close())
+    runs.append(("64 conns x 200 x 64 KiB, 4 pollers, clients shutdown(SHUT_WR) after the last frame",
+                 ["--conns", "64", "--frames", "200", "--size", "65536", "--client-threads", "4", "--pollers", "4",
+                  "--shutdown"], ["gpu", "cpu_port"]))
     bins = {"gpu": (gpu, []), "gpu_sync": (gpu, ["--sync"]), "cpu_port": (cpu, [])}
     res = {}
     for name, args, kinds in runs:

@@ -104,8 +104,8 @@ struct wsc_ctx {
     uint32_t u8_grid = 0;               // WSC_U8_GRID: k_u8_check workgroups (A/B experiments; 0 = 5 per CU)
     bool walk_tiled = true;             // WSC_WALK_TILED=0: the three-launch walk for mode 3 (A/B)
     bool quad_pre = true;               // WSC_QUAD_PRE=0: the fused walk without its quad pre-pass (A/B)
-    int xcd_map = 0;                    // WSC_XCD_MAP=1: unmask windows XCD-contiguous (A/B; measured slower:
-                                        // configs[4] COMPACT 0.945-0.955 -> 0.971 ms, headline 0.347 -> 0.359 ms)
+    uint32_t xcd_run = 8;               // WSC_XCD_RUN: unmask blocks per XCD run (1 = the hardware deal; one run
+                                        // per XCD over the whole grid measured slower: headline 0.347 -> 0.359 ms)
     bool ab_no_u8 = false;              // WSC_AB_NO_U8=1: A/B timing only -- binary unmask, no UTF-8 launches
                                         // (wrong for text batches; never set in tests or the bench)
     int walk_mode = 0;                  // WSC_WALK_MODE: 16, 32, 64, 65, 66, 256 or 3 pins the walk geometry (A/B, tests); 0 = auto
@@ -327,7 +327,7 @@ int wsc_create(int device, const wsc_config* cfg_in, wsc_ctx** out) {
     if (const char* e = std::getenv("WSC_AB_NO_U8"); e && e[0] == '1') c->ab_no_u8 = true;
     if (const char* e = std::getenv("WSC_WALK_TILED"); e && e[0] == '0') c->walk_tiled = false;
     if (const char* e = std::getenv("WSC_QUAD_PRE"); e && e[0] == '0') c->quad_pre = false;
-    if (const char* e = std::getenv("WSC_XCD_MAP"); e && *e) c->xcd_map = std::atoi(e) ? 1 : 0;
+    if (const char* e = std::getenv("WSC_XCD_RUN"); e && *e) c->xcd_run = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("WSC_WALK_MODE"); e && *e) {   // pin a walk geometry (tests, A/B): 16, 32, 64, 65, 66, 256 or 3
         const int m = std::atoi(e);
         c->walk_mode = (m == 16 || m == 32 || m == 64 || m == 65 || m == 66 || m == 256 || m == 3) ? m : 0;
@@ -571,7 +571,7 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     const bool sig_unmask = signal && !need_u8;
     U8Win uw{};
     uw.rearm = c->u8ctr + 32 * (c->u8par ^ 1u);
-    uw.grid_map = c->xcd_map == 1 ? 1u : 0u;
+    uw.xcd_run = c->xcd_run;
     if (need_u8) {
         uw.flag = c->win_flag;
         uw.map = c->win_map;

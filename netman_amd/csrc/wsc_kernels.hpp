@@ -160,8 +160,8 @@ struct U8Win {
     uint64_t* map;
     const uint32_t* count;
     uint32_t* rearm;             // the next decode's item counter (zeroed by the unmask: always launched)
-    uint32_t grid_map;           // bit 0: XCD-contiguous windows (block b -> logical block so that the
-                                 // blocks sharing an XCD, b mod 8, take one contiguous run of windows)
+    uint32_t xcd_run;            // blocks per XCD run: consecutive logical blocks (windows) on one XCD
+                                 // (0 / 1: the hardware's round-robin deal), see unmask_all
 };
 
 

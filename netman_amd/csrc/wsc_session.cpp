@@ -879,6 +879,14 @@ int wsc_session_eof(wsc_session* s, uint32_t conn) {
     Conn* c = lookup(s, conn);
     if (!c) return WSC_E_STATE;
     c->eof = true;
+    // a read that returned 0 may follow a reserve that placed the connection in the staging being
+    // filled with nothing in it: that empty region is dropped (else it would wait for a submit that
+    // wsc_session_pending() == 0 never asks for, and Close() would never come)
+    Stage& f = s->st[s->fill];
+    if (c->fill_epoch == s->fill_epoch && c->seg < f.seg_conn.size() && f.seg_len[c->seg] == 0) {
+        f.seg_conn[c->seg] = DEAD_SEG;
+        c->fill_epoch = ~0ull;
+    }
     maybe_eof(s, *c);
     return WSC_OK;
 }
