@@ -106,6 +106,8 @@ struct wsc_ctx {
     bool quad_pre = true;               // WSC_QUAD_PRE=0: the fused walk without its quad pre-pass (A/B)
     uint32_t xcd_run = 8;               // WSC_XCD_RUN: unmask blocks per XCD run (1 = the hardware deal; one run
                                         // per XCD over the whole grid measured slower: headline 0.347 -> 0.359 ms)
+    uint32_t enc_xcd_run = 1;           // WSC_ENC_XCD_RUN: the same for the encode copy (8 measured 0.381 ->
+                                        // 0.383-0.399 ms at 64 KiB, no change at 1 KiB: off)
     bool ab_no_u8 = false;              // WSC_AB_NO_U8=1: A/B timing only -- binary unmask, no UTF-8 launches
                                         // (wrong for text batches; never set in tests or the bench)
     int walk_mode = 0;                  // WSC_WALK_MODE: 16, 32, 64, 65, 66, 256 or 3 pins the walk geometry (A/B, tests); 0 = auto
@@ -328,6 +330,7 @@ int wsc_create(int device, const wsc_config* cfg_in, wsc_ctx** out) {
     if (const char* e = std::getenv("WSC_WALK_TILED"); e && e[0] == '0') c->walk_tiled = false;
     if (const char* e = std::getenv("WSC_QUAD_PRE"); e && e[0] == '0') c->quad_pre = false;
     if (const char* e = std::getenv("WSC_XCD_RUN"); e && *e) c->xcd_run = (uint32_t)std::strtoul(e, nullptr, 10);
+    if (const char* e = std::getenv("WSC_ENC_XCD_RUN"); e && *e) c->enc_xcd_run = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("WSC_WALK_MODE"); e && *e) {   // pin a walk geometry (tests, A/B): 16, 32, 64, 65, 66, 256 or 3
         const int m = std::atoi(e);
         c->walk_mode = (m == 16 || m == 32 || m == 64 || m == 65 || m == 66 || m == 256 || m == 3) ? m : 0;
@@ -807,6 +810,7 @@ static int launch_encode(wsc_ctx* c, const wsc_out_msg* msgs, uint32_t n, const 
     ca.tile_entries = c->enc_tile_entries;
     ca.lb_state = c->enc_lb_state;
     ca.n_lb = sblocks + 2;
+    ca.xcd_run = c->enc_xcd_run;
     uint64_t wins = (out_cap + ENC_WIN - 1) / ENC_WIN;   // the grid covers out_cap; waves past the total exit
     if (wins > c->enc_tile_entries) wins = c->enc_tile_entries;
     if (wins == 0) wins = 1;

@@ -146,6 +146,20 @@ __device__ __forceinline__ void store_run(uint8_t* p, u32x4 x, uint32_t lo, uint
     if (n & 1) *p = (uint8_t)y.x;
 }
 
+// XCD runs of blocks for the streaming kernels (unmask, encode copy).  Blocks are dealt
+// round-robin over the 8 XCDs (MI355X_MICROARCH.md, workgroup dispatch: blocks b and b + 8 share
+// one), so with the identity map neighbouring blocks' windows sit in different XCDs' L2s.  With
+// R > 1 each chunk of 8R blocks is remapped so that XCD x (b mod 8) takes R consecutive logical
+// blocks while the eight XCDs still stream one 8R-block region together.  A bijection on the full
+// chunks (the tail keeps the identity); placement changes speed only, never results.
+__device__ __forceinline__ uint32_t xcd_run_block(uint32_t bid, uint32_t grid, uint32_t R) {
+    if (R <= 1) return bid;
+    const uint32_t chunk = 8u * R;
+    if (bid >= grid / chunk * chunk) return bid;
+    const uint32_t j = bid % chunk;
+    return bid - j + (j & 7u) * R + (j >> 3);
+}
+
 template <int NT>
 __device__ __forceinline__ uint4 ld16(const uint8_t* p) {
     const u32x4 t = ld16v<NT>(p);

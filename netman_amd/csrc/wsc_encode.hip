@@ -330,7 +330,8 @@ __global__ __launch_bounds__(256) void k_encode_copy(EncCopyArgs a) {
     const uint32_t n = a.n_msgs;
     if (n == 0) return;
     const uint32_t lane = threadIdx.x & 63;
-    const uint64_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+    const uint64_t gw = __builtin_amdgcn_readfirstlane(xcd_run_block(blockIdx.x, gridDim.x, a.xcd_run) * 4 +
+                                                       (threadIdx.x >> 6));
     uint64_t limit = a.out_off[n];
     if (limit > a.out_cap) limit = a.out_cap;
     const uint64_t wbase = gw << ENC_WIN_SHIFT;

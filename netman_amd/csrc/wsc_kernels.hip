@@ -239,6 +239,13 @@ __device__ __forceinline__ uint4 rec_pack(const wsc_frame& fr, uint64_t seg_star
 #define WSC_WALK_SPEC 2
 #endif
 
+// A segment's inputs loaded ahead by the caller (the tiled walk pipelines them across tiles): its
+// bounds and the 16 bytes at its first frame.
+struct SegIn {
+    uint64_t start, end;
+    uint4 hdr;
+};
+
 // What the quad pre-pass (quad_prefix, below) already walked of a segment: its leading run of
 // plain complete BIN messages, recorded in LDS.  The serial walk continues after it.  Offsets are
 // relative to the segment start (the pre-pass runs only on segments < 4 GiB).
@@ -252,14 +259,15 @@ template <bool EMIT, bool COMPACT, uint32_t LS = 64, int SPEC_D = WSC_WALK_SPEC,
 __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, const SegCount& base,
                                                  const SegCount& own, uint4* lrec, WalkEnd* wend,
                                                  uint4* lrec2 = nullptr, uint32_t cap = 0, uint32_t tag = 0,
-                                                 const PreState* pre = nullptr, const uint4* hc_in = nullptr,
+                                                 const PreState* pre = nullptr, const SegIn* in = nullptr,
                                                  uint4* hc_out = nullptr) {
-    // hc_out / hc_in: the tiled walk's header cache -- its counting pass stores the 16 bytes at the
-    // segment's first frame (one coalesced 16 B store per lane), the emitting pass takes them from
-    // there instead of re-reading a scattered wire line per segment
+    // in: the segment's bounds and first 16 bytes, loaded ahead by the caller (the tiled walk);
+    // hc_out: its header cache -- the counting pass stores the 16 bytes at the segment's first
+    // frame (one coalesced 16 B store per lane), the emitting pass loads them from there instead
+    // of re-reading a scattered wire line per segment
     const uint8_t* __restrict__ w = a.wire;
-    const uint64_t seg_start = a.seg_off[s];
-    const uint64_t seg_end = a.seg_off[s + 1];
+    const uint64_t seg_start = in ? in->start : a.seg_off[s];
+    const uint64_t seg_end = in ? in->end : a.seg_off[s + 1];
 
     wsc_conn_state st = {};
     if (a.state_in) st = a.state_in[s];
@@ -801,7 +809,7 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
         for (int k = 0; k < SPEC_D; ++k) {
             hp[k] = pos + (uint64_t)k * stride;
             hc[k] = make_uint4(0, 0, 0, 0);
-            if (k == 0 && hc_in && pos == seg_start) hc[k] = hc_in[s];
+            if (k == 0 && in && pos == seg_start) hc[k] = in->hdr;
             else if (k == 0 || (stride != 0 && hp[k] + 2 <= seg_end)) hc[k] = hdr_load(w, a.n_bytes, hp[k]);
             else hp[k] = ~0ull;
         }
@@ -1239,7 +1247,7 @@ struct WalkLds {
 template <bool COMPACT, uint32_t KR, uint32_t NT, uint32_t G, uint32_t WL>
 __device__ __forceinline__ SegCount tile_count(const WalkArgs& a, WalkLds<COMPACT, KR, NT, G, WL>& L, uint32_t s0,
                                                uint32_t seg_lim, uint32_t lane, uint32_t& nrec, bool pre = false,
-                                               const uint4* hcache = nullptr) {
+                                               const SegIn* in = nullptr) {
     const SegCount zero = {};
     SegCount tot = zero;
     nrec = 0;
@@ -1256,7 +1264,8 @@ __device__ __forceinline__ SegCount tile_count(const WalkArgs& a, WalkLds<COMPAC
         WalkEnd we;
         const uint32_t cap = KR - nrec;
         const PreState* ps = pre && j == 0 ? L.pre + (lane < WL ? lane : 0) : nullptr;
-        const uint64_t ss = a.seg_off[s];
+        const SegIn* sin = j == 0 ? in : nullptr;
+        const uint64_t ss = sin ? sin->start : a.seg_off[s];
         SegCount c;
         if (ps && ps->full && ps->nf) {
             // the quad pre-pass walked the whole segment (plain BIN messages from a connection with
@@ -1280,7 +1289,7 @@ __device__ __forceinline__ SegCount tile_count(const WalkArgs& a, WalkLds<COMPAC
             we.replay = true;         // (nf <= cap and the segment is < 4 GiB)
         } else {
             c = walk_segment<false, COMPACT, WL>(a, s, zero, zero, L.rec + nrec * WL + lane, &we,
-                                                 L.rec2 + nrec * WL + lane, cap, j, ps, hcache);
+                                                 L.rec2 + nrec * WL + lane, cap, j, ps, sin);
         }
         const bool rep = we.replay;
         L.r0[q] = (uint8_t)nrec;
@@ -1661,25 +1670,61 @@ __global__ __launch_bounds__(NT) void k_walk_tiled(WalkArgs a, uint32_t per_bloc
     const uint32_t sb = bid * per_block < a.n_segs ? bid * per_block : a.n_segs;
     const uint32_t se = a.n_segs - sb < per_block ? a.n_segs : sb + per_block;
     const SegCount zero = {};
+    uint64_t t0 = 0, t1 = 0, t2 = 0;   // diagnostic stamps (WSC_DEBUG_STAMPS=1)
+    if (a.dbg && lane == 0) t0 = __builtin_amdgcn_s_memrealtime();
+    // Inputs are pipelined across tiles: while tile t is walked, tile t+1's first headers and
+    // tile t+2's bounds are already in flight (phase 1); tile t+1's bounds and cached headers
+    // (phase 2) -- so a tile costs no dependent round trip of its own.
+    auto bounds = [&](uint32_t t, SegIn& x) {
+        const uint32_t s = t + lane;
+        if (t < se && s < se) { x.start = a.seg_off[s]; x.end = a.seg_off[s + 1]; }
+        else x.start = x.end = 0;
+    };
+    auto first_hdr = [&](SegIn& x) {
+        x.hdr = x.end - x.start >= 2 ? hdr_load(a.wire, a.n_bytes, x.start) : make_uint4(0, 0, 0, 0);
+    };
     // ---- phase 1: the block's total ----
     SegCount tot = zero;
-    for (uint32_t t = sb; t < se; t += NT)
-        if (t + lane < se)
-            tot = sc_add(tot, walk_segment<false, COMPACT, NT, 4, true>(a, t + lane, zero, zero, nullptr, nullptr, nullptr, 0,
-                                                                        0, nullptr, nullptr, a.hdr_cache));
+    {
+        SegIn x0, x1, x2;
+        bounds(sb, x0);
+        bounds(sb + NT, x1);
+        first_hdr(x0);
+        for (uint32_t t = sb; t < se; t += NT) {
+            if (t + NT < se) first_hdr(x1);
+            bounds(t + 2 * NT, x2);
+            if (t + lane < se)
+                tot = sc_add(tot, walk_segment<false, COMPACT, NT, 4, true>(a, t + lane, zero, zero, nullptr, nullptr, nullptr, 0,
+                                                                            0, nullptr, &x0, a.hdr_cache));
+            x0 = x1;
+            x1 = x2;
+        }
+    }
     SegCount btot;
     (void)tile_scan<NT>(tot, L, wl, wave, btot);
+    if (a.dbg && lane == 0) t1 = __builtin_amdgcn_s_memrealtime();
     if (wave == 0) {
         const SegCount prefix = block_lookback(a, bid, btot, wl);
         if (wl == 0) L.prefix = prefix;
     }
     __syncthreads();
+    if (a.dbg && lane == 0) t2 = __builtin_amdgcn_s_memrealtime();
     const SegCount block_prefix = L.prefix;
     // ---- phase 2: tiles in order, each on top of the running prefix ----
     SegCount run = block_prefix;
+    auto cached = [&](uint32_t t, SegIn& x) {   // the header cache phase 1 wrote (coalesced)
+        bounds(t, x);
+        const uint32_t s = t + lane;
+        x.hdr = (t < se && s < se && a.hdr_cache) ? a.hdr_cache[s] : make_uint4(0, 0, 0, 0);
+        if (!a.hdr_cache) first_hdr(x);
+    };
+    SegIn y0, y1;
+    cached(sb, y0);
     for (uint32_t t = sb; t < se; t += NT) {
+        cached(t + NT, y1);
         uint32_t nrec;   // (lanes past the block's last segment count nothing)
-        const SegCount c = tile_count<COMPACT, KR, NT, 1>(a, L, t + lane, se, lane, nrec, false, a.hdr_cache);
+        const SegCount c = tile_count<COMPACT, KR, NT, 1>(a, L, t + lane, se, lane, nrec, false, &y0);
+        y0 = y1;
         SegCount ttot;
         const SegCount excl = tile_scan<NT>(c, L, wl, wave, ttot);
         tile_emit<COMPACT, KR, NT, 1>(a, L, sc_add(run, excl), nrec, t, se, lane);
@@ -1695,6 +1740,12 @@ __global__ __launch_bounds__(NT) void k_walk_tiled(WalkArgs a, uint32_t per_bloc
             run.bytes0 != want.bytes0 || run.bytes1 != want.bytes1) {
             __hip_atomic_fetch_or(a.lb_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_fetch_or(a.sticky, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (a.dbg) {
+            a.dbg[8 * bid + 0] = t0;
+            a.dbg[8 * bid + 1] = t1;
+            a.dbg[8 * bid + 2] = t2;
+            a.dbg[8 * bid + 3] = __builtin_amdgcn_s_memrealtime();
         }
     }
     if (se == a.n_segs && sb < se && lane == 0) write_summary<COMPACT>(a, sc_add(block_prefix, btot));

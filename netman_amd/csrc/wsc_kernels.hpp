@@ -196,6 +196,7 @@ struct EncCopyArgs {
     uint64_t tile_entries;
     uint32_t* lb_state;          // the scan's look-back state, re-armed by this launch
     uint32_t n_lb;
+    uint32_t xcd_run;            // blocks per XCD run (xcd_run_block)
 };
 
 }  // namespace wsc

@@ -414,21 +414,9 @@ __device__ __forceinline__ void unmask_all(uint8_t* __restrict__ dst, const uint
     if (blockIdx.x == 0 && threadIdx.x == 0 && u8w.rearm) *u8w.rearm = 0;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t waves_per_block = blockDim.x >> 6;
-    // XCD runs of windows.  Blocks are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md,
-    // workgroup dispatch: blocks b and b + 8 share one), so with the identity map neighbouring
-    // blocks' windows sit in different XCDs' L2s.  With R = xcd_run, each chunk of 8R blocks is
-    // remapped so that XCD x (b mod 8) takes R consecutive logical blocks (4R consecutive windows)
-    // while the eight XCDs still stream one 8R-block region together.  Measured: R = 8 streams the
-    // headline 1 GiB unmask in 0.319 ms instead of 0.335 (6.73 TB/s), configs[3] 1.307 vs 1.372 ms.
-    // A bijection on the full chunks (the tail keeps the identity); speed only, never results.
-    uint32_t bid = blockIdx.x;
-    if (const uint32_t R = u8w.xcd_run; R > 1) {
-        const uint32_t chunk = 8u * R;
-        if (bid < gridDim.x / chunk * chunk) {
-            const uint32_t j = bid % chunk;
-            bid = bid - j + (j & 7u) * R + (j >> 3);
-        }
-    }
+    // XCD runs of 4R consecutive windows (xcd_run_block, wsc_dev.hpp).  Measured: R = 8 streams the
+    // headline 1 GiB unmask in 0.319 ms instead of 0.335 (6.73 TB/s), configs[3] 1.316 vs 1.368 ms.
+    const uint32_t bid = xcd_run_block(blockIdx.x, gridDim.x, u8w.xcd_run);
     const uint32_t gw = __builtin_amdgcn_readfirstlane(bid * waves_per_block + (threadIdx.x >> 6));
     const uint32_t nw = gridDim.x * waves_per_block;
     const uint32_t n_spans = summary->n_spans;

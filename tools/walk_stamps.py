@@ -26,14 +26,16 @@ arena = torch.zeros(len(cfg["wire"]) + 64, dtype=torch.uint8, device=dev) if com
 fdst = torch.zeros(cfg["n_frames"] + 16, dtype=torch.int64, device=dev) if compact else None
 b = c.make_batch(t[0], t[1], None, t[2], t[3], t[4], t[5], compact=compact, arena=arena, frame_dst=fdst)
 n_cu = torch.cuda.get_device_properties(0).multi_processor_count
-if n > 256 * n_cu:   # the library's walk geometry (wsc_api.cpp walk_mode): three-launch walk, no stamps
-    print(f"{wl}: {n} segments -> three-launch walk (no per-block stamps)")
-    print(c.profile(b, 5) if False else "")
-    raise SystemExit(0)
 mode = int(os.environ.get("WSC_WALK_MODE", "0"))
 if mode == 0:
-    mode = 65 if n <= 64 * n_cu else 256
-nb = (n + 63) // 64 if mode in (64, 65) else (n + 255) // 256
+    mode = 65 if n <= 64 * n_cu else (256 if n <= 256 * n_cu else 3)
+if mode == 3:   # the tiled walk (wsc_api.cpp): a persistent grid of 2 blocks per CU; stamps: start,
+    # phase 1 counted, look-back done, phase 2 emitted
+    nb = max(1, min(2 * n_cu, (n + 255) // 256))
+    per = ((n + nb - 1) // nb + 255) // 256 * 256
+    nb = (n + per - 1) // per
+else:
+    nb = (n + 63) // 64 if mode in (64, 65) else (n + 255) // 256
 for it in range(3):
     c.decode(b)
     c.sync()
