@@ -52,8 +52,11 @@ def main():
     cfg = synth.fragmented_batch()
     print(f"configs[4]: {cfg['n_frames']} frames, {cfg['payload_bytes']} payload bytes, wire {len(cfg['wire'])}")
     ref = None
-    for compact, nt, window, cnt in [(False, 3 | 2 << 2, 4096, 0), (True, 3 | 2 << 2, 4096, 0), (True, 3 | 3 << 2, 4096, 0),
-                                     (True, 3 | 2 << 2, 8192, 0)]:
+    variants = [(False, 3 | 2 << 2, 4096, 0), (True, 3 | 2 << 2, 4096, 0), (True, 3 | 3 << 2, 4096, 0),
+                (True, 3 | 2 << 2, 8192, 0), (True, 3 | 0 << 2, 4096, 0), (True, 3 | 1 << 2, 4096, 0)]
+    if os.environ.get("WSC_PROBE_VARIANT"):   # one variant alone (a PMC pass per variant)
+        variants = [variants[int(os.environ["WSC_PROBE_VARIANT"])]]
+    for compact, nt, window, cnt in variants:
         a = run(cfg, compact, nt, window, iters, cnt)
         if a is not None:   # every COMPACT variant writes the same arena
             ref = a if ref is None else ref
