@@ -26,6 +26,7 @@ def build_codec(force=False, verbose=False):
     srcs = [os.path.join(CSRC, s) for s in SOURCES]
     deps = srcs + [os.path.join(CSRC, "wsc_kernels.hpp"), os.path.join(CSRC, "wsc_dev.hpp"),
                    os.path.join(CSRC, "wsc_unmask.inl"),
+                   os.path.join(CSRC, "wsc_u8.hpp"), os.path.join(CSRC, "wsc_u8check.inl"),
                    os.path.join(ROOT, "include", "wscodec.h")]
     if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= _newest(deps):
         return LIB

@@ -121,6 +121,7 @@ struct WalkArgs {
     uint32_t quad_pre;           // fused walk with one walking wave per 4: the quad pre-pass (WSC_QUAD_PRE=0: off, A/B)
     uint4* hdr_cache;            // tiled walk: per segment, the 16 bytes at its first frame (null: off)
     uint32_t* stride_hint;       // quad pre-pass: the stride the last decode ended with (first speculation)
+    uint32_t hw_order;           // look-back order = hardware workgroup index (no ticket atomic), walk_block_id
 };
 
 // k_u8_check runs AFTER the unmask: the unmask has already folded every text window that lies

@@ -82,6 +82,59 @@ def test_fuzz_walk_geometries(codec_lib, monkeypatch, compact, mode):
         c.close()
 
 
+def _run_streams(seed, n):
+    """Segments built from runs of equal-size masked BIN frames (the quad pre-pass speculates 16
+    headers per round trip at the last stride): run lengths 1..40, sizes across the 7/16-bit length
+    forms, a TEXT or PING frame between runs, and some segments cut inside a header or payload."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(n):
+        parts = []
+        for _ in range(int(rng.integers(1, 5))):
+            size = int(rng.choice([0, 1, 5, 60, 125, 126, 300, 1000, 4096]))
+            parts += [synth.frame(2, bytes(rng.integers(0, 256, size, dtype=np.uint8)), rng=rng)
+                      for _ in range(int(rng.integers(1, 41)))]
+            r = rng.random()
+            if r < 0.2:
+                parts.append(synth.frame(1, "ok ü".encode() * int(rng.integers(1, 4)), rng=rng))
+            elif r < 0.3:
+                parts.append(synth.frame(9, b"ping", rng=rng))
+        s = b"".join(parts)
+        if rng.random() < 0.2:
+            s = s[:int(rng.integers(1, len(s) + 1))]
+        out.append(s)
+    return out
+
+
+@pytest.mark.parametrize("compact,pre", [(False, "1"), (True, "1"), (False, "0")])
+def test_quad_prepass_runs(codec_lib, monkeypatch, compact, pre):
+    """The fused walk's quad pre-pass (mode 65, WSC_QUAD_PRE) on runs of equal frames, stride
+    changes, non-BIN frames that end a run, and segments cut mid-frame: records, bytes and carried
+    state equal the oracle's, and equal the serial walk's (WSC_QUAD_PRE=0)."""
+    monkeypatch.setenv("WSC_WALK_MODE", "65")
+    monkeypatch.setenv("WSC_QUAD_PRE", pre)
+    c = K.Codec(0, max_batch_bytes=64 << 20, max_segs=1 << 14, max_frames=1 << 18)
+    try:
+        for rep in range(2):   # the second decode starts from the first one's stride hint
+            _check_batch(c, _run_streams(4242 + rep, 600), compact=compact)
+    finally:
+        c.close()
+
+
+@pytest.mark.parametrize("cache", ["1", "0"])
+def test_tiled_walk_header_cache(codec_lib, monkeypatch, cache):
+    """The tiled walk (mode 3) with and without its per-segment header cache (WSC_HDR_CACHE), on
+    the fuzz corpus and on runs of equal frames."""
+    monkeypatch.setenv("WSC_WALK_MODE", "3")
+    monkeypatch.setenv("WSC_HDR_CACHE", cache)
+    c = K.Codec(0, max_batch_bytes=64 << 20, max_segs=1 << 14, max_frames=1 << 18)
+    try:
+        _check_batch(c, [random_stream(8000 + i, n_units=int(1 + i % 9), text_p=0.3) for i in range(500)])
+        _check_batch(c, _run_streams(77, 400), compact=True)
+    finally:
+        c.close()
+
+
 def _close_streams():
     from fuzz_streams import close_in_chain_stream, CLOSE_PAYLOADS
     streams = [close_in_chain_stream(11000 + i) for i in range(600)]
