@@ -103,6 +103,7 @@ struct wsc_ctx {
     uint32_t u8_inline_max = 256;
     uint32_t u8_grid = 0;               // WSC_U8_GRID: k_u8_check workgroups (A/B experiments; 0 = 5 per CU)
     bool walk_tiled = true;             // WSC_WALK_TILED=0: the three-launch walk for mode 3 (A/B)
+    int hdr_nt = -1;                    // WSC_HDR_NT: the walk's header loads non-temporal: 0 never, 1 always, default COMPACT batches
     bool walk_hw_order = false;         // WSC_WALK_HW_ORDER=1: walk blocks ordered by workgroup index, not a ticket
     bool quad_pre = true;               // WSC_QUAD_PRE=0: the fused walk without its quad pre-pass (A/B)
     uint32_t xcd_run = 8;               // WSC_XCD_RUN: unmask blocks per XCD run (1 = the hardware deal; one run
@@ -334,6 +335,7 @@ int wsc_create(int device, const wsc_config* cfg_in, wsc_ctx** out) {
     if (const char* e = std::getenv("WSC_WALK_TILED"); e && e[0] == '0') c->walk_tiled = false;
     if (const char* e = std::getenv("WSC_QUAD_PRE"); e && e[0] == '0') c->quad_pre = false;
     if (const char* e = std::getenv("WSC_WALK_HW_ORDER"); e && *e) c->walk_hw_order = e[0] == '1';
+    if (const char* e = std::getenv("WSC_HDR_NT"); e && *e) c->hdr_nt = e[0] == '1' ? 1 : 0;
     if (const char* e = std::getenv("WSC_XCD_RUN"); e && *e) c->xcd_run = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("WSC_ENC_XCD_RUN"); e && *e) c->enc_xcd_run = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("WSC_WALK_MODE"); e && *e) {   // pin a walk geometry (tests, A/B): 16, 32, 64, 65, 66, 256 or 3
@@ -463,6 +465,7 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     wa.hdr_cache = c->hdr_cache;
     wa.stride_hint = c->stride_hint;
     wa.hw_order = c->walk_hw_order ? 1u : 0u;
+    wa.hdr_nt = (c->hdr_nt < 0 ? compact : c->hdr_nt != 0) ? 1u : 0u;
 
     // walk geometry: the fused walk with blocks that fill the CUs once (64 lanes for up to 64
     // segments per CU, else 256), or -- for more segments than the chip holds lanes at once -- the
@@ -522,6 +525,7 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
         else if (mode == 16) hipLaunchKernelGGL((k_walk_fused<true, 16, 64, 1, 16, 0>), wgrid, wblk, 0, ws, wa);
         else if (mode == 32) hipLaunchKernelGGL((k_walk_fused<true, 16, 64, 1, 32, 0>), wgrid, wblk, 0, ws, wa);
         else if (wnt == 64) hipLaunchKernelGGL((k_walk_fused<true, 16, 64, 1, 64, 0>), wgrid, wblk, 0, ws, wa);
+        else if (mode == 257) hipLaunchKernelGGL((k_walk_fused<true, 4, 256, 1, 256, 0>), wgrid, wblk, 0, ws, wa);
         else hipLaunchKernelGGL((k_walk_fused<true, 16, 256, 1, 256, 0>), wgrid, wblk, 0, ws, wa);
     } else {
         if (mode == 65) hipLaunchKernelGGL((k_walk_fused<false, 16, 256, 1, 64, 0>), wgrid, wblk, 0, ws, wa);
@@ -529,6 +533,7 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
         else if (mode == 16) hipLaunchKernelGGL((k_walk_fused<false, 16, 64, 1, 16, 0>), wgrid, wblk, 0, ws, wa);
         else if (mode == 32) hipLaunchKernelGGL((k_walk_fused<false, 16, 64, 1, 32, 0>), wgrid, wblk, 0, ws, wa);
         else if (wnt == 64) hipLaunchKernelGGL((k_walk_fused<false, 16, 64, 1, 64, 0>), wgrid, wblk, 0, ws, wa);
+        else if (mode == 257) hipLaunchKernelGGL((k_walk_fused<false, 4, 256, 1, 256, 0>), wgrid, wblk, 0, ws, wa);
         else hipLaunchKernelGGL((k_walk_fused<false, 16, 256, 1, 256, 0>), wgrid, wblk, 0, ws, wa);
     }
     HIP_TRY(hipGetLastError());

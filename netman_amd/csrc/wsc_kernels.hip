@@ -60,12 +60,12 @@ __device__ __attribute__((noinline)) uint32_t u8_run_masked(uint32_t s, const ui
 // frame's first byte covers it (gfx950 takes unaligned dwordx4 addresses); the last 16 bytes of the
 // buffer are read byte by byte (nothing past n).  Bytes past the segment end are never used
 // (every use is guarded by `avail`).
-__device__ __forceinline__ uint4 hdr_load(const uint8_t* __restrict__ w, uint64_t n, uint64_t pos) {
-#ifdef WSC_HDR_NT   // experiment build (tools/build_variant.sh): non-temporal header loads
-    return load16u<1>(w, (int64_t)pos, n);
-#else
-    return load16_unaligned(w, (int64_t)pos, n);
-#endif
+// nt (WalkArgs.hdr_nt; the host sets it for COMPACT batches): a non-temporal load.  Measured
+// (profiles/r04_hdr_nt_ab.log, r04_hdr_nt_policy_ab.log; FETCH bytes unchanged): the configs[4]
+// (COMPACT) walk 91 -> 65 us, decode -2.5 %; in place the unmask re-reads the header lines and
+// loses what the walk gains (configs[1], [2], [3]: walk -2..-6 us, unmask +2..+6 us).
+__device__ __forceinline__ uint4 hdr_load(const uint8_t* __restrict__ w, uint64_t n, uint64_t pos, bool nt) {
+    return nt ? load16u<1>(w, (int64_t)pos, n) : load16_unaligned(w, (int64_t)pos, n);
 }
 __device__ __forceinline__ void hdr_bytes(const uint4& hd, uint32_t (&h)[14]) {
     const uint32_t d[4] = {hd.x, hd.y, hd.z, hd.w};
@@ -245,10 +245,11 @@ __device__ __forceinline__ uint4 rec_pack(const wsc_frame& fr, uint64_t seg_star
 #endif
 
 // A segment's inputs loaded ahead by the caller (the tiled walk pipelines them across tiles): its
-// bounds and the 16 bytes at its first frame.
+// bounds, its carried state and the 16 bytes at its first frame.
 struct SegIn {
     uint64_t start, end;
     uint4 hdr;
+    wsc_conn_state st;
 };
 
 // What the quad pre-pass (quad_prefix, below) already walked of a segment: its leading run of
@@ -275,7 +276,8 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
     const uint64_t seg_end = in ? in->end : a.seg_off[s + 1];
 
     wsc_conn_state st = {};
-    if (a.state_in) st = a.state_in[s];
+    if (in) st = in->st;
+    else if (a.state_in) st = a.state_in[s];
     uint64_t cont = st.cont_len;
     uint32_t msg = st.msg_id;
     uint32_t mode = st.message_mode;
@@ -815,7 +817,7 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
             hp[k] = pos + (uint64_t)k * stride;
             hc[k] = make_uint4(0, 0, 0, 0);
             if (k == 0 && in && pos == seg_start) hc[k] = in->hdr;
-            else if (k == 0 || (stride != 0 && hp[k] + 2 <= seg_end)) hc[k] = hdr_load(w, a.n_bytes, hp[k]);
+            else if (k == 0 || (stride != 0 && hp[k] + 2 <= seg_end)) hc[k] = hdr_load(w, a.n_bytes, hp[k], a.hdr_nt);
             else hp[k] = ~0ull;
         }
         if (hc_out && pos == seg_start) hc_out[s] = hc[0];
@@ -1100,7 +1102,7 @@ __device__ __forceinline__ void quad_prefix(const WalkArgs& a, uint32_t s, uint3
             const uint32_t idx = 4 * q + j;
             hp[j] = pos + (uint64_t)idx * stride;
             const bool ld = idx == 0 || (stride != 0 && hp[j] + 2 <= seg_end);
-            hd[j] = ld ? hdr_load(w, a.n_bytes, hp[j]) : make_uint4(0, 0, 0, 0);
+            hd[j] = ld ? hdr_load(w, a.n_bytes, hp[j], a.hdr_nt) : make_uint4(0, 0, 0, 0);
             if (!ld) hp[j] = ~0ull;
         }
         uint32_t fbits = 0, lbits = 0;
@@ -1689,15 +1691,21 @@ __global__ __launch_bounds__(NT) void k_walk_tiled(WalkArgs a, uint32_t per_bloc
     uint64_t t0 = 0, t1 = 0, t2 = 0;   // diagnostic stamps (WSC_DEBUG_STAMPS=1)
     if (a.dbg && lane == 0) t0 = __builtin_amdgcn_s_memrealtime();
     // Inputs are pipelined across tiles: while tile t is walked, tile t+1's first headers and
-    // tile t+2's bounds are already in flight (phase 1); tile t+1's bounds and cached headers
-    // (phase 2) -- so a tile costs no dependent round trip of its own.
+    // tile t+2's bounds and carried states are already in flight (phase 1); tile t+1's bounds,
+    // states and cached headers (phase 2) -- so a tile costs no dependent round trip of its own.
     auto bounds = [&](uint32_t t, SegIn& x) {
         const uint32_t s = t + lane;
-        if (t < se && s < se) { x.start = a.seg_off[s]; x.end = a.seg_off[s + 1]; }
-        else x.start = x.end = 0;
+        x.st = wsc_conn_state{};
+        if (t < se && s < se) {
+            x.start = a.seg_off[s];
+            x.end = a.seg_off[s + 1];
+            if (a.state_in) x.st = a.state_in[s];
+        } else {
+            x.start = x.end = 0;
+        }
     };
     auto first_hdr = [&](SegIn& x) {
-        x.hdr = x.end - x.start >= 2 ? hdr_load(a.wire, a.n_bytes, x.start) : make_uint4(0, 0, 0, 0);
+        x.hdr = x.end - x.start >= 2 ? hdr_load(a.wire, a.n_bytes, x.start, a.hdr_nt) : make_uint4(0, 0, 0, 0);
     };
     // ---- phase 1: the block's total ----
     SegCount tot = zero;
@@ -1796,6 +1804,8 @@ template __global__ void k_walk_fused<true, 16, 64, 1, 32, 0>(WalkArgs);
 template __global__ void k_walk_fused<true, 16, 64, 1, 64, 0>(WalkArgs);
 template __global__ void k_walk_fused<false, 16, 256, 1, 256, 0>(WalkArgs);
 template __global__ void k_walk_fused<true, 16, 256, 1, 256, 0>(WalkArgs);
+template __global__ void k_walk_fused<false, 4, 256, 1, 256, 0>(WalkArgs);
+template __global__ void k_walk_fused<true, 4, 256, 1, 256, 0>(WalkArgs);
 template __global__ void k_walk_fused<false, 16, 256, 1, 64, 0>(WalkArgs);
 template __global__ void k_walk_fused<true, 16, 256, 1, 64, 0>(WalkArgs);
 template __global__ void k_walk_fused<false, 16, 256, 1, 64, 16>(WalkArgs);

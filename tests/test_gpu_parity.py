@@ -63,14 +63,15 @@ def test_fuzz_single_batch(codec, compact):
 
 @pytest.mark.parametrize("compact,mode", [(False, 3), (True, 3), (False, 256), (True, 256), (False, 64), (True, 64),
                                           (False, 65), (True, 65), (False, 16), (True, 16), (False, 32), (True, 32),
-                                          (False, 66), (True, 66)])
+                                          (False, 66), (True, 66), (False, 257), (True, 257)])
 def test_fuzz_walk_geometries(codec_lib, monkeypatch, compact, mode):
     """Every walk geometry forced on the same fuzz batches (5..44 units with text and errors, and
     1..6 units): the fused walk with 64- and 256-lane blocks (16 LDS records per lane, longer
     segments re-walked, the rest emitted cooperatively), 256-lane blocks whose first wave walks and
     all four emit (mode 65), 64-lane blocks whose first 16 / 32 lanes walk (modes 16, 32: several
     walking waves per CU), 256-lane blocks whose 64 walking columns are spread 16 per wave (mode
-    66), and the tiled walk for many segments (mode 3)."""
+    66), one segment per lane with 4 LDS records per lane (mode 257: 3 blocks per CU), and the tiled
+    walk for many segments (mode 3)."""
     monkeypatch.setenv("WSC_WALK_MODE", str(mode))
     c = K.Codec(0, max_batch_bytes=64 << 20, max_segs=1 << 14, max_frames=1 << 18)
     try:
@@ -131,6 +132,20 @@ def test_tiled_walk_header_cache(codec_lib, monkeypatch, cache):
     try:
         _check_batch(c, [random_stream(8000 + i, n_units=int(1 + i % 9), text_p=0.3) for i in range(500)])
         _check_batch(c, _run_streams(77, 400), compact=True)
+    finally:
+        c.close()
+
+
+@pytest.mark.parametrize("mode", ["65", "3"])
+def test_nontemporal_header_loads(codec_lib, monkeypatch, mode):
+    """The walk's non-temporal header loads (COMPACT batches by default) forced on in-place
+    batches too (WSC_HDR_NT=1): the same records and bytes as the oracle's."""
+    monkeypatch.setenv("WSC_WALK_MODE", mode)
+    monkeypatch.setenv("WSC_HDR_NT", "1")
+    c = K.Codec(0, max_batch_bytes=64 << 20, max_segs=1 << 14, max_frames=1 << 18)
+    try:
+        _check_batch(c, [random_stream(9100 + i, n_units=int(1 + i % 30), text_p=0.3) for i in range(400)])
+        _check_batch(c, _run_streams(91, 300), compact=True)
     finally:
         c.close()
 
