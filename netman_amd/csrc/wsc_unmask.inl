@@ -299,6 +299,98 @@ __device__ __forceinline__ bool unmask_window_lanes(uint8_t* __restrict__ dst, c
     return true;
 }
 
+#ifndef WSC_COMPACT_EDGE2   // (-DWSC_COMPACT_EDGE2=0: the one-pass unmask_window_lanes<true>, for A/B)
+#define WSC_COMPACT_EDGE2 1
+#endif
+// COMPACT, lane-parallel, in two passes (the encoder's edge pass, wsc_encode.hip): (1) every piece
+// lying inside one span is one byte-aligned 16-byte store at its arena offset, and the pieces that
+// meet a span edge are listed -- id and wire bytes -- in the wave's LDS stage; (2) one lane per
+// listed piece stores the run of each span it meets.  The per-span run stores (store_run: a byte
+// shift and up to four partial stores) then run once per wave for all of a window's edge pieces
+// instead of once per 1 KiB slice for every lane, and the kernel needs 88 VGPRs instead of 110 (5
+// waves per SIMD instead of 4).  Measured (profiles/r04_compact_edge2_ab.log, same box): configs[4]
+// unmask 0.895 -> 0.859 ms (5.44 -> 5.63 TB/s), decode 0.956 -> 0.919 ms, pipelined 1.018 ->
+// 0.916 ms per batch.  stage: 288 uint4 per wave (256 pieces' bytes, then 256 u16 ids).  Same
+// results as unmask_window_lanes<true>.
+template <int P, int NT>
+__device__ __forceinline__ bool unmask_window_lanes_c(uint8_t* __restrict__ dst, const Span& sp, bool valid,
+                                                      uint32_t n_spans, uint32_t r0, uint64_t wbase, uint32_t lane,
+                                                      const u32x4 (&v)[P], uint4* __restrict__ stage) {
+    constexpr int32_t WB = 1024 * P;
+    static_assert(P * 64 <= 256, "stage holds 256 pieces");
+    int32_t rd = WB + 64, re = WB + 64;   // window-relative wire [start, end), clipped to [-1, WB + 64]
+    uint32_t key = 0;
+    int64_t sd = 0;                       // dst - src
+    if (valid) {
+        const int64_t d0 = (int64_t)sp.src - (int64_t)wbase, d1 = d0 + (int64_t)sp.len;
+        rd = (int32_t)(d0 < -1 ? -1 : (d0 > WB + 64 ? WB + 64 : d0));
+        re = (int32_t)(d1 < -1 ? -1 : (d1 > WB + 64 ? WB + 64 : d1));
+        key = sp.key;
+        sd = (int64_t)sp.dst - (int64_t)sp.src;
+    }
+    const uint64_t inwin = __ballot(rd < WB);
+    const uint32_t nl = (uint32_t)__builtin_popcountll(inwin);
+    if (nl == 64 && __shfl(re, 63) < WB && r0 + 64 < n_spans) return false;
+    const uint32_t sd_lo = (uint32_t)sd, sd_hi = (uint32_t)((uint64_t)sd >> 32);
+    const int32_t st0 = nl == 0 ? 0 : (nl >= 32 ? 32 : (int32_t)((1u << (32 - __builtin_clz(nl))) >> 1));
+    auto find = [&](int32_t pr) -> int32_t {   // largest t < nl with rd[t] <= pr (0 if none)
+        int32_t lo = -1;
+        for (int32_t st = st0; st >= 1; st >>= 1) {
+            const int32_t c = lo + st;
+            const int32_t dv = __shfl(rd, c & 63);
+            if (c < (int32_t)nl && dv <= pr) lo = c;
+        }
+        return lo < 0 ? 0 : lo;
+    };
+    uint16_t* const ids = reinterpret_cast<uint16_t*>(stage + 256);
+    // ---- pass 1: pieces inside one span ----
+    uint32_t n_edge = 0;
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+        const int32_t pr = k * 1024 + (int32_t)lane * 16;
+        const int32_t a = find(pr);
+        const int32_t dA = __shfl(rd, a & 63), eA = __shfl(re, a & 63), dB = __shfl(rd, (a + 1) & 63);
+        const uint32_t ka = __shfl(key, a & 63), al = __shfl(sd_lo, a & 63), ah = __shfl(sd_hi, a & 63);
+        const bool inside = a < (int32_t)nl && dA <= pr && pr + 16 <= eA;
+        if (inside) st16u<NT>(dst + ((int64_t)((uint64_t)ah << 32 | al) + (int64_t)wbase + pr), v[k] ^ ka);
+        const bool meets = (a < (int32_t)nl && dA < pr + 16 && eA > pr) || (a + 1 < (int32_t)nl && dB < pr + 16);
+        const bool edge = !inside && meets;
+        const uint64_t em = __ballot(edge);
+        if (edge) {
+            const uint32_t slot = n_edge + __builtin_amdgcn_mbcnt_hi((uint32_t)(em >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)em, 0u));
+            ids[slot] = (uint16_t)(k * 64 + lane);
+            stage[slot] = make_uint4(v[k][0], v[k][1], v[k][2], v[k][3]);
+        }
+        n_edge += (uint32_t)__builtin_popcountll(em);
+    }
+    if (n_edge == 0) return true;
+    __builtin_amdgcn_wave_barrier();
+    // ---- pass 2: one edge piece per lane, each span it meets ----
+    for (uint32_t base = 0; base < n_edge; base += 64) {
+        const bool act = base + lane < n_edge;
+        const uint32_t pid = act ? ids[base + lane] : 0u;
+        const int32_t pr = (int32_t)((pid >> 6) * 1024 + (pid & 63) * 16);
+        const uint4 xs = act ? stage[base + lane] : make_uint4(0, 0, 0, 0);
+        const u32x4 x = {xs.x, xs.y, xs.z, xs.w};
+        int32_t t = find(pr);
+        bool go = act;
+        while (__ballot(go)) {
+            const int32_t dt = __shfl(rd, t & 63), et = __shfl(re, t & 63);
+            const uint32_t kt = __shfl(key, t & 63), tl = __shfl(sd_lo, t & 63), th = __shfl(sd_hi, t & 63);
+            go = go && t < (int32_t)nl && dt < pr + 16;
+            if (go) {
+                const int32_t l = (dt > pr ? dt : pr) - pr, h = (et < pr + 16 ? et : pr + 16) - pr;
+                if (l < h)
+                    store_run<NT>(dst + ((int64_t)((uint64_t)th << 32 | tl) + (int64_t)wbase + pr + l), x ^ kt,
+                                  (uint32_t)l, (uint32_t)h);
+            }
+            ++t;
+        }
+    }
+    __builtin_amdgcn_wave_barrier();   // (the stage is reused by the wave's next window)
+    return true;
+}
+
 // Deferred text (k_u8_check runs after this kernel): a window the walk flagged lies inside one
 // UTF-8 item, so the wave that has just unmasked it folds its DFA map from the registers (text is
 // read from HBM once) and publishes it in win_map; the check reads only the items' partial windows.
@@ -311,6 +403,8 @@ struct U8Block {
 };
 // (namespace scope: allocated only in the kernels that reach it, the U8 instantiations)
 __shared__ U8Block g_u8b;
+// COMPACT edge stage of the binary variants (unmask_window_lanes_c; U8 variants use g_u8b.stage)
+__shared__ uint4 c_stage[4][288];
 
 // The fold of a window whose first 4 KiB the caller has written to the wave's stage: tables (built
 // once per workgroup), then the map of every 4 KiB group.  COMPACT calls it out of line: its window
@@ -469,8 +563,16 @@ __device__ __forceinline__ void unmask_all(uint8_t* __restrict__ dst, const uint
         // span lookup; more than 64 spans in one window falls back to the serial span walk.
         Span sp;
         const bool valid = load_span_lane(spans, n_spans, r, lane, sp);
-        if (!unmask_window_lanes<COMPACT, P, NT>(dst, sp, valid, n_spans, r, wbase, lane, v, pm))
-            unmask_window_general<COMPACT, P, NT>(dst, src, src_bytes, total, spans, n_spans, r, wbase, lofs);
+        bool done;
+        if constexpr (COMPACT && WSC_COMPACT_EDGE2 && P == 4) {
+            uint4* stage;
+            if constexpr (U8) stage = g_u8b.stage[(threadIdx.x >> 6) & 3];   // (the fold's stage: fast-path windows only)
+            else stage = c_stage[(threadIdx.x >> 6) & 3];
+            done = unmask_window_lanes_c<P, NT>(dst, sp, valid, n_spans, r, wbase, lane, v, stage);
+        } else {
+            done = unmask_window_lanes<COMPACT, P, NT>(dst, sp, valid, n_spans, r, wbase, lane, v, pm);
+        }
+        if (!done) unmask_window_general<COMPACT, P, NT>(dst, src, src_bytes, total, spans, n_spans, r, wbase, lofs);
     }
 }
 
