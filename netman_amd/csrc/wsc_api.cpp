@@ -625,6 +625,7 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
         // 3 waves/SIMD without the large path's spills measured slower: 64 KiB TEXT check 79 -> 95 us)
         if (c->u8_chains == 1) hipLaunchKernelGGL(k_u8_check<1>, ug, dim3(256), 0, st, ua);
         else if (c->u8_chains == 4) hipLaunchKernelGGL(k_u8_check<4>, ug, dim3(256), 0, st, ua);
+        else if (c->u8_chains == 8) hipLaunchKernelGGL(k_u8_check<8>, ug, dim3(256), 0, st, ua);
         else hipLaunchKernelGGL(k_u8_check<2>, ug, dim3(256), 0, st, ua);
         HIP_TRY(hipGetLastError());
     }

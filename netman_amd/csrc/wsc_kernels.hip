@@ -1793,6 +1793,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
 template __global__ void k_u8_check<1>(U8Args);
 template __global__ void k_u8_check<2>(U8Args);
 template __global__ void k_u8_check<4>(U8Args);
+template __global__ void k_u8_check<8>(U8Args);
 
 // explicit instantiations used by the host code: 16 frame records per lane, one segment per
 // lane, blocks of 64 or 256 lanes; batches of more segments use the three-launch walk below

@@ -406,6 +406,9 @@ __shared__ U8Block g_u8b;
 // COMPACT edge stage of the binary variants (unmask_window_lanes_c; U8 variants use g_u8b.stage)
 __shared__ uint4 c_stage[4][288];
 
+#ifndef WSC_FOLD_NCH   // independent DFA chains per 64-byte lane chunk in the fold (A/B: tools/build_variant.sh)
+#define WSC_FOLD_NCH 4
+#endif
 // The fold of a window whose first 4 KiB the caller has written to the wave's stage: tables (built
 // once per workgroup), then the map of every 4 KiB group.  COMPACT calls it out of line: its window
 // loop keeps more registers live, and the fold inlined there pushed it past 128 VGPRs (spill)
@@ -468,7 +471,7 @@ __device__ __forceinline__ void fold_staged(const u32x4* v, uint32_t key, U8Win 
         }
         __builtin_amdgcn_wave_barrier();
         bool plain;
-        const uint64_t pm = u8_chunk_map<2, U8P_NONE>(b.t, q, 0u, 64u, plain);
+        const uint64_t pm = u8_chunk_map<WSC_FOLD_NCH, U8P_NONE>(b.t, q, 0u, 64u, plain);
         m = u8m_then(m, u8_wave_map(pm, plain, lane));
     }
     if (lane == 0) {
