@@ -1779,7 +1779,10 @@ __global__ __launch_bounds__(NT) void k_walk_tiled(WalkArgs a, uint32_t per_bloc
 // extra workgroups of the unmask launch, waiting on an unmask-done counter, it measured no faster
 // on binary batches and far slower on text: profiles/r04_u8_merge_ab.log, DESIGN.md "Round 4".)
 template <uint32_t NCH>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_u8_check(U8Args a) {
+#ifndef WSC_CHECK_WPE   // waves per SIMD k_u8_check is built for (A/B: tools/build_variant.sh)
+#define WSC_CHECK_WPE 4
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WSC_CHECK_WPE))) void k_u8_check(U8Args a) {
     __shared__ U8Lds T;
     __shared__ uint4 stage[4][U8_STAGE];
     u8_check_run<NCH>(a, T, stage, blockIdx.x, gridDim.x);
