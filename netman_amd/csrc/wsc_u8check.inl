@@ -147,6 +147,13 @@ __device__ __forceinline__ void u8_remask(const U8Args& a, uint32_t seg, uint64_
 // the chip's VALU cycles).
 // The check's work for workgroup `bid` of `nblk` check workgroups.  T / stage: the workgroup's LDS
 // tables and per-wave stages.
+// WSC_CHECK_PREFETCH 1: a small unit's data loads go out one unit ahead.  Off: the second 16-VGPR
+// buffer pushed the kernel past 128 VGPRs into 20 B of spills; without it 127 VGPRs and none, and
+// 1 KiB TEXT 0.218 -> 0.214 ms, 64 KiB 0.417 -> 0.413 ms (profiles/r04_check_variants_ab.log;
+// built for 5 waves per SIMD instead, 96 VGPRs with 112-188 B of spills, the check ran 2.5-5x slower)
+#ifndef WSC_CHECK_PREFETCH
+#define WSC_CHECK_PREFETCH 0
+#endif
 template <uint32_t NCH>
 __device__ __forceinline__ void u8_check_run(const U8Args& a, U8Lds& T, uint4 (*stage)[U8_STAGE], uint32_t bid,
                                              uint32_t nblk) {
@@ -333,7 +340,7 @@ __device__ __forceinline__ void u8_check_run(const U8Args& a, U8Lds& T, uint4 (*
     if (gw < n_units) {
         unit_items(gw, xc);
         cur_small = unit_small(xc);
-        if (cur_small) unit_data(xc, qc);
+        if (cur_small && WSC_CHECK_PREFETCH) unit_data(xc, qc);
     }
     if (gw + nw < n_units) unit_items(gw + nw, xn);
     for (uint32_t u = gw; u < n_units; u += nw) {
@@ -343,6 +350,7 @@ __device__ __forceinline__ void u8_check_run(const U8Args& a, U8Lds& T, uint4 (*
         bool nsmall = false;
         u32x4 qn[4] = {};
         if (cur_small) {
+            if (!WSC_CHECK_PREFETCH) unit_data(xc, qc);
             // restaged so that row r (lanes 16r..16r+15) holds item r in 64-byte chunks (items
             // <= 1 KiB hold no window).  The row's full item is needed only by the verdict: its
             // load overlaps the fold.
@@ -357,7 +365,7 @@ __device__ __forceinline__ void u8_check_run(const U8Args& a, U8Lds& T, uint4 (*
             const uint64_t rm = u8_row_maps(pm, lane);
             if (un < n_units) {
                 nsmall = unit_small(xn);
-                if (nsmall) unit_data(xn, qn);
+                if (nsmall && WSC_CHECK_PREFETCH) unit_data(xn, qn);
             }
             settle(pact && pret + pcnt == pn, pseg);
             // the unit's items: failures applied at once; composite items counted per run of
@@ -393,7 +401,7 @@ __device__ __forceinline__ void u8_check_run(const U8Args& a, U8Lds& T, uint4 (*
             unit_large(i0, cnt);
             if (un < n_units) {
                 nsmall = unit_small(xn);
-                if (nsmall) unit_data(xn, qn);
+                if (nsmall && WSC_CHECK_PREFETCH) unit_data(xn, qn);
             }
         }
         xc = xn;
