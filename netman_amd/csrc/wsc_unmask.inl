@@ -24,7 +24,21 @@ namespace wsc {
 // General window: several spans overlap it (small frames), or it is the last, partial window.
 // Builds a per-byte key from every span that overlaps each 16-byte piece.
 template <bool COMPACT, int P, int NT>
-__device__ __attribute__((noinline)) void unmask_window_general(
+// Inlined (WSC_GENERAL_INLINE=1, the default): as an out-of-line call the general window cost the
+// kernel its live registers across the call (in place 116 VGPRs, 4 waves per SIMD; 52 B of spills
+// when built for 5).  Inlined, in place needs 84 VGPRs (96 with the UTF-8 fold), COMPACT 72 (80),
+// and every P = 4 unmask runs at 5 waves per SIMD without spills: headline 3,064 -> 3,157 GiB/s,
+// configs[1] 0.400 -> 0.382 ms, configs[3] 1.357 -> 1.305 ms, 64 KiB TEXT 0.415 -> 0.393 ms
+// (profiles/r04_unmask_inline_ab.log).
+#ifndef WSC_GENERAL_INLINE
+#define WSC_GENERAL_INLINE 1
+#endif
+#if WSC_GENERAL_INLINE
+__device__ __forceinline__
+#else
+__device__ __attribute__((noinline))
+#endif
+void unmask_window_general(
     uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, uint64_t src_bytes, uint64_t total,
     const Span* __restrict__ spans, uint32_t n_spans, uint32_t r, uint64_t wbase, uint32_t lofs) {
     constexpr uint32_t WB = 1024u * P;
@@ -585,7 +599,10 @@ __device__ __forceinline__ void unmask_all(uint8_t* __restrict__ dst, const uint
 // workgroups that re-armed lb_state release it before counting (the next walk may run while this
 // grid's tail drains).
 template <bool COMPACT, int P, int NT, int MINW = 1, bool U8 = false>
-__global__ __launch_bounds__(256, (P == 4 ? 4 : 2) * MINW) void k_unmask(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src,
+#ifndef WSC_UNMASK_WPE   // waves per SIMD the P = 4 unmask kernels are built for (with the general window inlined)
+#define WSC_UNMASK_WPE 5
+#endif
+__global__ __launch_bounds__(256, (P == 4 ? WSC_UNMASK_WPE : 2) * MINW) void k_unmask(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src,
                                                 uint64_t src_bytes, uint64_t total,
                                                 const Span* __restrict__ spans,
                                                 const uint32_t* __restrict__ tile_first,
