@@ -315,6 +315,11 @@ int wsc_profile(wsc_ctx* ctx, const wsc_batch* batch, int iters, double* out_ms)
  * emitted, quad pre-pass done (0 if none), 3 reserved.  `out` has room for 8 * max_blocks.     */
 int wsc_debug_stamps(wsc_ctx* ctx, uint64_t* out, uint32_t max_blocks);
 
+/* Diagnostics: the header-walk geometry the context's last decode launched (*mode: 16, 32, 64, 65,
+ * 66, 256, 257 = fused walks, 3 = tiled or three-launch; 0 before any decode) and its block count.
+ * Tests use it to check that a geometry pinned with WSC_WALK_MODE really ran.                   */
+int wsc_walk_info(wsc_ctx* ctx, uint32_t* mode, uint32_t* blocks);
+
 /* ---- session: the per-connection DecodePacket() mirror (C++ host side above the ABI) ---------
  * One session per poller thread (eventloop/epoll.go:36-143).  Per round the poller reads each
  * ready connection once -- straight into the session's pinned staging with wsc_session_reserve +
@@ -360,6 +365,16 @@ int wsc_debug_stamps(wsc_ctx* ctx, uint64_t* out, uint32_t max_blocks);
  * close_code 1000 and err 0 -- Close() -- as the connection's last event; an incomplete frame at
  * the EOF is dropped (the reference's next read of it returns io.EOF).  Do NOT close the socket on
  * the zero-byte read itself: that loses the messages still queued or in flight.
+ *
+ * Byte source and TLS.  The staging takes the connection's POST-TLS byte stream: exactly what the
+ * reference's readData returns (baseconnect.go:347-353) -- unix.Read on the fd for a plain
+ * connection, tls.Conn.Read on the layer built at baseconnect.go:56-63 when TLS is on (wss; the
+ * poller completes the TLS handshake first, epoll.go:85-102).  The codec never sees ciphertext.  A
+ * tls.Conn returns at most one record's plaintext per Read and keeps the rest in its own buffers,
+ * which level-triggered epoll cannot see: a TLS reader fills its reserved room with repeated Reads
+ * until the layer reports EAGAIN (or the room is full, and then reads again next round without
+ * waiting for EPOLLIN), and maps the layer's io.EOF to wsc_session_eof.  INTEGRATION.md has both
+ * branches of the Go shim.
  *
  * Livelock guard: a batch in which one connection's whole segment (max_batch_bytes of its bytes)
  * decoded nothing -- possible only for a header or PING / CLOSE frame longer than the batch, i.e.

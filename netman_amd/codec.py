@@ -121,6 +121,7 @@ SIGNATURES = {
     "wsc_encode_host": (_I, [_P, _P, _U32, _P, _U64, _P, _U64, _P]),
     "wsc_profile": (_I, [_P, C.POINTER(WscBatch), _I, C.POINTER(C.c_double)]),
     "wsc_debug_stamps": (_I, [_P, _P, _U32]),
+    "wsc_walk_info": (_I, [_P, C.POINTER(_U32), C.POINTER(_U32)]),
     "wsc_session_create": (_I, [_I, C.POINTER(WscConfig), _U32, C.POINTER(_P)]),
     "wsc_session_destroy": (_I, [_P]),
     "wsc_session_open": (_I, [_P, C.POINTER(_U32)]),
@@ -277,6 +278,12 @@ class Codec:
     def decode_split(self, batch: WscBatch, walk_stream: int, unmask_stream: int):
         """walk on walk_stream, UTF-8 check + unmask on unmask_stream (wsc_decode_split)"""
         _check(self.lib.wsc_decode_split(self.h, C.byref(batch), walk_stream, unmask_stream), "wsc_decode_split")
+
+    def walk_info(self) -> tuple[int, int]:
+        """(geometry, blocks) of the last decode's header walk (wsc_walk_info)"""
+        m, b = C.c_uint32(), C.c_uint32()
+        _check(self.lib.wsc_walk_info(self.h, C.byref(m), C.byref(b)), "wsc_walk_info")
+        return m.value, b.value
 
     def error_flags(self, clear: bool = False) -> int:
         """sticky error bits of every decode/encode on this context (wsc_error_flags): bit0 frame
@@ -502,6 +509,31 @@ class Session:
         C.memmove(p.value, data, k)
         _check(self.lib.wsc_session_commit(self.h, conn, k), "wsc_session_commit")
         return k
+
+    def read_tls(self, conn: int, layer, max_bytes: int):
+        """INTEGRATION.md's Session.ReadTLS: with TLS on, readData reads through the tls.Conn
+        (server/baseconnect.go:347-353), which returns at most one record's plaintext per Read and
+        keeps later records in its own buffers, out of epoll's sight.  So read into the reserved
+        room until the layer reports EAGAIN (layer.read raises BlockingIOError) or the room is
+        full.  layer.read(n) returns up to n plaintext bytes, b"" for io.EOF.
+        Returns (bytes read, more, eof): more = the room filled, read again next round."""
+        p, avail = C.c_void_p(), C.c_uint64()
+        _check(self.lib.wsc_session_reserve(self.h, conn, max_bytes, C.byref(p), C.byref(avail)), "wsc_session_reserve")
+        if not p.value:
+            return 0, False, False
+        n, eof = 0, False
+        while n < avail.value:
+            try:
+                b = layer.read(avail.value - n)
+            except BlockingIOError:
+                break
+            if not b:
+                eof = True
+                break
+            C.memmove(p.value + n, b, len(b))
+            n += len(b)
+        _check(self.lib.wsc_session_commit(self.h, conn, n), "wsc_session_commit")
+        return n, (n == avail.value and not eof), eof
 
     def submit(self):
         _check(self.lib.wsc_session_submit(self.h), "wsc_session_submit")

@@ -338,9 +338,9 @@ int wsc_create(int device, const wsc_config* cfg_in, wsc_ctx** out) {
     if (const char* e = std::getenv("WSC_HDR_NT"); e && *e) c->hdr_nt = e[0] == '1' ? 1 : 0;
     if (const char* e = std::getenv("WSC_XCD_RUN"); e && *e) c->xcd_run = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("WSC_ENC_XCD_RUN"); e && *e) c->enc_xcd_run = (uint32_t)std::strtoul(e, nullptr, 10);
-    if (const char* e = std::getenv("WSC_WALK_MODE"); e && *e) {   // pin a walk geometry (tests, A/B): 16, 32, 64, 65, 66, 256 or 3
+    if (const char* e = std::getenv("WSC_WALK_MODE"); e && *e) {   // pin a walk geometry (tests, A/B): 16, 32, 64, 65, 66, 256, 257 or 3
         const int m = std::atoi(e);
-        c->walk_mode = (m == 16 || m == 32 || m == 64 || m == 65 || m == 66 || m == 256 || m == 3) ? m : 0;
+        c->walk_mode = (m == 16 || m == 32 || m == 64 || m == 65 || m == 66 || m == 256 || m == 257 || m == 3) ? m : 0;
     }
     if (const char* e = std::getenv("WSC_U8_INLINE_MAX"); e && *e)   // test knob: 0 sends all text chip-wide
         c->u8_inline_max = (uint32_t)std::strtoul(e, nullptr, 10);
@@ -900,6 +900,13 @@ int wsc_debug_stamps(wsc_ctx* c, uint64_t* out, uint32_t max_blocks) {
     HIP_TRY(hipDeviceSynchronize());
     if (max_blocks > c->max_walk_blocks) max_blocks = c->max_walk_blocks;
     HIP_TRY(hipMemcpy(out, c->dbg, (uint64_t)max_blocks * 8 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    return WSC_OK;
+}
+
+int wsc_walk_info(wsc_ctx* c, uint32_t* mode, uint32_t* blocks) {
+    if (!c || !mode || !blocks) return fail(WSC_E_INVAL, "NULL argument");
+    *mode = c->walk_used;
+    *blocks = c->walk_blocks;
     return WSC_OK;
 }
 

@@ -261,6 +261,43 @@ struct PreState {
     uint32_t msg, stride;  // msgID after the run; the stride it speculated with last
     bool full;             // the run reached the segment's end (< 2 bytes left): no serial walk
 };
+
+// A frame the pre-pass takes -- a plain complete masked BIN message, the serial walk's `fast`
+// path -- as the record walk_segment would keep for it (rec_pack, tag 0: one segment per lane)
+__device__ __forceinline__ uint4 pre_record(uint64_t hdr_off, uint32_t plen, uint32_t mask, uint32_t hl,
+                                            uint64_t seg_start) {
+    wsc_frame fr{};
+    fr.hdr_off = hdr_off;
+    fr.payload_len = plen;
+    fr.mask = mask;
+    fr.opcode = 2;
+    fr.fin = 1;
+    fr.kind = WSC_FK_MESSAGE;
+    fr.mode = 2;
+    fr.err = WSC_ERR_NONE;
+    fr.hdr_len = (uint8_t)hl;
+    fr.flags = WSC_FF_UNMASKED;
+    return rec_pack(fr, seg_start, plen != 0, 0);
+}
+
+// What walk_segment returns for a segment the pre-pass walked to its end (a connection with no
+// fragmented message or frame open, status OPEN: the pre-pass runs only then) -- mode 0 after a
+// FIN message, msgID advanced, no text, nothing in progress.  Its LDS records hold the segment.
+__device__ __forceinline__ WalkEnd pre_end(const PreState& p, uint64_t seg_start, uint32_t status) {
+    WalkEnd we{};
+    we.pos = seg_start + p.pos;
+    we.cont = 0;
+    we.last_dend = seg_start + p.pend;
+    we.frem = we.flen = 0;
+    we.fmask = we.fhdr = 0;
+    we.msg = p.msg;
+    we.mode = 0;
+    we.status = status;
+    we.close_code = we.err = 0;
+    we.u8dfa = we.pdfa = 0;
+    we.replay = true;
+    return we;
+}
 template <bool EMIT, bool COMPACT, uint32_t LS = 64, int SPEC_D = WSC_WALK_SPEC, bool PURE = false>
 __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, const SegCount& base,
                                                  const SegCount& own, uint4* lrec, WalkEnd* wend,
@@ -1183,9 +1220,7 @@ __device__ __forceinline__ void quad_prefix(const WalkArgs& a, uint32_t s, uint3
         for (int j = 0; j < 4; ++j) {
             const uint32_t idx = 4 * q + j;
             if (idx < r) {
-                const uint32_t bits = 2u | 1u << 4 | (uint32_t)WSC_FK_MESSAGE << 5 | 2u << 9 | hlj[j] << 14 |
-                                      (uint32_t)WSC_FF_UNMASKED << 18 | (pl[j] ? 1u : 0u) << 27;
-                lrec[(nf + idx) * LS] = make_uint4((uint32_t)(hp[j] - seg_start), pl[j], mk[j], bits);
+                lrec[(nf + idx) * LS] = pre_record(hp[j], pl[j], mk[j], hlj[j], seg_start);
                 lrec2[(nf + idx) * LS] = make_uint4(msg + idx, ns + cnt_x, nb + bytes_x, (uint32_t)(lend_x - seg_start));
                 if (pl[j]) {
                     cnt_x += 1;
@@ -1283,17 +1318,7 @@ __device__ __forceinline__ SegCount tile_count(const WalkArgs& a, WalkLds<COMPAC
             c.frames = ps->nf;
             c.spans0 = ps->ns;
             c.bytes0 = ps->nb;
-            we.pos = ss + ps->pos;
-            we.cont = 0;
-            we.last_dend = ss + ps->pend;
-            we.frem = we.flen = 0;
-            we.fmask = we.fhdr = 0;
-            we.msg = ps->msg;
-            we.mode = 0;
-            we.status = st0.status;   // (OPEN: the pre-pass runs only then)
-            we.close_code = we.err = 0;
-            we.u8dfa = we.pdfa = 0;
-            we.replay = true;         // (nf <= cap and the segment is < 4 GiB)
+            we = pre_end(*ps, ss, st0.status);   // (nf <= cap and the segment is < 4 GiB)
         } else {
             c = walk_segment<false, COMPACT, WL>(a, s, zero, zero, L.rec + nrec * WL + lane, &we,
                                                  L.rec2 + nrec * WL + lane, cap, j, ps, sin);

@@ -684,6 +684,7 @@ int wsc_session_commit(wsc_session* s, uint32_t conn, uint64_t n) {
         f.bytes += n;
     }
     c->reserved = 0;
+    if (c->eof) maybe_eof(s, *c);   // nothing left of it to decode: Close() is due now
     return WSC_OK;
 }
 
@@ -878,6 +879,10 @@ int wsc_session_eof(wsc_session* s, uint32_t conn) {
     apply_removes(s);
     Conn* c = lookup(s, conn);
     if (!c) return WSC_E_STATE;
+    // a reservation not committed yet (reserve -> read() == 0 -> eof, commit left for later): the
+    // read brought nothing, so drop it now -- a spill region held open would keep maybe_eof waiting
+    // after the commit had shrunk it away (round-4 ADVICE)
+    if (c->reserved) (void)wsc_session_commit(s, conn, 0);
     c->eof = true;
     // a read that returned 0 may follow a reserve that placed the connection in the staging being
     // filled with nothing in it: that empty region is dropped (else it would wait for a submit that

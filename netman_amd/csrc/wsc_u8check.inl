@@ -75,9 +75,20 @@ __device__ __forceinline__ uint32_t u8_comp_verdict(const U8Args& a, uint32_t s,
         }
         j = x.next;
     }
-    if ((g.pending_end & 1u) && (a.state_out[s].cont_len || a.state_out[s].frame_rem))
-        a.state_out[s].cont_utf8 = (uint8_t)(cur > 7 ? 8u : cur);
-    if (g.pending_end & 4u) a.state_out[s].frame_utf8 = (uint8_t)(pcur > 7 ? 8u : pcur);
+    if (g.pending_end & 5u) {
+        wsc_conn_state* so = a.state_out + s;
+        if ((g.pending_end & 1u) && (so->cont_len || so->frame_rem)) so->cont_utf8 = (uint8_t)(cur > 7 ? 8u : cur);
+        if (g.pending_end & 4u) so->frame_utf8 = (uint8_t)(pcur > 7 ? 8u : pcur);
+        // a single-piece TEXT item of this segment may fail concurrently (u8_fail, another wave),
+        // and a closed connection carries no open state (round-4 ADVICE): store, full fence, then
+        // look at the segment's failure minimum -- u8_fail sets it (seq_cst) before it zeroes the
+        // state, so whichever side runs second leaves the state zero
+        __atomic_thread_fence(__ATOMIC_SEQ_CST);
+        if (__hip_atomic_load(&a.seg[s].minfail, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_AGENT) != 0xFFFFFFFFu) {
+            so->cont_utf8 = 0;
+            so->frame_utf8 = 0;
+        }
+    }
     return 0xFFFFFFFFu;
 }
 
@@ -90,7 +101,7 @@ __device__ __forceinline__ uint32_t u8_comp_verdict(const U8Args& a, uint32_t s,
 // [lo, hi) (empty: nothing to re-mask).
 __device__ __forceinline__ void u8_fail(const U8Args& a, uint32_t s, uint32_t ord, uint64_t& lo, uint64_t& hi) {
     lo = hi = 0;
-    const uint32_t old = __hip_atomic_fetch_min(&a.seg[s].minfail, ord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t old = __hip_atomic_fetch_min(&a.seg[s].minfail, ord, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_AGENT);
     if (ord >= old) return;   // an earlier frame already failed
     const uint32_t fbase = a.seg[s].fbase;
     auto frame_end = [&](uint32_t o) {
@@ -115,6 +126,7 @@ __device__ __forceinline__ void u8_fail(const U8Args& a, uint32_t s, uint32_t or
     so->frame_mask = 0;
     so->frame_hdr = 0;
     so->frame_utf8 = 0;
+    so->cont_utf8 = 0;
     lo = fend;
     hi = old == 0xFFFFFFFFu ? ~0ull : frame_end(old);
 }

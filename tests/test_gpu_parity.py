@@ -77,8 +77,10 @@ def test_fuzz_walk_geometries(codec_lib, monkeypatch, compact, mode):
     try:
         streams = [random_stream(7000 + i, n_units=int(5 + i % 40), text_p=0.5) for i in range(400)]
         _check_batch(c, streams, compact=compact)
+        assert c.walk_info()[0] == mode          # the pinned geometry really ran (round-4 ADVICE)
         streams = [random_stream(7500 + i, n_units=int(1 + i % 6)) for i in range(300)]
         _check_batch(c, streams, compact=compact)
+        assert c.walk_info()[0] == mode
     finally:
         c.close()
 

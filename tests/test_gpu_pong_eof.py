@@ -248,3 +248,31 @@ def test_eof_delivers_queued_messages_first(codec_lib, pipelined):
     sess.decode()
     assert events_of_session(sess, conns[0]) == []
     sess.close()
+
+
+@pytest.mark.parametrize("in_flight", [False, True])
+def test_eof_between_reserve_and_commit(codec_lib, in_flight):
+    """round-4 ADVICE: reserve -> read() == 0 -> wsc_session_eof -> commit(0).  With the
+    connection's earlier bytes in flight the reservation is a spill region; Close() must still
+    come, after the messages (O.run(stream, eof=True))"""
+    import ctypes as C
+    sess = K.Session(0, max_batch_bytes=1 << 20, max_segs=16, max_frames=1024)
+    a = sess.open()
+    s = synth.frame(2, b"one", mask=1) + synth.frame(1, b"two", mask=2)
+    sess.feed(a, s)
+    got = []
+    if in_flight:
+        sess.submit()
+    p, avail = C.c_void_p(), C.c_uint64()
+    assert sess.lib.wsc_session_reserve(sess.h, a, 4096, C.byref(p), C.byref(avail)) == 0 and p.value
+    sess.eof(a)
+    assert sess.lib.wsc_session_commit(sess.h, a, 0) == 0
+    if in_flight:
+        sess.complete()
+        got += events_of_session(sess, a)
+    for _ in range(4):
+        sess.decode()
+        got += events_of_session(sess, a)
+    assert got == [e.key() for e in O.run(s, cap=1 << 12, eof=True).events]
+    assert got[-1][0] == K.EV_CLOSE
+    sess.close()
