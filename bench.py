@@ -27,7 +27,8 @@ FRAMES_PER_SEG = 4
 RECORD_BYTES = 32          # sizeof(wsc_frame)
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 # (walk CUs, unmask only on the other CUs) tried for each other_configs line's pipelined column
-PIPELINE_SPLITS = [(16, 0), (32, 1), (64, 1), (80, 1), (96, 1), (112, 1), (128, 1), (128, 0)]
+# (0, 0): the walk on a high-priority stream over all CUs, the unmask on a normal one over all CUs
+PIPELINE_SPLITS = [(0, 0), (16, 0), (32, 1), (64, 1), (80, 1), (96, 1), (112, 1), (128, 1), (128, 0)]
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 
 
@@ -51,6 +52,8 @@ def parse():
                     help="split pipeline (wsc_decode_split): the header walk runs on a stream masked to this "
                          "many CUs, the unmask (+ UTF-8 check when text was deferred) on --unmask-streams streams over every CU "
                          "(0 = every stage of a batch in order on its own stream)")
+    ap.add_argument("--walk-prio", type=int, default=0,
+                    help="1: the pipelined walk on a high-priority stream over all CUs instead of --walk-cus CUs")
     ap.add_argument("--unmask-streams", type=int, default=1)
     ap.add_argument("--staged", type=int, default=1,
                     help="split pipeline staged by the host: walk, wait for it, then the unmask, so "
@@ -208,10 +211,10 @@ def main():
     # batch on the rest, so batch k+1's walk runs beside batch k's unmask and the unmasks' ramp
     # and tail overlap (tools/split_probe.py, profiles/r01_split_probe.log)
     n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
-    split = P > 1 and 0 < a.walk_cus < n_cu
+    split = P > 1 and (a.walk_prio or 0 < a.walk_cus < n_cu)
     n_dec = [1] * P   # decodes issued per in-flight buffer (the gate above did one each)
     if split:
-        walk_st = codec.stream_create(K.cu_mask(range(a.walk_cus), n_cu))
+        walk_st = codec.stream_create(priority=1) if a.walk_prio else codec.stream_create(K.cu_mask(range(a.walk_cus), n_cu))
         um = K.cu_mask(range(a.walk_cus, n_cu), n_cu) if a.unmask_rest else None
         unmask_st = [codec.stream_create(um) for _ in range(max(1, a.unmask_streams))]
 
@@ -323,7 +326,7 @@ def main():
                    "frames_per_gpu": a.frames, "frame_bytes": a.frame_bytes,
                    "segments_per_gpu": n_segs, "parallelism": f"shard{world}",
                    "batches_in_flight": P,
-                   "pipeline": (f"split: walk on a stream masked to {a.walk_cus} CUs, unmask (+ UTF-8 check when text was deferred) on "
+                   "pipeline": (f"split: walk on {'a high-priority stream over all CUs' if a.walk_prio else 'a stream masked to ' + str(a.walk_cus) + ' CUs'}, unmask (+ UTF-8 check when text was deferred) on "
                                 f"{len(unmask_st)} stream(s) over "
                                 f"{'the other ' + str(n_cu - a.walk_cus) if a.unmask_rest else 'all ' + str(n_cu)} CUs") if split
                                else "each batch in order on its own stream"},
@@ -610,7 +613,7 @@ def other_configs(torch, K, synth, only=None):
         pair = [(c, b), (c2, b2)]
         best = None
         for wcus, rest in PIPELINE_SPLITS:
-            ws = c.stream_create(K.cu_mask(range(wcus), n_cu))
+            ws = c.stream_create(priority=1) if wcus == 0 else c.stream_create(K.cu_mask(range(wcus), n_cu))
             us = c.stream_create(K.cu_mask(range(wcus, n_cu), n_cu) if rest else None)
 
             def staged(k):
@@ -637,7 +640,8 @@ def other_configs(torch, K, synth, only=None):
                      "walk_ms": round(wk, 4), "unmask_ms": round(um, 4), "unmask_gb_s": round(alg / (um * 1e-3) / 1e9, 1),
                      "pipelined_gib_s": round(cfg["payload_bytes"] / (pms * 1e-3) / 2**30, 1),
                      "pipelined_ms_per_batch": round(pms, 4),
-                     "pipelined_frac": round(alg / (pms * 1e-3) / 1e9 / HBM_PEAK_GBS, 3), "pipelined_walk_cus": wcus,
+                     "pipelined_frac": round(alg / (pms * 1e-3) / 1e9 / HBM_PEAK_GBS, 3),
+                     "pipelined_walk_cus": wcus if wcus else "all, high-priority stream",
                      "pipelined_unmask_cus": "the other CUs" if rest else "all",
                      "frames": int(cfg["n_frames"]), "payload_bytes": int(cfg["payload_bytes"]), "alg_bytes": alg,
                      "device_errors": not ok}
@@ -791,7 +795,7 @@ def host_inclusive(codec, cfg, K):
         lib.wsc_host_free(p)
 
 
-def host_inclusive_pipelined(torch, codecs, streams, cfg, K, chunks=16, iters=3):
+def host_inclusive_pipelined(torch, codecs, streams, cfg, K, chunks=16, iters=3, dir_streams=False):
     """The same batch from pinned host memory, cut at segment boundaries into `chunks` pieces that
     alternate between the in-flight contexts/streams: H2D of piece i+1 overlaps the decode and
     the D2H of piece i (PCIe is full duplex).  Output: unmasked wire + frame records in pinned
@@ -828,15 +832,40 @@ def host_inclusive_pipelined(torch, codecs, streams, cfg, K, chunks=16, iters=3)
     for i, (a0, a1, k, _) in enumerate(pieces):
         rec_n[i] = int(np.count_nonzero((cfg["payload_off"] >= a0) & (cfg["payload_off"] < a1)))
 
+    # one stream per PCIe direction (dir_streams): H2D of piece i+1 queued on its own stream can run
+    # beside piece i's D2H on another, instead of queueing behind it on the piece's stream; events
+    # order buffer reuse (H2D into buffer j waits for the D2H out of it) and each decode
+    h2d, d2h = (torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)) if dir_streams else (None, None)
+    ev_free = [None] * P
+
     def one_pass():
         for i, (a0, a1, k, rel) in enumerate(pieces):
             j = i % P
             st, b = streams[j], bufs[j]
+            batch = codecs[j].make_batch(b["wire"], b["seg_off"][: k + 1], None, b["st"], b["so"], b["fr"],
+                                         b["sm"], n_bytes=a1 - a0)
+            if dir_streams:
+                with torch.cuda.stream(h2d):
+                    if ev_free[j] is not None:
+                        h2d.wait_event(ev_free[j])
+                    b["wire"][: a1 - a0].copy_(wire_h[a0:a1], non_blocking=True)
+                    b["seg_off"][: k + 1].copy_(rel, non_blocking=True)
+                    ev_in = torch.cuda.Event()
+                    ev_in.record(h2d)
+                st.wait_event(ev_in)
+                codecs[j].decode(batch, st.cuda_stream)
+                ev_dec = torch.cuda.Event()
+                ev_dec.record(st)
+                with torch.cuda.stream(d2h):
+                    d2h.wait_event(ev_dec)
+                    out_h[a0:a1].copy_(b["wire"][: a1 - a0], non_blocking=True)
+                    rec_h[i][: rec_n[i] * 32].copy_(b["fr"][: rec_n[i] * 32], non_blocking=True)
+                    ev_free[j] = torch.cuda.Event()
+                    ev_free[j].record(d2h)
+                continue
             with torch.cuda.stream(st):
                 b["wire"][: a1 - a0].copy_(wire_h[a0:a1], non_blocking=True)
                 b["seg_off"][: k + 1].copy_(rel, non_blocking=True)
-                batch = codecs[j].make_batch(b["wire"], b["seg_off"][: k + 1], None, b["st"], b["so"], b["fr"],
-                                             b["sm"], n_bytes=a1 - a0)
                 codecs[j].decode(batch, st.cuda_stream)
                 out_h[a0:a1].copy_(b["wire"][: a1 - a0], non_blocking=True)
                 rec_h[i][: rec_n[i] * 32].copy_(b["fr"][: rec_n[i] * 32], non_blocking=True)
@@ -852,7 +881,8 @@ def host_inclusive_pipelined(torch, codecs, streams, cfg, K, chunks=16, iters=3)
     el = (time.perf_counter() - t0) / iters
     return {"gib_s": round(cfg["payload_bytes"] / el / 2**30, 2), "ms_per_batch": round(el * 1e3, 2),
             "chunks": len(pieces), "streams": P, "parity_ok": ok,
-            "note": "pinned host wire -> H2D -> decode -> D2H wire+records, pieces alternating over streams"}
+            "note": "pinned host wire -> H2D -> decode -> D2H wire+records, pieces alternating over streams"
+                    + (" (one stream per copy direction, events between them)" if dir_streams else " (each piece's copies on its decode stream)")}
 
 
 def host_inclusive_zero_copy(torch, codecs, streams, cfg, K, chunks=16, iters=3):

@@ -267,6 +267,11 @@ int wsc_walk_wait(wsc_ctx* ctx);
 /* A non-blocking stream on the context's device, restricted to the CUs whose bits are set in
  * cu_mask[0..mask_words) (hipExtStreamCreateWithCUMask); cu_mask NULL = all CUs.             */
 int wsc_stream_create(wsc_ctx* ctx, const uint32_t* cu_mask, uint32_t mask_words, void** out);
+/* Same, with a queue priority: priority > 0 = the device's greatest stream priority, < 0 = its
+ * least, 0 = wsc_stream_create.  A prioritised stream spans all CUs (cu_mask must be NULL): the
+ * staged pipeline's walk stream, beside unmasks on a normal stream.  (The walk's waves also raise
+ * their SIMD issue priority, s_setprio, whatever stream they run on.)                          */
+int wsc_stream_create_ex(wsc_ctx* ctx, const uint32_t* cu_mask, uint32_t mask_words, int priority, void** out);
 int wsc_stream_destroy(wsc_ctx* ctx, void* stream);
 
 /* Host-buffer path: copies wire/offsets/state to the device through the context's pinned

@@ -115,6 +115,7 @@ SIGNATURES = {
     "wsc_decode_finish": (_I, [_P, C.POINTER(WscBatch), _P]),
     "wsc_walk_wait": (_I, [_P]),
     "wsc_stream_create": (_I, [_P, _P, _U32, C.POINTER(_P)]),
+    "wsc_stream_create_ex": (_I, [_P, _P, _U32, _I, C.POINTER(_P)]),
     "wsc_stream_destroy": (_I, [_P, _P]),
     "wsc_decode_host": (_I, [_P, _P, _U64, _P, _U32, _U32, _P, _P, _P, _P, _U32, _P, _P, _P]),
     "wsc_encode": (_I, [_P, _P, _U32, _P, _U64, _P, _U64, _P, _P]),
@@ -311,10 +312,13 @@ class Codec:
     def walk_wait(self):
         _check(self.lib.wsc_walk_wait(self.h), "wsc_walk_wait")
 
-    def stream_create(self, cu_mask=None) -> int:
-        """a raw hipStream_t (int), restricted to the CUs set in cu_mask (list of u32 words)"""
+    def stream_create(self, cu_mask=None, priority: int = 0) -> int:
+        """a raw hipStream_t (int), restricted to the CUs set in cu_mask (list of u32 words);
+        priority > 0: the device's greatest queue priority over all CUs (wsc_stream_create_ex)"""
         out = C.c_void_p()
-        if cu_mask is None:
+        if priority:
+            _check(self.lib.wsc_stream_create_ex(self.h, None, 0, int(priority), C.byref(out)), "wsc_stream_create_ex")
+        elif cu_mask is None:
             _check(self.lib.wsc_stream_create(self.h, None, 0, C.byref(out)), "wsc_stream_create")
         else:
             arr = (C.c_uint32 * len(cu_mask))(*cu_mask)

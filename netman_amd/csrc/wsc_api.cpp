@@ -20,7 +20,7 @@ template <bool COMPACT, uint32_t KR, uint32_t NT> __global__ void k_walk_tiled(W
 template <bool COMPACT> __global__ void k_walk_count(WalkArgs);
 __global__ void k_walk_scan(WalkArgs, uint32_t);
 template <bool COMPACT> __global__ void k_walk_emit(WalkArgs);
-template <uint32_t NCH> __global__ void k_u8_check(U8Args);
+template <uint32_t NCH, uint32_t WPB> __global__ void k_u8_check(U8Args);
 template <bool COMPACT, int P, int NT, int MINW, bool U8>
 __global__ void k_unmask(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*,
                          const wsc_summary*, uint32_t*, uint32_t, uint32_t*, uint32_t*, uint32_t, U8Win);
@@ -102,9 +102,11 @@ struct wsc_ctx {
                                         // counter) was not: the next walk zeroes its counter itself
     uint32_t u8_inline_max = 256;
     uint32_t u8_grid = 0;               // WSC_U8_GRID: k_u8_check workgroups (A/B experiments; 0 = 5 per CU)
+    uint32_t u8_wpb = 4;                // WSC_U8_WPB: k_u8_check waves per workgroup (4, or 16 = 1024-thread workgroups)
     bool walk_tiled = true;             // WSC_WALK_TILED=0: the three-launch walk for mode 3 (A/B)
     int hdr_nt = -1;                    // WSC_HDR_NT: the walk's header loads non-temporal: 0 never, 1 always, default COMPACT batches
     bool walk_hw_order = false;         // WSC_WALK_HW_ORDER=1: walk blocks ordered by workgroup index, not a ticket
+    bool walk_prio = true;              // WSC_WALK_PRIO=0: the walk's waves keep the default issue priority
     bool quad_pre = true;               // WSC_QUAD_PRE=0: the fused walk without its quad pre-pass (A/B)
     uint32_t xcd_run = 8;               // WSC_XCD_RUN: unmask blocks per XCD run (1 = the hardware deal; one run
                                         // per XCD over the whole grid measured slower: headline 0.347 -> 0.359 ms)
@@ -331,11 +333,13 @@ int wsc_create(int device, const wsc_config* cfg_in, wsc_ctx** out) {
     if (const char* e = std::getenv("WSC_UNMASK_BUF"); e && *e) c->unmask_buf = std::atoi(e);
     if (const char* e = std::getenv("WSC_U8_CHAINS"); e && *e) c->u8_chains = std::atoi(e);
     if (const char* e = std::getenv("WSC_U8_GRID"); e && *e) c->u8_grid = (uint32_t)std::strtoul(e, nullptr, 10);
+    if (const char* e = std::getenv("WSC_U8_WPB"); e && *e) c->u8_wpb = std::atoi(e) == 16 ? 16u : 4u;
     if (const char* e = std::getenv("WSC_AB_NO_U8"); e && e[0] == '1') c->ab_no_u8 = true;
     if (const char* e = std::getenv("WSC_WALK_TILED"); e && e[0] == '0') c->walk_tiled = false;
     if (const char* e = std::getenv("WSC_QUAD_PRE"); e && e[0] == '0') c->quad_pre = false;
     if (const char* e = std::getenv("WSC_WALK_HW_ORDER"); e && *e) c->walk_hw_order = e[0] == '1';
     if (const char* e = std::getenv("WSC_HDR_NT"); e && *e) c->hdr_nt = e[0] == '1' ? 1 : 0;
+    if (const char* e = std::getenv("WSC_WALK_PRIO"); e && *e) c->walk_prio = e[0] == '1';
     if (const char* e = std::getenv("WSC_XCD_RUN"); e && *e) c->xcd_run = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("WSC_ENC_XCD_RUN"); e && *e) c->enc_xcd_run = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("WSC_WALK_MODE"); e && *e) {   // pin a walk geometry (tests, A/B): 16, 32, 64, 65, 66, 256, 257 or 3
@@ -466,6 +470,7 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     wa.stride_hint = c->stride_hint;
     wa.hw_order = c->walk_hw_order ? 1u : 0u;
     wa.hdr_nt = (c->hdr_nt < 0 ? compact : c->hdr_nt != 0) ? 1u : 0u;
+    wa.prio = c->walk_prio ? 1u : 0u;
 
     // walk geometry: the fused walk with blocks that fill the CUs once (64 lanes for up to 64
     // segments per CU, else 256), or -- for more segments than the chip holds lanes at once -- the
@@ -623,10 +628,11 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
         ua.fin_seq = c->fin_seq + 1;
         const dim3 ug(c->u8_grid ? c->u8_grid : (uint32_t)c->n_cu * 4);   // resident: 4 waves/SIMD (128 VGPRs;
         // 3 waves/SIMD without the large path's spills measured slower: 64 KiB TEXT check 79 -> 95 us)
-        if (c->u8_chains == 1) hipLaunchKernelGGL(k_u8_check<1>, ug, dim3(256), 0, st, ua);
-        else if (c->u8_chains == 4) hipLaunchKernelGGL(k_u8_check<4>, ug, dim3(256), 0, st, ua);
-        else if (c->u8_chains == 8) hipLaunchKernelGGL(k_u8_check<8>, ug, dim3(256), 0, st, ua);
-        else hipLaunchKernelGGL(k_u8_check<2>, ug, dim3(256), 0, st, ua);
+        if (c->u8_wpb == 16 && c->u8_chains == 4) hipLaunchKernelGGL((k_u8_check<4, 16>), dim3((ug.x + 3) / 4), dim3(1024), 0, st, ua);
+        else if (c->u8_chains == 1) hipLaunchKernelGGL((k_u8_check<1, 4>), ug, dim3(256), 0, st, ua);
+        else if (c->u8_chains == 4) hipLaunchKernelGGL((k_u8_check<4, 4>), ug, dim3(256), 0, st, ua);
+        else if (c->u8_chains == 8) hipLaunchKernelGGL((k_u8_check<8, 4>), ug, dim3(256), 0, st, ua);
+        else hipLaunchKernelGGL((k_u8_check<2, 4>), ug, dim3(256), 0, st, ua);
         HIP_TRY(hipGetLastError());
     }
     rec(3);
@@ -691,6 +697,20 @@ int wsc_stream_create(wsc_ctx* c, const uint32_t* cu_mask, uint32_t mask_words, 
     } else {
         HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     }
+    *out = s;
+    return WSC_OK;
+}
+
+int wsc_stream_create_ex(wsc_ctx* c, const uint32_t* cu_mask, uint32_t mask_words, int priority, void** out) {
+    if (!c || !out) return fail(WSC_E_INVAL, "NULL argument");
+    if (priority == 0) return wsc_stream_create(c, cu_mask, mask_words, out);
+    if (cu_mask && mask_words) return fail(WSC_E_INVAL, "a CU-masked stream has the default priority");
+    *out = nullptr;
+    HIP_TRY(hipSetDevice(c->device));
+    int least = 0, greatest = 0;
+    HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    hipStream_t s = nullptr;
+    HIP_TRY(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, priority > 0 ? greatest : least));
     *out = s;
     return WSC_OK;
 }

@@ -1625,6 +1625,7 @@ __global__ __launch_bounds__(NT) void k_walk_fused(WalkArgs a) {
     __shared__ uint32_t sh_bid;
     __shared__ WalkLds<COMPACT, KR, NT, G, WL> L;
     const uint32_t lane = threadIdx.x, wl = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (a.prio) __builtin_amdgcn_s_setprio(3);   // a latency-bound chain beside streaming unmask waves
     if (lane == 0) sh_bid = walk_block_id(a);
     __syncthreads();
     const uint32_t bid = sh_bid;
@@ -1707,6 +1708,7 @@ __global__ __launch_bounds__(NT) void k_walk_tiled(WalkArgs a, uint32_t per_bloc
     __shared__ uint32_t sh_bid;
     __shared__ WalkLds<COMPACT, KR, NT, 1> L;
     const uint32_t lane = threadIdx.x, wl = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (a.prio) __builtin_amdgcn_s_setprio(3);   // a latency-bound chain beside streaming unmask waves
     if (lane == 0) sh_bid = walk_block_id(a);
     __syncthreads();
     const uint32_t bid = sh_bid;
@@ -1803,14 +1805,14 @@ __global__ __launch_bounds__(NT) void k_walk_tiled(WalkArgs a, uint32_t per_bloc
 // 4 waves per SIMD (128 VGPRs).  Launched after the unmask on the same stream.  (Run instead as
 // extra workgroups of the unmask launch, waiting on an unmask-done counter, it measured no faster
 // on binary batches and far slower on text: profiles/r04_u8_merge_ab.log, DESIGN.md "Round 4".)
-template <uint32_t NCH>
+template <uint32_t NCH, uint32_t WPB>
 #ifndef WSC_CHECK_WPE   // waves per SIMD k_u8_check is built for (A/B: tools/build_variant.sh)
 #define WSC_CHECK_WPE 4
 #endif
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WSC_CHECK_WPE))) void k_u8_check(U8Args a) {
+__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(WSC_CHECK_WPE))) void k_u8_check(U8Args a) {
     __shared__ U8Lds T;
-    __shared__ uint4 stage[4][U8_STAGE];
-    u8_check_run<NCH>(a, T, stage, blockIdx.x, gridDim.x);
+    __shared__ uint4 stage[WPB][U8_STAGE];
+    u8_check_run<NCH, WPB>(a, T, stage, blockIdx.x, gridDim.x);
     // staged pipeline: the decode's last kernel tells the host its scratch is free
     if (a.fin_host) {
         __syncthreads();
@@ -1818,10 +1820,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WSC_CHECK_W
     }
 }
 
-template __global__ void k_u8_check<1>(U8Args);
-template __global__ void k_u8_check<2>(U8Args);
-template __global__ void k_u8_check<4>(U8Args);
-template __global__ void k_u8_check<8>(U8Args);
+template __global__ void k_u8_check<1, 4>(U8Args);
+template __global__ void k_u8_check<2, 4>(U8Args);
+template __global__ void k_u8_check<4, 4>(U8Args);
+template __global__ void k_u8_check<8, 4>(U8Args);
+template __global__ void k_u8_check<4, 16>(U8Args);
 
 // explicit instantiations used by the host code: 16 frame records per lane, one segment per
 // lane, blocks of 64 or 256 lanes; batches of more segments use the three-launch walk below

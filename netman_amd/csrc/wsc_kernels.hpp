@@ -123,6 +123,7 @@ struct WalkArgs {
     uint32_t* stride_hint;       // quad pre-pass: the stride the last decode ended with (first speculation)
     uint32_t hw_order;           // look-back order = hardware workgroup index (no ticket atomic), walk_block_id
     uint32_t hdr_nt;             // non-temporal header loads (hdr_load): COMPACT batches by default
+    uint32_t prio;               // walk waves raise their issue priority (s_setprio) over the unmask waves they share SIMDs with
 };
 
 // k_u8_check runs AFTER the unmask: the unmask has already folded every text window that lies

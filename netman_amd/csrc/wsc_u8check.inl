@@ -166,7 +166,9 @@ __device__ __forceinline__ void u8_remask(const U8Args& a, uint32_t seg, uint64_
 #ifndef WSC_CHECK_PREFETCH
 #define WSC_CHECK_PREFETCH 0
 #endif
-template <uint32_t NCH>
+// WPB: waves per workgroup (4: 256-thread workgroups; 16: one 1024-thread workgroup per CU, a
+// quarter of the workgroups to dispatch for the same waves)
+template <uint32_t NCH, uint32_t WPB = 4>
 __device__ __forceinline__ void u8_check_run(const U8Args& a, U8Lds& T, uint4 (*stage)[U8_STAGE], uint32_t bid,
                                              uint32_t nblk) {
     // (items past the capacity were dropped by the walk: only a batch whose records overflowed
@@ -202,11 +204,11 @@ __device__ __forceinline__ void u8_check_run(const U8Args& a, U8Lds& T, uint4 (*
         if (trig && !ovf) ord = u8_comp_verdict(a, seg, a.seg[seg]);
         fail_settle(ord != 0xFFFFFFFFu, seg, ord);
     };
-    if (bid * 4 < n_items) {   // (nothing deferred, or fewer units than waves: only the signal)
-    u8_tables_init(T, threadIdx.x);
+    if (bid * WPB < n_items) {   // (nothing deferred, or fewer units than waves: only the signal)
+    if (threadIdx.x < 256) u8_tables_init(T, threadIdx.x);
     __syncthreads();
-    const uint32_t gw = __builtin_amdgcn_readfirstlane(bid * 4 + (threadIdx.x >> 6));
-    const uint32_t nw = nblk * 4;
+    const uint32_t gw = __builtin_amdgcn_readfirstlane(bid * WPB + (threadIdx.x >> 6));
+    const uint32_t nw = nblk * WPB;
     // Global loads stay coalesced (piece k of a step: 16 B per lane at base_k + 16 * lane, 1 KiB
     // per instruction); a per-wave LDS stage turns them into one contiguous 64-byte chunk per lane.
     // Strided 16-byte global loads at a 64-byte lane stride measured slower.
