@@ -716,7 +716,9 @@ def echo_configs(with_cpu=True):
     """configs[0]: examples/websocket echo on loopback, rebuilt around a pluggable decoder
     (tools/echo_harness.hpp; the Go reference server cannot run here).  gpu = tools/ws_echo
     (libwscodec wsc_session: recv straight into pinned staging, round r+1 submitted to the device
-    while round r is echoed); gpu_sync = the same with one synchronous decode per round; cpu = oracle/_build/ws_echo_cpu,
+    while round r is echoed); gpu_sync = the same with one synchronous decode per round; gpu_blocking_wait =
+    gpu with the session's completion sleeping on a blocking-sync event (WSC_SESSION_BLOCKING_WAIT)
+    instead of spinning; cpu = oracle/_build/ws_echo_cpu,
     the reference's frame-at-a-time decode ported to C++ (cpu_baseline leg, kind "port").  Each
     run is a separate process; msgs/s and GiB/s of echoed payload, every byte checked.  P pollers
     (netman runs NumCPU, eventloop/event.go:33-37): connection i on poller i % P, each poller its
@@ -729,7 +731,7 @@ def echo_configs(with_cpu=True):
     for P in (1, 4, 8):
         runs.append((f"64 conns x 200 x 64 KiB, {P} poller(s)", ["--conns", "64", "--frames", "200", "--size", "65536",
                                                                   "--client-threads", "4", "--pollers", str(P)],
-                     ["gpu", "cpu_port"]))
+                     ["gpu", "gpu_blocking_wait", "cpu_port"]))
         runs.append((f"64 conns x 2000 x 1 KiB, {P} poller(s)", ["--conns", "64", "--frames", "2000", "--size", "1024",
                                                                  "--client-threads", "4", "--pollers", str(P)],
                      ["gpu", "gpu_sync", "cpu_port"]))
@@ -737,7 +739,8 @@ def echo_configs(with_cpu=True):
     runs.append(("64 conns x 200 x 64 KiB, 4 pollers, clients shutdown(SHUT_WR) after the last frame",
                  ["--conns", "64", "--frames", "200", "--size", "65536", "--client-threads", "4", "--pollers", "4",
                   "--shutdown"], ["gpu", "cpu_port"]))
-    bins = {"gpu": (gpu, []), "gpu_sync": (gpu, ["--sync"]), "cpu_port": (cpu, [])}
+    bins = {"gpu": (gpu, []), "gpu_sync": (gpu, ["--sync"]), "gpu_blocking_wait": (gpu, ["--blocking-wait"]),
+            "cpu_port": (cpu, [])}
 
     def one(exe, args):
         try:

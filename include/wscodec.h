@@ -114,6 +114,12 @@ extern "C" {
                                [data payloads (continuation chains contiguous)][control payloads]; a
                                frame's payload is at frame_dst[i]                                  */
 
+/* session flags (wsc_session_create; batch flags above apply too) */
+#define WSC_SESSION_BLOCKING_WAIT 0x100   /* complete() sleeps on a blocking-sync event instead of
+                                             spinning in hipStreamSynchronize: the poller's core is
+                                             free for recv/send while the device works (many pollers
+                                             on few cores)                                          */
+
 /* Decoder state carried between batches for one connection (subset of websocket.go:38-56).   */
 typedef struct wsc_conn_state {
     uint64_t cont_len;     /* continueBuffer length (bytes of an unfinished fragmented message)  */

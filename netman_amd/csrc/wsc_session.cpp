@@ -98,6 +98,7 @@ struct Conn {
 struct Stage {                    // one staging set: pinned host buffers, device buffers, context
     wsc_ctx* ctx = nullptr;
     hipStream_t stream = nullptr;
+    hipEvent_t ev = nullptr;      // WSC_SESSION_BLOCKING_WAIT: a blocking-sync event complete() sleeps on
     uint8_t* h_wire = nullptr;    // masked bytes as read (input)
     uint8_t* h_res = nullptr;     // results: unmasked wire (in place) or the arena (COMPACT)
     uint64_t* h_seg_off = nullptr;
@@ -496,8 +497,19 @@ int launch_stage(wsc_session* s, Stage& g) {
     HT(hipMemcpyAsync(g.h_summary, g.d_summary, sizeof(wsc_summary), hipMemcpyDeviceToHost, st));
     HT(hipMemcpyAsync(g.h_state_out, g.d_state_out, n * sizeof(wsc_conn_state), hipMemcpyDeviceToHost, st));
     HT(hipMemcpyAsync(g.h_seg_out, g.d_seg_out, n * sizeof(wsc_seg_result), hipMemcpyDeviceToHost, st));
+    // in place the unmasked wire is the batch's whole input range, known now: its D2H goes out with
+    // the launch instead of after complete()'s first wait, so it overlaps the host's work on the
+    // previous round (views into h_res of this set were materialised by the complete() before)
+    if (!compact) HT(hipMemcpyAsync(g.h_res, g.d_wire, g.bytes, hipMemcpyDeviceToHost, st));
 #undef HT
     return WSC_OK;
+}
+
+// wait for everything enqueued on the stage's stream so far
+hipError_t stage_wait(const wsc_session* s, Stage& g) {
+    if (!(s->flags & WSC_SESSION_BLOCKING_WAIT)) return hipStreamSynchronize(g.stream);
+    const hipError_t e = hipEventRecord(g.ev, g.stream);
+    return e != hipSuccess ? e : hipEventSynchronize(g.ev);
 }
 
 void reset_stage(Stage& g) {
@@ -523,7 +535,7 @@ int wsc_session_create(int device, const wsc_config* cfg, uint32_t flags, wsc_se
     wsc_config& g = s->cfg;
     if (g.max_frames < 2 || g.max_segs < 2 || g.max_batch_bytes < 64) { delete s; return WSC_E_INVAL; }
     // (no clamp of max_frame_len to the batch: payloads stream across batches)
-    s->flags = flags & WSC_F_COMPACT;
+    s->flags = flags & (WSC_F_COMPACT | WSC_SESSION_BLOCKING_WAIT);
     s->device = device;
     int rc = WSC_OK;
     for (Stage& t : s->st) {
@@ -534,6 +546,11 @@ int wsc_session_create(int device, const wsc_config* cfg, uint32_t flags, wsc_se
             rc = hip_fail("hipStreamCreateWithFlags", e);
             break;
         }
+        if (s->flags & WSC_SESSION_BLOCKING_WAIT)
+            if (const hipError_t e = hipEventCreateWithFlags(&t.ev, hipEventBlockingSync | hipEventDisableTiming); e != hipSuccess) {
+                rc = hip_fail("hipEventCreateWithFlags", e);
+                break;
+            }
         auto H = [&](uint64_t bytes) -> void* {
             void* p = nullptr;
             if (rc == WSC_OK) rc = wsc_host_alloc(bytes, &p);
@@ -587,6 +604,7 @@ int wsc_session_destroy(wsc_session* s) {
             for (void* p : ds)
                 if (p) wsc_dev_free(t.ctx, p);
         }
+        if (t.ev) (void)hipEventDestroy(t.ev);
         if (t.stream) (void)hipStreamDestroy(t.stream);
         if (t.ctx) wsc_destroy(t.ctx);
     }
@@ -775,7 +793,7 @@ int wsc_session_complete(wsc_session* s) {
     const double t0 = s->timing ? now_s() : 0;
     int rc = g.launch_rc;
     if (rc == WSC_OK)
-        if (const hipError_t e = hipStreamSynchronize(g.stream); e != hipSuccess) rc = hip_fail("hipStreamSynchronize", e);
+        if (const hipError_t e = stage_wait(s, g); e != hipSuccess) rc = hip_fail("hipStreamSynchronize", e);
     if (rc == WSC_OK && (g.h_summary->overflow & 2u))
         rc = wsc::set_last_error(WSC_E_INTERNAL, "wsc_session: device look-back timeout: batch results are invalid");
     const uint32_t n = (uint32_t)g.seg_conn.size();
@@ -797,10 +815,8 @@ int wsc_session_complete(wsc_session* s) {
         if (compact) {
             D2H(g.h_res, g.d_arena, g.h_summary->data_bytes + g.h_summary->ctrl_bytes, "hipMemcpyAsync arena");
             D2H(g.h_frame_dst, g.d_frame_dst, (uint64_t)nf * sizeof(uint64_t), "hipMemcpyAsync frame_dst");
-        } else {
-            D2H(g.h_res, g.d_wire, g.bytes, "hipMemcpyAsync wire");
-        }
-        if (e == hipSuccess && (e = hipStreamSynchronize(st)) != hipSuccess) what = "hipStreamSynchronize";
+        }   // (in place the wire came back with the launch: launch_stage)
+        if (e == hipSuccess && (e = stage_wait(s, g)) != hipSuccess) what = "hipStreamSynchronize";
         if (e != hipSuccess) rc = hip_fail(what, e);
     }
     const double t1 = s->timing ? now_s() : 0;

@@ -99,7 +99,8 @@ void phase(uint64_t batch_bytes, uint32_t max_frames, int mode, size_t n_conns, 
     cfg.max_segs = 64;
     cfg.max_frames = max_frames;
     wsc_session* s = nullptr;
-    CHECK(wsc_session_create(0, &cfg, 0, &s) == WSC_OK);
+    // (mode 2 with the blocking-wait completion: same results)
+    CHECK(wsc_session_create(0, &cfg, mode == 2 ? WSC_SESSION_BLOCKING_WAIT : 0u, &s) == WSC_OK);
     std::vector<Conn> cs;
     for (size_t i = 0; i < n_conns; ++i) {
         cs.push_back(make_conn(n_msgs, max_len));

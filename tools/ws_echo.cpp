@@ -3,7 +3,7 @@
 // pass on the MI355X.  Harness: tools/echo_harness.hpp.  The CPU baseline twin is
 // oracle/ws_echo_cpu.cpp.  Prints one JSON line.
 //   ws_echo [--pollers P] [--devices G] [--conns C] [--frames N] [--size BYTES] [--client-threads T]
-//           [--sync] [--shutdown]
+//           [--sync] [--shutdown] [--blocking-wait]
 // --pollers P: P poller threads, each with its own wsc_session (netman runs NumCPU pollers,
 // eventloop/event.go:33-37); connection i belongs to poller i % P.
 // --devices G: poller p's session lives on device p % G (one host thread, stream and
@@ -18,14 +18,14 @@ namespace {
 struct GpuDecoder : echo::Decoder {
     wsc_session* s = nullptr;
     wsc_event ev{};
-    GpuDecoder(int device, int conns, bool pipelined) : pipe(pipelined) {
+    GpuDecoder(int device, int conns, bool pipelined, uint32_t flags) : pipe(pipelined) {
         wsc_config cfg;
         wsc_config_default(&cfg);
         // one device batch per poller round: its connections' 4 MiB reads (+ a margin)
         cfg.max_batch_bytes = (uint64_t)(conns < 4 ? 4 : conns) * (5ull << 20);
         cfg.max_segs = (uint32_t)conns + 16;
         cfg.max_frames = 1u << 18;
-        if (wsc_session_create(device, &cfg, 0, &s) != WSC_OK) {
+        if (wsc_session_create(device, &cfg, flags, &s) != WSC_OK) {
             fprintf(stderr, "wsc_session_create: %s\n", wsc_last_error());
             exit(2);
         }
@@ -83,6 +83,10 @@ int main(int argc, char** argv) {
     echo::parse_args(argc, argv, conns, frames, size, threads, pollers);
     const bool pipe = !echo::has_flag(argc, argv, "--sync");   // --sync: one synchronous decode per round
     const bool shut = echo::has_flag(argc, argv, "--shutdown");
+    // --blocking-wait: the session sleeps on a blocking-sync event while the device works instead
+    // of spinning in hipStreamSynchronize (WSC_SESSION_BLOCKING_WAIT): P pollers leave their cores
+    // to the socket work
+    const uint32_t sflags = echo::has_flag(argc, argv, "--blocking-wait") ? WSC_SESSION_BLOCKING_WAIT : 0u;
     int devices = 1;
     for (int i = 1; i + 1 < argc; ++i)
         if (std::string(argv[i]) == "--devices") devices = atoi(argv[i + 1]);
@@ -95,8 +99,8 @@ int main(int argc, char** argv) {
         return 0;
     }
     const echo::Result r = echo::run(
-        [pipe, device_of](int poller, int n) {
-            return std::unique_ptr<echo::Decoder>(new GpuDecoder(device_of(poller), n, pipe));
+        [pipe, device_of, sflags](int poller, int n) {
+            return std::unique_ptr<echo::Decoder>(new GpuDecoder(device_of(poller), n, pipe, sflags));
         },
         pollers, conns, frames, size, threads, 60, shut);
     echo::print_json(pipe ? "gpu: libwscodec wsc_session per poller, recv into pinned staging, submit r+1 / echo r / complete"
