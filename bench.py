@@ -27,8 +27,11 @@ FRAMES_PER_SEG = 4
 RECORD_BYTES = 32          # sizeof(wsc_frame)
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 # (walk CUs, unmask only on the other CUs) tried for each other_configs line's pipelined column
-# (0, 0): the walk on a high-priority stream over all CUs, the unmask on a normal one over all CUs
-PIPELINE_SPLITS = [(0, 0), (16, 0), (32, 1), (64, 1), (80, 1), (96, 1), (112, 1), (128, 1), (128, 0)]
+# (0, 0): the walk on a high-priority stream over all CUs, the unmask on a normal one over all CUs;
+# (-1, 0): serial -- both contexts' walks and unmasks in order on one stream, for configs whose
+# latency-bound walk loses more beside an unmask than it saves (configs[1], [3]: the walk then
+# slows past the unmask it hides behind, profiles/r05/ab1_*.log)
+PIPELINE_SPLITS = [(-1, 0), (0, 0), (16, 0), (32, 1), (64, 1), (80, 1), (96, 1), (112, 1), (128, 1), (128, 0)]
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 
 
@@ -345,7 +348,7 @@ def main():
         out["configs3_dealt"] = config3_dealt(a, torch, dist, K, synth, world, rank, dev, cdev)
     if solo and not a.no_host_inclusive:
         out["host_inclusive"] = host_inclusive(codec, cfg, K)
-        out["host_inclusive_pipelined"] = host_inclusive_pipelined(torch, codecs, streams, cfg, K)
+        out["host_inclusive_pipelined"] = host_inclusive_pipelined(torch, codecs, streams, cfg, K, dir_streams=True)
         out["host_inclusive_zero_copy"] = host_inclusive_zero_copy(torch, codecs, streams, cfg, K)
     for c in codecs:
         c.close()
@@ -507,7 +510,7 @@ def other_configs(torch, K, synth, only=None):
     `walk_ms` / `unmask_ms`: per-kernel device time (wsc_profile hipEvents, median of 10);
     `pipelined_*`: two batches in flight through the staged split pipeline the headline runs
     (walk on a CU-masked stream, the host waits for it, then the unmask), wall time of 60 steps
-    after 20 warm-up steps, best of the PIPELINE_SPLITS CU partitions (reported).  `frac`: the
+    after 20 warm-up steps, best of the PIPELINE_SPLITS CU partitions and the serial order (reported).  `frac`: the
     decode's algorithmic bytes (2 x payload + header + 32 B record per frame) per second over
     the 8 TB/s HBM peak."""
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -613,12 +616,18 @@ def other_configs(torch, K, synth, only=None):
         pair = [(c, b), (c2, b2)]
         best = None
         for wcus, rest in PIPELINE_SPLITS:
-            ws = c.stream_create(priority=1) if wcus == 0 else c.stream_create(K.cu_mask(range(wcus), n_cu))
-            us = c.stream_create(K.cu_mask(range(wcus, n_cu), n_cu) if rest else None)
+            if wcus < 0:
+                ws = us = c.stream_create(None)
+            else:
+                ws = c.stream_create(priority=1) if wcus == 0 else c.stream_create(K.cu_mask(range(wcus), n_cu))
+                us = c.stream_create(K.cu_mask(range(wcus, n_cu), n_cu) if rest else None)
 
             def staged(k):
                 for i in range(k):
                     cx, bx = pair[i % 2]
+                    if wcus < 0:
+                        cx.decode(bx, us)
+                        continue
                     cx.decode_walk(bx, ws)
                     cx.walk_wait()
                     cx.decode_finish(bx, us)
@@ -630,7 +639,8 @@ def other_configs(torch, K, synth, only=None):
             torch.cuda.synchronize()
             pms = (time.perf_counter() - t0) / 60 * 1e3
             c.stream_destroy(ws)
-            c.stream_destroy(us)
+            if us != ws:
+                c.stream_destroy(us)
             if best is None or pms < best[0]:
                 best = (pms, wcus, rest)
         pms, wcus, rest = best
@@ -641,7 +651,8 @@ def other_configs(torch, K, synth, only=None):
                      "pipelined_gib_s": round(cfg["payload_bytes"] / (pms * 1e-3) / 2**30, 1),
                      "pipelined_ms_per_batch": round(pms, 4),
                      "pipelined_frac": round(alg / (pms * 1e-3) / 1e9 / HBM_PEAK_GBS, 3),
-                     "pipelined_walk_cus": wcus if wcus else "all, high-priority stream",
+                     "pipelined_walk_cus": wcus if wcus > 0 else ("all, high-priority stream" if wcus == 0 else
+                                                                  "serial: walks and unmasks in order on one stream"),
                      "pipelined_unmask_cus": "the other CUs" if rest else "all",
                      "frames": int(cfg["n_frames"]), "payload_bytes": int(cfg["payload_bytes"]), "alg_bytes": alg,
                      "device_errors": not ok}

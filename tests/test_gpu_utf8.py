@@ -210,3 +210,49 @@ def test_rejected_geometry_leaves_utf8_counters_consistent(codec_lib, monkeypatc
                     c.decode_host(wire, off)
     finally:
         c.close()
+
+
+def _edge_batch(rng, bad, brng=None):
+    """TEXT frames of 300..3000 B (multi-byte characters; deferred, no whole window: every byte is
+    in an edge window) from 16 connections, so frames start and end at every offset of the 4 KiB
+    unmask windows; `bad`: one 0xC0 byte per connection at a random place (often by an edge)"""
+    streams = []
+    for i in range(16):
+        parts = []
+        for _ in range(int(rng.integers(8, 20))):
+            n = int(rng.integers(300, 3000))
+            t = bytearray(("é€😀a" * (n // 10 + 1)).encode()[:n])
+            while True:   # cut at a character boundary (valid text)
+                try:
+                    bytes(t).decode()
+                    break
+                except UnicodeDecodeError:
+                    t = t[:-1]
+            parts.append(t)
+        if bad:
+            br = brng if brng is not None else rng
+            k = int(br.integers(0, len(parts)))
+            parts[k][int(br.integers(0, len(parts[k])))] = 0xC0
+        streams.append(b"".join(synth.frame(1, bytes(p)) for p in parts))
+    return streams
+
+
+@pytest.mark.parametrize("edge", ["1", "0"])
+def test_edge_tables_never_stale(codec_lib, monkeypatch, edge):
+    """The unmask folds the text pieces of the windows where deferred items start or end (edge
+    tables, WF_EDGE) and the check reads no bytes for them.  The same window layout decoded valid
+    then invalid, in place then COMPACT then in place on one context: every decode equals the
+    oracle (a stale table would let the invalid text pass); WSC_U8_EDGE=0 reads every byte."""
+    monkeypatch.setenv("WSC_U8_EDGE", edge)
+    rng = np.random.default_rng(23)
+    good = _edge_batch(np.random.default_rng(1), bad=False)
+    c = K.Codec(0, max_batch_bytes=16 << 20, max_segs=256, max_frames=1 << 14)
+    try:
+        for compact in (False, True, False, False):
+            for streams in (good, _edge_batch(np.random.default_rng(1), bad=True, brng=rng)):
+                # the bad batch: same frames as `good` (same seed), one invalid byte per connection
+                _check(c, streams, compact=compact)
+        res = _check(c, _edge_batch(rng, bad=True))
+        assert int((res.seg["status"] == K.SEG_ERROR).sum()) == 16
+    finally:
+        c.close()

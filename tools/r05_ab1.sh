@@ -4,6 +4,7 @@
 # Results in gpurun_out/r05ab1/; stops at the first failing step.
 o=gpurun_out/r05ab1; mkdir -p $o; export TMPDIR=/tmp
 step() { name=$1; secs=$2; shift 2; echo "=== $name"; timeout -k 10 $secs "$@" > $o/$name.log 2>&1; rc=$?; tail -2 $o/$name.log; [ $rc -eq 0 ] || { echo "$name rc=$rc"; exit $rc; }; }
+step tls 300 python3 -u -m pytest tests/test_gpu_tls.py tests/test_gpu_pong_eof.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider
 HL="--steps 100 --warmup 5 --no-cpu --no-host-inclusive --no-echo --no-other-configs --no-config3"
 for rep in 1 2; do
   step hl_default_$rep 120 python3 bench.py $HL
