@@ -431,6 +431,11 @@ int wsc_session_decode(wsc_session* s);    /* submit + complete until everything
 /* Bytes fed but not yet submitted (a batch takes what fits; the rest waits in per-connection
  * spills): a double-buffered poller submits again while this is non-zero, new reads or not.   */
 int wsc_session_pending(wsc_session* s, uint64_t* bytes);
+/* *ready = 1 when wsc_session_complete would not wait for the device (nothing in flight, or the
+ * submitted batch's work has finished), 0 otherwise.  Lets a thread that shares a session among
+ * pollers (one batching thread per device) hold the session's lock only for calls that do not
+ * block: submit, poll ready without the lock, then complete.                                   */
+int wsc_session_ready(wsc_session* s, int* ready);
 int wsc_session_next(wsc_session* s, uint32_t conn, wsc_event* ev);  /* DecodePacket() */
 /* The peer closed: a read returned 0 (see the EOF rule above).  Reads for conn stop; its queued
  * and still-undecoded bytes are delivered, then WSC_EV_CLOSE 1000 / err 0.                      */

@@ -134,6 +134,7 @@ SIGNATURES = {
     "wsc_session_complete": (_I, [_P]),
     "wsc_session_decode": (_I, [_P]),
     "wsc_session_pending": (_I, [_P, C.POINTER(_U64)]),
+    "wsc_session_ready": (_I, [_P, C.POINTER(_I)]),
     "wsc_session_next": (_I, [_P, _U32, C.POINTER(WscEvent)]),
     "wsc_session_eof": (_I, [_P, _U32]),
     "wsc_session_set_max_message": (_I, [_P, _U64]),
@@ -554,6 +555,12 @@ class Session:
 
     def set_max_message(self, nbytes: int):
         _check(self.lib.wsc_session_set_max_message(self.h, int(nbytes)), "wsc_session_set_max_message")
+
+    def ready(self) -> bool:
+        """complete() would not wait for the device (wsc_session_ready)"""
+        r = C.c_int()
+        _check(self.lib.wsc_session_ready(self.h, C.byref(r)), "wsc_session_ready")
+        return bool(r.value)
 
     def pending(self) -> int:
         """bytes fed but not yet submitted (submit again while non-zero)"""

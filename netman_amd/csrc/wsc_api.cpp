@@ -95,7 +95,6 @@ struct wsc_ctx {
     U8Seg* u8seg = nullptr;
     uint32_t* win_flag = nullptr;       // per unmask window: inside a deferred text item (walk sets, unmask clears)
     uint64_t* win_map = nullptr;        // per unmask window: the DFA map the unmask folded
-    uint4* u8edge = nullptr;            // per unmask window: EDGE_SLOTS edge-piece maps (fold_edges, wsc_unmask.inl)
     uint32_t* u8ctr = nullptr;          // UTF-8 item counters, one per decode parity ([0], [32]): a decode's walk
                                         // allocates from its own, its unmask zeroes the other (the next decode's)
     uint32_t u8par = 0;                 // parity of the decode the last walk belongs to
@@ -103,7 +102,6 @@ struct wsc_ctx {
                                         // counter) was not: the next walk zeroes its counter itself
     uint32_t u8_inline_max = 256;
     uint32_t u8_grid = 0;               // WSC_U8_GRID: k_u8_check workgroups (A/B experiments; 0 = 5 per CU)
-    bool u8_edge = true;                // WSC_U8_EDGE=0: no edge tables (the check reads every partial window's bytes)
     uint32_t u8_wpb = 4;                // WSC_U8_WPB: k_u8_check waves per workgroup (4, or 16 = 1024-thread workgroups)
     bool walk_tiled = true;             // WSC_WALK_TILED=0: the three-launch walk for mode 3 (A/B)
     int hdr_nt = -1;                    // WSC_HDR_NT: the walk's header loads non-temporal: 0 never, 1 always, default COMPACT batches
@@ -326,7 +324,6 @@ int wsc_create(int device, const wsc_config* cfg_in, wsc_ctx** out) {
     chk(hipMalloc(&c->u8seg, (uint64_t)cfg.max_segs * sizeof(U8Seg)), "hipMalloc u8seg");
     chk(hipMalloc(&c->win_flag, c->tile_entries * sizeof(uint32_t)), "hipMalloc win_flag");
     chk(hipMalloc(&c->win_map, c->tile_entries * sizeof(uint64_t)), "hipMalloc win_map");
-    chk(hipMalloc(&c->u8edge, (cfg.max_batch_bytes / 4096 + 2) * EDGE_SLOTS * sizeof(uint4)), "hipMalloc u8edge");
     chk(hipMalloc(&c->u8ctr, 64 * sizeof(uint32_t)), "hipMalloc u8ctr");
     if (rc == WSC_OK) {
         chk(hipMemsetAsync(c->win_flag, 0, c->tile_entries * sizeof(uint32_t), c->stream), "hipMemset win_flag");
@@ -336,7 +333,6 @@ int wsc_create(int device, const wsc_config* cfg_in, wsc_ctx** out) {
     if (const char* e = std::getenv("WSC_UNMASK_BUF"); e && *e) c->unmask_buf = std::atoi(e);
     if (const char* e = std::getenv("WSC_U8_CHAINS"); e && *e) c->u8_chains = std::atoi(e);
     if (const char* e = std::getenv("WSC_U8_GRID"); e && *e) c->u8_grid = (uint32_t)std::strtoul(e, nullptr, 10);
-    if (const char* e = std::getenv("WSC_U8_EDGE"); e && *e) c->u8_edge = e[0] == '1';
     if (const char* e = std::getenv("WSC_U8_WPB"); e && *e) c->u8_wpb = std::atoi(e) == 16 ? 16u : 4u;
     if (const char* e = std::getenv("WSC_AB_NO_U8"); e && e[0] == '1') c->ab_no_u8 = true;
     if (const char* e = std::getenv("WSC_WALK_TILED"); e && e[0] == '0') c->walk_tiled = false;
@@ -381,7 +377,7 @@ int wsc_destroy(wsc_ctx* c) {
                     c->d_seg_off, c->d_state_in, c->d_state_out, c->d_seg_out, c->d_frames,
                     c->d_frame_dst, c->d_summary, c->enc_lb_state, c->enc_lb_agg, c->enc_lb_incl, c->enc_tile,
                     c->d_enc_msgs, c->d_enc_src, c->d_enc_out, c->d_enc_off, c->u8items, c->u8maps, c->u8seg,
-                    c->win_flag, c->win_map, c->u8ctr, c->u8edge};
+                    c->win_flag, c->win_map, c->u8ctr};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -598,7 +594,6 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     if (need_u8) {
         uw.flag = c->win_flag;
         uw.map = c->win_map;
-        uw.edge = c->u8_edge ? c->u8edge : nullptr;
         uw.count = c->u8ctr + 32 * c->u8par;
     }
     hipLaunchKernelGGL(kern, ugrid, ublk, 0, st, udst, (const uint8_t*)b->wire, b->n_bytes, b->n_bytes,
@@ -624,7 +619,6 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
         ua.state_out = b->state_out;
         ua.summary = b->summary;
         ua.win_map = c->win_map;
-        ua.edge = c->u8_edge ? c->u8edge : nullptr;
         ua.win_shift = ilog2(c->pieces * 1024);
         ua.unmasked = compact ? 0u : 1u;
         ua.out = udst;

@@ -443,16 +443,9 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
             if (a.win_flag) {   // windows inside the piece: folded by the unmask
                 uint64_t wi = (ps + W - 1) >> a.win_shift;
                 const uint64_t we = pe >> a.win_shift;
-                for (; wi < we && (wi & 3); ++wi) a.win_flag[wi] = WF_WHOLE;
-                for (; wi + 4 <= we; wi += 4)
-                    *reinterpret_cast<uint4*>(a.win_flag + wi) = make_uint4(WF_WHOLE, WF_WHOLE, WF_WHOLE, WF_WHOLE);
-                for (; wi < we; ++wi) a.win_flag[wi] = WF_WHOLE;
-                // the windows the piece starts or ends inside: the unmask folds their span pieces into
-                // the window's edge table (no window inside an item is another item's edge window)
-                if (pe > ps) {
-                    if (ps & (W - 1)) a.win_flag[ps >> a.win_shift] = WF_EDGE;
-                    if (pe & (W - 1)) a.win_flag[(pe - 1) >> a.win_shift] = WF_EDGE;
-                }
+                for (; wi < we && (wi & 3); ++wi) a.win_flag[wi] = 1u;
+                for (; wi + 4 <= we; wi += 4) *reinterpret_cast<uint4*>(a.win_flag + wi) = make_uint4(1, 1, 1, 1);
+                for (; wi < we; ++wi) a.win_flag[wi] = 1u;
             }
             it.seg = s;
             it.ordinal = nf;

@@ -147,7 +147,6 @@ struct U8Args {
     wsc_conn_state* state_out;
     wsc_summary* summary;
     const uint64_t* win_map;     // per unmask window: the map the unmask folded
-    const uint4* edge;           // per unmask window: EDGE_SLOTS edge-piece maps the unmask folded (U8Win.edge)
     uint32_t win_shift;
     uint32_t unmasked;           // 1: the wire is already unmasked (in place): items are read with mask 0
     uint8_t* out;                // where the spans' bytes went: the wire (in place) or the arena (COMPACT)
@@ -159,21 +158,9 @@ struct U8Args {
 
 // The unmask's side of the text windows (k_unmask): flag / map per window, and the item count
 // (zero = nothing deferred: the LDS tables are not even built).
-// Window flags the walk sets (win_flag): WF_WHOLE = the window lies inside one deferred item (the
-// unmask folds its map into win_map); WF_EDGE = a deferred item starts or ends inside it (the
-// unmask folds each span piece of the window into the window's edge table, or clears the table).
-// Edge table: EDGE_SLOTS entries per window, {x = piece start in the window | EDGE_VALID, y = 0,
-// z/w = the piece's map}; the check looks an item's partial windows up there (its key: the item's
-// start offset in its first window, 0 in its last) and reads the bytes only on a miss.  Every
-// window flagged WF_EDGE has its whole table rewritten by the unmask of the decode, so a hit is
-// never stale.
-constexpr uint32_t WF_WHOLE = 1u, WF_EDGE = 2u;
-constexpr uint32_t EDGE_SLOTS = 8;
-constexpr uint32_t EDGE_VALID = 0x80000000u;
 struct U8Win {
     uint32_t* flag;
     uint64_t* map;
-    uint4* edge;                 // EDGE_SLOTS per window (null: edges never published -- the check reads bytes)
     const uint32_t* count;
     uint32_t* rearm;             // the next decode's item counter (zeroed by the unmask: always launched)
     uint32_t xcd_run;            // blocks per XCD run: consecutive logical blocks (windows) on one XCD

@@ -99,6 +99,7 @@ struct Stage {                    // one staging set: pinned host buffers, devic
     wsc_ctx* ctx = nullptr;
     hipStream_t stream = nullptr;
     hipEvent_t ev = nullptr;      // WSC_SESSION_BLOCKING_WAIT: a blocking-sync event complete() sleeps on
+    hipEvent_t done_ev = nullptr; // recorded after the launch's last operation: wsc_session_ready
     uint8_t* h_wire = nullptr;    // masked bytes as read (input)
     uint8_t* h_res = nullptr;     // results: unmasked wire (in place) or the arena (COMPACT)
     uint64_t* h_seg_off = nullptr;
@@ -501,6 +502,7 @@ int launch_stage(wsc_session* s, Stage& g) {
     // the launch instead of after complete()'s first wait, so it overlaps the host's work on the
     // previous round (views into h_res of this set were materialised by the complete() before)
     if (!compact) HT(hipMemcpyAsync(g.h_res, g.d_wire, g.bytes, hipMemcpyDeviceToHost, st));
+    HT(hipEventRecord(g.done_ev, st));
 #undef HT
     return WSC_OK;
 }
@@ -544,6 +546,10 @@ int wsc_session_create(int device, const wsc_config* cfg, uint32_t flags, wsc_se
         if (const hipError_t e = hipSetDevice(device); e != hipSuccess) { rc = hip_fail("hipSetDevice", e); break; }
         if (const hipError_t e = hipStreamCreateWithFlags(&t.stream, hipStreamNonBlocking); e != hipSuccess) {
             rc = hip_fail("hipStreamCreateWithFlags", e);
+            break;
+        }
+        if (const hipError_t e = hipEventCreateWithFlags(&t.done_ev, hipEventDisableTiming); e != hipSuccess) {
+            rc = hip_fail("hipEventCreateWithFlags", e);
             break;
         }
         if (s->flags & WSC_SESSION_BLOCKING_WAIT)
@@ -605,6 +611,7 @@ int wsc_session_destroy(wsc_session* s) {
                 if (p) wsc_dev_free(t.ctx, p);
         }
         if (t.ev) (void)hipEventDestroy(t.ev);
+        if (t.done_ev) (void)hipEventDestroy(t.done_ev);
         if (t.stream) (void)hipStreamDestroy(t.stream);
         if (t.ctx) wsc_destroy(t.ctx);
     }
@@ -878,6 +885,14 @@ int wsc_session_decode(wsc_session* s) {
 
 // bytes fed but not yet submitted (the staging being filled + connections' spills): a poller calls
 // submit again while this is non-zero, even in a round without new reads
+int wsc_session_ready(wsc_session* s, int* ready) {
+    if (!s || !ready) return WSC_E_INVAL;
+    *ready = 1;
+    for (const Stage& g : s->st)
+        if (g.in_flight && g.launch_rc == WSC_OK && g.done_ev && hipEventQuery(g.done_ev) == hipErrorNotReady) *ready = 0;
+    return WSC_OK;
+}
+
 int wsc_session_pending(wsc_session* s, uint64_t* bytes) {
     if (!s || !bytes) return WSC_E_INVAL;
     apply_removes(s);

@@ -256,32 +256,6 @@ __device__ __forceinline__ void u8_check_run(const U8Args& a, U8Lds& T, uint4 (*
     auto chunk_len = [](uint32_t len, uint32_t off) -> uint32_t {
         return off < len ? (len - off >= 64 ? 64u : len - off) : 0u;
     };
-    // The item's partial windows from the unmask's edge tables (fold_edges): its piece in its first
-    // window (key = its start offset there) unless that window is whole, and its piece in its last
-    // window (key 0) when that is another window and partial.  16 lanes per query group g: lanes
-    // 8 g' + slot of the group look up the head (g' = 0) and the tail (g' = 1).  Returns, on the
-    // group's lanes, whether every needed piece was found, and the head and tail maps (identity
-    // where not needed; the whole windows between them are the caller's).
-    auto edge_lookup = [&](uint64_t src, uint32_t len, bool valid, uint64_t& hm, uint64_t& tm) -> bool {
-        const uint32_t g = lane & ~15u, j = lane & 7u;
-        const bool tl = (lane & 8u) != 0;
-        const uint64_t e = src + len;
-        const uint64_t wh = src >> a.win_shift, wt = (e - 1) >> a.win_shift;
-        const bool first_whole = (src & (W - 1)) == 0 && e >= src + W;
-        const bool need_h = valid && len && !first_whole;
-        const bool need_t = valid && len && wt != wh && (e & (W - 1)) != 0;
-        const bool want = tl ? need_t : need_h;
-        const uint32_t key = (tl ? 0u : (uint32_t)(src & (W - 1))) | EDGE_VALID;
-        const uint4 en = want ? a.edge[(tl ? wt : wh) * EDGE_SLOTS + j] : make_uint4(0, 0, 0, 0);
-        const uint64_t mm = __ballot(want && en.x == key);
-        const uint32_t hb = (uint32_t)(mm >> g) & 0xFFu, tb = (uint32_t)(mm >> (g + 8)) & 0xFFu;
-        const uint32_t sh = g + (hb ? (uint32_t)__builtin_ctz(hb) : 0u), st = g + 8 + (tb ? (uint32_t)__builtin_ctz(tb) : 0u);
-        const uint64_t mh = (uint64_t)(uint32_t)__shfl((int)en.w, (int)sh) << 32 | (uint32_t)__shfl((int)en.z, (int)sh);
-        const uint64_t mt = (uint64_t)(uint32_t)__shfl((int)en.w, (int)st) << 32 | (uint32_t)__shfl((int)en.z, (int)st);
-        hm = need_h ? mh : u8m_id();
-        tm = need_t ? mt : u8m_id();
-        return (!need_h || hb) && (!need_t || tb);
-    };
     // A unit is 4 consecutive items.  Units of small items (<= 1 KiB each: 1 KiB text frames) take
     // one step: row r (16 lanes x 64 B) holds item r, and lanes 0, 16, 32, 48 publish the 4 items'
     // maps.  Other units walk their items' steps in order, the next step's loads -- the next
@@ -290,35 +264,26 @@ __device__ __forceinline__ void u8_check_run(const U8Args& a, U8Lds& T, uint4 (*
     // items one by one paid a scan of every unit's lengths per wave.)
     // Other units walk their items' steps in order, the next step's loads -- the next item's first
     // step too -- issued before the current step is folded.
-    // the windows between an item's head and tail, folded by the unmask: each lane composes a run of
-    // ceil(nwin / 64) of them, the wave composes the lanes in order
-    auto item_mids = [&](const Geo& g) -> uint64_t {
-        if (!g.nwin) return u8m_id();
-        const uint32_t k = (g.nwin + 63) / 64;
-        uint64_t m = u8m_id();
-        for (uint32_t q = 0; q < k; ++q)
-            if (lane * k + q < g.nwin) m = u8m_then(m, a.win_map[g.w0 + (uint64_t)lane * k + q]);
-        return u8_wave_map(m, false, lane);
-    };
     auto unit_large = [&](uint32_t i0, uint32_t cnt) {
         // (prefetch within an item only: carrying the next item's geometry and first step across
         // the fold held ~15 more VGPRs, past 128)
         for (uint32_t j = 0; j < cnt; ++j) {
             const U8Item item = a.items[i0 + j];
             const Geo g = geo(item);
-            // partial windows the unmask folded: no bytes read (lanes 0..15 look them up)
-            uint64_t ehm = u8m_id(), etm = u8m_id();
-            const bool ehit = a.edge && __builtin_amdgcn_readfirstlane((int)edge_lookup(item.src, item.len, true, ehm, etm)) != 0;
-            uint64_t acc = u8m_id();
-            if (ehit) {   // head, the windows between, tail (lane 0's maps)
-                acc = u8m_then(u8m_then(ehm, item_mids(g)), etm);
-            } else {
             uint32_t b0 = first_step(g, item.len);
             u32x4 nxt[4];
             if (b0 != NONE) fetch(item, b0, b0 < g.hl ? g.hl : item.len, nxt);
             // the windows between head and tail, folded by the unmask: each lane composes a run
             // of ceil(nwin / 64) of them, the wave composes the lanes in order
-            const uint64_t mids = item_mids(g);
+            uint64_t mids = u8m_id();
+            if (g.nwin) {
+                const uint32_t k = (g.nwin + 63) / 64;
+                uint64_t m = u8m_id();
+                for (uint32_t q = 0; q < k; ++q)
+                    if (lane * k + q < g.nwin) m = u8m_then(m, a.win_map[g.w0 + (uint64_t)lane * k + q]);
+                mids = u8_wave_map(m, false, lane);
+            }
+            uint64_t acc = u8m_id();
             bool mids_in = false;
             while (b0 != NONE) {
                 u32x4 cur4[4];
@@ -339,7 +304,6 @@ __device__ __forceinline__ void u8_check_run(const U8Args& a, U8Lds& T, uint4 (*
                 b0 = nb;
             }
             if (!mids_in) acc = u8m_then(acc, mids);
-            }
             uint32_t res = U8R_DEAD, ret = 0, n = 0;
             if (lane == 0) res = u8_store(a, i0 + j, item, acc);
             res = (uint32_t)__builtin_amdgcn_readfirstlane((int)res);
@@ -400,28 +364,19 @@ __device__ __forceinline__ void u8_check_run(const U8Args& a, U8Lds& T, uint4 (*
         bool nsmall = false;
         u32x4 qn[4] = {};
         if (cur_small) {
-            const uint32_t r = lane >> 4;
-            // row r's item (the verdict's, and the edge lookup's)
-            const U8Item xr = a.items[i0 + (r < cnt ? r : 0u)];
-            const uint32_t rlen = r < cnt ? xr.len : 0u;
-            // the unit's items (<= 1 KiB: no whole window) from the unmask's edge tables, when all
-            // four are there: no text byte is read again
-            uint64_t ehm = u8m_id(), etm = u8m_id();
-            const bool rhit = a.edge ? edge_lookup(xr.src, rlen, r < cnt, ehm, etm) : false;
-            const bool hit = a.edge && __ballot(!rhit) == 0;
-            if (!hit && !WSC_CHECK_PREFETCH) unit_data(xc, qc);
+            if (!WSC_CHECK_PREFETCH) unit_data(xc, qc);
             // restaged so that row r (lanes 16r..16r+15) holds item r in 64-byte chunks (items
-            // <= 1 KiB hold no window)
-            uint64_t rm;
-            if (hit) {
-                rm = u8m_then(ehm, etm);
-            } else {
-                u8_restage(sw, qc, lane);
-                const uint32_t off = (lane & 15) * 64;
-                bool plain;
-                const uint64_t pm = u8_chunk_map<NCH, U8P_LANE>(T, qc, a.unmasked ? 0u : xr.mask, chunk_len(rlen, off), plain);
-                rm = u8_row_maps(pm, lane);
-            }
+            // <= 1 KiB hold no window).  The row's full item is needed only by the verdict: its
+            // load overlaps the fold.
+            const uint32_t r = lane >> 4;
+            const U8Item xr = a.items[i0 + (r < cnt ? r : 0u)];
+            const uint32_t rlen = r == 0 ? xc.len[0] : r == 1 ? xc.len[1] : r == 2 ? xc.len[2] : xc.len[3];
+            const uint32_t rmask = r == 0 ? xc.mask[0] : r == 1 ? xc.mask[1] : r == 2 ? xc.mask[2] : xc.mask[3];
+            u8_restage(sw, qc, lane);
+            const uint32_t off = (lane & 15) * 64;
+            bool plain;
+            const uint64_t pm = u8_chunk_map<NCH, U8P_LANE>(T, qc, a.unmasked ? 0u : rmask, chunk_len(rlen, off), plain);
+            const uint64_t rm = u8_row_maps(pm, lane);
             if (un < n_units) {
                 nsmall = unit_small(xn);
                 if (nsmall && WSC_CHECK_PREFETCH) unit_data(xn, qn);

@@ -162,24 +162,16 @@ __device__ __forceinline__ bool load_span_lane(const Span* __restrict__ spans, u
     return false;
 }
 
-// Edge text pieces of a lane-parallel in-place window (WF_EDGE): defined below (fold_edges).
-[[maybe_unused]] static __device__ __attribute__((noinline)) void fold_edges(U8Win u8w, uint64_t win, uint32_t lane,
-                                                                              int32_t rd, int32_t re, uint32_t nl,
-                                                                              u32x4 a0, u32x4 a1, u32x4 a2, u32x4 a3);
-
 // General window, lane-parallel: the wave loads the window's spans into lanes with one vector
 // load (span r0 + lane), then every lane finds the span holding its piece by a binary search over
 // the lanes (ds_bpermute; as many steps as the window has spans need) and takes that span and the
 // next one -- at most 2 spans per 16-byte piece unless spans are shorter than 16 B, which a
 // uniform tail loop handles.  No dependent scalar loads per span.  v[] holds the window's wire
 // pieces.  Returns false (nothing written) when more than 64 spans overlap the window.
-// EDGE (the U8 in-place variants, P = 4): when the window is flagged WF_EDGE (`text`), the pieces
-// just unmasked are folded into the window's edge table (fold_edges) before returning.
-template <bool COMPACT, int P, int NT, bool EDGE = false>
+template <bool COMPACT, int P, int NT>
 __device__ __forceinline__ bool unmask_window_lanes(uint8_t* __restrict__ dst, const Span& sp, bool valid,
                                                     uint32_t n_spans, uint32_t r0, uint64_t wbase, uint32_t lane,
-                                                    const u32x4 (&v)[P], const u32x4* __restrict__ pm,
-                                                    uint32_t text = 0, U8Win u8w = U8Win{}, uint64_t win = 0) {
+                                                    const u32x4 (&v)[P], const u32x4* __restrict__ pm) {
     constexpr int32_t WB = 1024 * P;
     int32_t rd = WB + 64, re = WB + 64;   // window-relative wire [start, end), clipped to [-1, WB + 64]
     uint32_t key = 0;
@@ -293,8 +285,6 @@ __device__ __forceinline__ bool unmask_window_lanes(uint8_t* __restrict__ dst, c
 #pragma unroll
             for (int k = 0; k < P; ++k) st16v<NT>(dst + wbase + k * 1024u + lane * 16u, acc[k]);
         }
-        if constexpr (EDGE && P == 4)
-            if (text & WF_EDGE) fold_edges(u8w, win, lane, rd, re, nl, acc[0], acc[1], acc[2], acc[3]);
         return true;
     }
     if (__ballot(more)) {
@@ -457,9 +447,18 @@ __device__ __forceinline__ void fold_text_window(const u32x4 (&v)[P], uint32_t k
         fold_staged<P>(v, key, u8w, win, lane);
     }
 }
-// The workgroup's UTF-8 tables (g_u8b.t): built by the first wave that needs them, the others wait.
-__device__ __forceinline__ void u8b_tables_ready(uint32_t lane) {
+template <int P>
+__device__ __forceinline__ void fold_staged(const u32x4* v, uint32_t key, U8Win u8w, uint64_t win, uint32_t lane) {
     U8Block& b = g_u8b;
+    uint4* sw = b.stage[(threadIdx.x >> 6) & 3];
+    auto stage_write = [&](int g) {   // groups after the first (P = 8)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t o = 1024u * k + 16u * lane;
+            const u32x4 x = v[4 * g + k] ^ key;
+            sw[(o >> 6) * 5 + ((o >> 4) & 3)] = make_uint4(x[0], x[1], x[2], x[3]);
+        }
+    };
     uint32_t prev = 0;
     if (lane == 0) prev = __hip_atomic_compare_exchange_strong(&b.state, &prev, 1u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                                __HIP_MEMORY_SCOPE_WORKGROUP) ? 0u : prev;
@@ -473,21 +472,6 @@ __device__ __forceinline__ void u8b_tables_ready(uint32_t lane) {
         while (__hip_atomic_load(&b.state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 2u) __builtin_amdgcn_s_sleep(1);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     }
-}
-
-template <int P>
-__device__ __forceinline__ void fold_staged(const u32x4* v, uint32_t key, U8Win u8w, uint64_t win, uint32_t lane) {
-    U8Block& b = g_u8b;
-    uint4* sw = b.stage[(threadIdx.x >> 6) & 3];
-    auto stage_write = [&](int g) {   // groups after the first (P = 8)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t o = 1024u * k + 16u * lane;
-            const u32x4 x = v[4 * g + k] ^ key;
-            sw[(o >> 6) * 5 + ((o >> 4) & 3)] = make_uint4(x[0], x[1], x[2], x[3]);
-        }
-    };
-    u8b_tables_ready(lane);
     uint64_t m = u8m_id();
 #pragma unroll
     for (int g = 0; g < P / 4; ++g) {
@@ -512,112 +496,6 @@ __device__ __forceinline__ void fold_staged(const u32x4* v, uint32_t key, U8Win 
 
 static inline __device__ __attribute__((noinline)) void fold_staged4(U8Win u8w, uint64_t win, uint32_t lane) {
     fold_staged<4>(nullptr, 0u, u8w, win, lane);
-}
-
-// A WF_EDGE window that no fold publishes (COMPACT, 8 KiB windows, the general window): its edge
-// table is emptied -- the check then reads those items' bytes, never a stale map -- and the flag
-// consumed.
-__device__ __forceinline__ void edge_clear(U8Win u8w, uint64_t win, uint32_t lane) {
-    if (u8w.edge && lane < EDGE_SLOTS) u8w.edge[win * EDGE_SLOTS + lane] = make_uint4(0, 0, 0, 0);
-    if (lane == 0) u8w.flag[win] = 0u;
-}
-
-// The UTF-8 maps of a lane-parallel in-place window's span pieces (WF_EDGE: a deferred text item
-// starts or ends inside it), from the bytes the wave has just unmasked (a0..a3: piece k of lane l
-// = window bytes 1024 k + 16 l), so that k_u8_check reads no text bytes for these partial windows
-// (1 KiB TEXT was read twice: by the unmask and by the check).  Lane i holds span r + i, window-
-// relative [rd, re) (nl spans overlap the window).  The window goes to the wave's stage in 68-byte
-// rows (a pad dword after each 64 bytes: 64-byte chunks 64 bytes apart hit distinct banks); each
-// piece is cut into 64-byte chunks from its own start, one chunk per lane (u8_chunk_map, the check's
-// fold), the chunks of a piece composed in order by a segmented scan over the lanes, and the
-// piece's last chunk publishes {start | EDGE_VALID, map} in slot <piece ordinal>.  Pieces past
-// EDGE_SLOTS are not folded (the check reads them); slots no piece took are zeroed.
-[[maybe_unused]] static __device__ __attribute__((noinline)) void fold_edges(U8Win u8w, uint64_t win, uint32_t lane,
-                                                                              int32_t rd, int32_t re, uint32_t nl,
-                                                                              u32x4 a0, u32x4 a1, u32x4 a2, u32x4 a3) {
-    constexpr int32_t WB = 4096;
-    if (!u8w.edge) {
-        edge_clear(u8w, win, lane);
-        return;
-    }
-    U8Block& b = g_u8b;
-    uint32_t* sd = reinterpret_cast<uint32_t*>(b.stage[(threadIdx.x >> 6) & 3]);
-    const u32x4 av[4] = {a0, a1, a2, a3};
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const uint32_t x = (1024u * k + 16u * lane) >> 2;   // dword of the window, then padded
-        const uint32_t d = x + (x >> 4);
-        sd[d] = av[k][0];
-        sd[d + 1] = av[k][1];
-        sd[d + 2] = av[k][2];
-        sd[d + 3] = av[k][3];
-    }
-    u8b_tables_ready(lane);
-    __builtin_amdgcn_wave_barrier();
-    // this lane's piece; slot = ordinal among the window's pieces
-    const int32_t pa = rd < 0 ? 0 : rd, pb = re > WB ? WB : re;
-    const bool piece = lane < nl && pa < pb;
-    const uint64_t pmask = __ballot(piece);
-    const uint32_t slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(pmask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)pmask, 0u));
-    const bool pub = piece && slot < EDGE_SLOTS;
-    const uint32_t npub = (uint32_t)__builtin_popcountll(__ballot(pub));
-    const uint32_t nch = pub ? (uint32_t)(pb - pa + 63) >> 6 : 0u;
-    uint32_t e = nch;   // inclusive scan of the chunk counts: piece i owns chunks [e_i - nch_i, e_i)
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t t = __shfl_up(e, d);
-        if (lane >= (uint32_t)d) e += t;
-    }
-    const uint32_t C = __shfl(e, 63);
-    uint64_t carry = u8m_id();   // a piece whose chunks continue into the next round
-    int32_t carry_p = -1;
-    for (uint32_t base = 0; base < C; base += 64) {
-        const uint32_t q = base + lane;
-        const bool act = q < C;
-        int32_t lo = -1;   // the chunk's piece: the first lane p with e_p > q
-#pragma unroll
-        for (int32_t st = 32; st >= 1; st >>= 1) {
-            const int32_t c = lo + st;
-            if (__shfl(e, c) <= q) lo = c;
-        }
-        const int32_t p = lo + 1 > 63 ? 63 : lo + 1;
-        const uint32_t ep = __shfl(e, p), cb = ep - __shfl(nch, p);
-        const int32_t ppa = __shfl(pa, p), ppb = __shfl(pb, p);
-        const uint32_t pslot = __shfl(slot, p);
-        const uint32_t o = act ? (uint32_t)ppa + 64u * (q - cb) : 0u;
-        const uint32_t nk = act ? ((int32_t)o + 64 <= ppb ? 64u : (uint32_t)(ppb - (int32_t)o)) : 0u;
-        u32x4 c4[4];
-        {
-            const uint32_t x0 = o >> 2, sh = o & 3;
-            uint32_t w[17];
-#pragma unroll
-            for (int j = 0; j < 17; ++j) {
-                const uint32_t x = x0 + j;
-                w[j] = sd[x + (x >> 4)];
-            }
-#pragma unroll
-            for (int j = 0; j < 16; ++j) c4[j >> 2][j & 3] = __builtin_amdgcn_alignbyte(w[j + 1], w[j], sh);
-        }
-        bool plain;
-        uint64_t m = u8_chunk_map<WSC_FOLD_NCH, U8P_WAVE>(b.t, c4, 0u, nk, plain);
-        if (lane == 0 && p == carry_p) m = u8m_then(carry, m);
-        // segmented inclusive scan: the chunks of one piece composed in order
-        const uint32_t s0 = cb > base ? cb - base : 0u;   // the piece's first lane in this round
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t ml = __shfl_up((uint32_t)m, d), mh = __shfl_up((uint32_t)(m >> 32), d);
-            if (lane >= (uint32_t)d && lane - (uint32_t)d >= s0) m = u8m_then((uint64_t)mh << 32 | ml, m);
-        }
-        const bool last = act && q + 1 == ep;
-        if (last) u8w.edge[win * EDGE_SLOTS + pslot] = make_uint4((uint32_t)ppa | EDGE_VALID, 0u, (uint32_t)m, (uint32_t)(m >> 32));
-        // lane 63's piece goes on in the next round: its map so far prefixes that round's lane 0
-        carry = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(m >> 32), 63) << 32 |
-                (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)m, 63);
-        carry_p = __builtin_amdgcn_readlane(last ? -1 : p, 63);
-    }
-    if (lane >= npub && lane < EDGE_SLOTS) u8w.edge[win * EDGE_SLOTS + lane] = make_uint4(0, 0, 0, 0);
-    __builtin_amdgcn_wave_barrier();   // (the stage is reused by the wave's next window)
-    if (lane == 0) u8w.flag[win] = 0u;
 }
 
 // NT bit 0: non-temporal loads, bit 1: non-temporal stores.  In place `src` is unused (dst is
@@ -663,7 +541,6 @@ __device__ __forceinline__ void unmask_all(uint8_t* __restrict__ dst, const uint
         if (wbase + WB > total) {   // the last, partial window
             const uint32_t r = tile_first[win];
             unmask_window_general<COMPACT, P, NT>(dst, src, src_bytes, total, spans, n_spans, r, wbase, lofs);
-            if constexpr (U8) if (u8w.flag[win] & WF_EDGE) edge_clear(u8w, win, lane);
             continue;
         }
         u32x4 v[P];
@@ -696,10 +573,7 @@ __device__ __forceinline__ void unmask_all(uint8_t* __restrict__ dst, const uint
 #pragma unroll
                 for (int k = 0; k < P; ++k) st16v<NT>(dst + wbase + k * 1024u + lofs, v[k] ^ s0.key);
             }
-            if constexpr (U8) {
-                if (text & WF_WHOLE) fold_text_window<COMPACT, P>(v, s0.key, u8w, win, lane);
-                else if (text & WF_EDGE) edge_clear(u8w, win, lane);   // (the walk never flags one)
-            }
+            if constexpr (U8) if (text) fold_text_window<COMPACT, P>(v, s0.key, u8w, win, lane);
             continue;
         }
         // Several spans overlap the window (small frames) or it holds a frame edge: lane-parallel
@@ -707,20 +581,15 @@ __device__ __forceinline__ void unmask_all(uint8_t* __restrict__ dst, const uint
         Span sp;
         const bool valid = load_span_lane(spans, n_spans, r, lane, sp);
         bool done;
-        [[maybe_unused]] bool edged = false;   // the window's edge pieces were folded (fold_edges)
         if constexpr (COMPACT && WSC_COMPACT_EDGE2 && P == 4) {
             uint4* stage;
             if constexpr (U8) stage = g_u8b.stage[(threadIdx.x >> 6) & 3];   // (the fold's stage: fast-path windows only)
             else stage = c_stage[(threadIdx.x >> 6) & 3];
             done = unmask_window_lanes_c<P, NT>(dst, sp, valid, n_spans, r, wbase, lane, v, stage);
-        } else if constexpr (!COMPACT && U8 && P == 4) {
-            done = unmask_window_lanes<false, P, NT, true>(dst, sp, valid, n_spans, r, wbase, lane, v, pm, text, u8w, win);
-            edged = done;
         } else {
             done = unmask_window_lanes<COMPACT, P, NT>(dst, sp, valid, n_spans, r, wbase, lane, v, pm);
         }
         if (!done) unmask_window_general<COMPACT, P, NT>(dst, src, src_bytes, total, spans, n_spans, r, wbase, lofs);
-        if constexpr (U8) if ((text & WF_EDGE) && !edged) edge_clear(u8w, win, lane);
     }
 }
 

@@ -237,13 +237,12 @@ def _edge_batch(rng, bad, brng=None):
     return streams
 
 
-@pytest.mark.parametrize("edge", ["1", "0"])
-def test_edge_tables_never_stale(codec_lib, monkeypatch, edge):
-    """The unmask folds the text pieces of the windows where deferred items start or end (edge
-    tables, WF_EDGE) and the check reads no bytes for them.  The same window layout decoded valid
-    then invalid, in place then COMPACT then in place on one context: every decode equals the
-    oracle (a stale table would let the invalid text pass); WSC_U8_EDGE=0 reads every byte."""
-    monkeypatch.setenv("WSC_U8_EDGE", edge)
+def test_text_window_edges_alternating_layouts(codec_lib):
+    """Deferred TEXT frames of 300..3000 B starting and ending at every offset of the 4 KiB unmask
+    windows (every byte in a partial window: the check's head/tail path), the same window layout
+    decoded valid then invalid, in place then COMPACT then in place on one context: every decode
+    equals the oracle -- state a decode leaves in the context (window flags and maps) never lets a
+    later decode's invalid text pass."""
     rng = np.random.default_rng(23)
     good = _edge_batch(np.random.default_rng(1), bad=False)
     c = K.Codec(0, max_batch_bytes=16 << 20, max_segs=256, max_frames=1 << 14)

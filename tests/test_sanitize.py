@@ -48,3 +48,20 @@ def test_oracle_sanitized():
     exe = _build("oracle_fuzz", ["gcc", "-fsanitize=address,undefined"] + FLAGS +
                  [os.path.join(SAN, "oracle_fuzz.c"), os.path.join(ROOT, "oracle", "ws_oracle.c")])
     assert "runs" in _run(exe)
+
+
+ECHO_SRCS = [os.path.join(ROOT, "tools", "ws_echo.cpp"), os.path.join(ROOT, "netman_amd", "csrc", "wsc_session.cpp"),
+             os.path.join(SAN, "session_stub.cpp")]
+
+
+@pytest.mark.parametrize("args", [["--pollers", "4"], ["--pollers", "8", "--shutdown"],
+                                  ["--pollers", "3", "--frames", "20", "--size", "70000", "--blocking-wait"]])
+def test_echo_batcher_thread_sanitized(args):
+    """ws_echo --batcher (one batching thread per device owning the session all pollers share:
+    feeds and event reads under its lock, the device polled with wsc_session_ready outside it)
+    over the host-memory device stand-in, under TSan: real loopback sockets, every echoed byte
+    checked by the clients, EOF ordering with --shutdown"""
+    exe = _build("ws_echo_batcher_tsan", ["g++", "-std=c++17", "-pthread", "-fsanitize=thread"] + FLAGS + HIP_INC +
+                 ECHO_SRCS)
+    out = _run(exe, "--batcher", "--conns", "16", "--frames", "50", "--size", "4096", "--client-threads", "2", *args)
+    assert '"ok": true' in out

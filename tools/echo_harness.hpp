@@ -65,6 +65,9 @@ struct Decoder {
     virtual void submit() { decode(); }
     virtual void complete() {}
     virtual bool pending() { return false; }   // fed bytes a batch could not take yet
+    // the poller has taken this round's events (next() until EV_NONE for every connection it fed);
+    // a decoder shared by several pollers may then hand out the next round's
+    virtual void drained() {}
 };
 
 struct Result {
@@ -391,6 +394,7 @@ inline Result run(const DecoderFactory& make_decoder, int pollers, int conns, in
                     if (!sc[q].closing) eofs[w++] = q;
                 eofs.resize(w);
             }
+            dec.drained();
             for (size_t i = 0; i < sc.size(); ++i) {
                 ServerConn& c = sc[i];
                 if (c.closed) continue;
