@@ -809,11 +809,30 @@ def host_inclusive(codec, cfg, K):
         lib.wsc_host_free(p)
 
 
-def host_inclusive_pipelined(torch, codecs, streams, cfg, K, chunks=16, iters=3, dir_streams=False):
+def host_inclusive_pipelined(torch, codecs, streams, cfg, K, chunks=16, iters=3, dir_streams=False, nbuf=0,
+                             copy_streams=1):
     """The same batch from pinned host memory, cut at segment boundaries into `chunks` pieces that
     alternate between the in-flight contexts/streams: H2D of piece i+1 overlaps the decode and
     the D2H of piece i (PCIe is full duplex).  Output: unmasked wire + frame records in pinned
-    host memory.  Reported in DESIGN.md, never as `value`."""
+    host memory.  Reported in DESIGN.md, never as `value`.  nbuf > len(codecs): that many piece-
+    sized contexts of its own; copy_streams: streams per copy direction (dir_streams), piece i on
+    stream i % copy_streams (the copy engines a stream lands on decide whether H2D and D2H overlap)."""
+    own = []
+    if nbuf > len(codecs):
+        n_segs_all = len(cfg["seg_off"]) - 1
+        piece_bytes = int(cfg["seg_off"][min(n_segs_all, (n_segs_all + chunks - 1) // chunks + 1)]) * 2 + 4096
+        own = [K.Codec(0, max_batch_bytes=piece_bytes, max_segs=n_segs_all // chunks + 16,
+                       max_frames=int(codecs[0].cfg.max_frames)) for _ in range(nbuf)]
+        codecs = own
+        streams = [torch.cuda.Stream() for _ in range(nbuf)]
+    try:
+        return _host_inclusive_pipelined(torch, codecs, streams, cfg, K, chunks, iters, dir_streams, copy_streams)
+    finally:
+        for c in own:
+            c.close()
+
+
+def _host_inclusive_pipelined(torch, codecs, streams, cfg, K, chunks, iters, dir_streams, copy_streams):
     P = len(codecs)
     if P < 2:
         return None
@@ -849,7 +868,8 @@ def host_inclusive_pipelined(torch, codecs, streams, cfg, K, chunks=16, iters=3,
     # one stream per PCIe direction (dir_streams): H2D of piece i+1 queued on its own stream can run
     # beside piece i's D2H on another, instead of queueing behind it on the piece's stream; events
     # order buffer reuse (H2D into buffer j waits for the D2H out of it) and each decode
-    h2d, d2h = (torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)) if dir_streams else (None, None)
+    h2ds = [torch.cuda.Stream(device=dev) for _ in range(copy_streams)] if dir_streams else []
+    d2hs = [torch.cuda.Stream(device=dev) for _ in range(copy_streams)] if dir_streams else []
     ev_free = [None] * P
 
     def one_pass():
@@ -859,6 +879,7 @@ def host_inclusive_pipelined(torch, codecs, streams, cfg, K, chunks=16, iters=3,
             batch = codecs[j].make_batch(b["wire"], b["seg_off"][: k + 1], None, b["st"], b["so"], b["fr"],
                                          b["sm"], n_bytes=a1 - a0)
             if dir_streams:
+                h2d, d2h = h2ds[i % copy_streams], d2hs[i % copy_streams]
                 with torch.cuda.stream(h2d):
                     if ev_free[j] is not None:
                         h2d.wait_event(ev_free[j])
@@ -894,7 +915,8 @@ def host_inclusive_pipelined(torch, codecs, streams, cfg, K, chunks=16, iters=3,
     torch.cuda.synchronize()
     el = (time.perf_counter() - t0) / iters
     return {"gib_s": round(cfg["payload_bytes"] / el / 2**30, 2), "ms_per_batch": round(el * 1e3, 2),
-            "chunks": len(pieces), "streams": P, "parity_ok": ok,
+            "chunks": len(pieces), "streams": P, "copy_streams_per_direction": copy_streams if dir_streams else 0,
+            "parity_ok": ok,
             "note": "pinned host wire -> H2D -> decode -> D2H wire+records, pieces alternating over streams"
                     + (" (one stream per copy direction, events between them)" if dir_streams else " (each piece's copies on its decode stream)")}
 
@@ -979,7 +1001,8 @@ def host_inclusive_zero_copy(torch, codecs, streams, cfg, K, chunks=16, iters=3)
         torch.cuda.synchronize()
         el = (time.perf_counter() - t0) / iters
         return {"gib_s": round(cfg["payload_bytes"] / el / 2**30, 2), "ms_per_batch": round(el * 1e3, 2),
-                "chunks": len(pieces), "streams": P, "parity_ok": ok,
+                "chunks": len(pieces), "streams": P, "copy_streams_per_direction": copy_streams if dir_streams else 0,
+            "parity_ok": ok,
                 "note": "pinned host wire -> H2D (copy engine) -> walk -> COMPACT unmask writing the messages "
                         "into a pinned host arena over PCIe (+ records D2H), pieces alternating over streams"}
     finally:

@@ -331,6 +331,8 @@ int wsc_create(int device, const wsc_config* cfg_in, wsc_ctx** out) {
         chk(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
     }
     if (const char* e = std::getenv("WSC_UNMASK_BUF"); e && *e) c->unmask_buf = std::atoi(e);
+    if (const char* e = std::getenv("WSC_UNMASK_WPC"); e && *e)   // A/B: persistent unmask grid, waves per CU
+        c->cfg.unmask_waves_per_cu = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("WSC_U8_CHAINS"); e && *e) c->u8_chains = std::atoi(e);
     if (const char* e = std::getenv("WSC_U8_GRID"); e && *e) c->u8_grid = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("WSC_U8_WPB"); e && *e) c->u8_wpb = std::atoi(e) == 16 ? 16u : 4u;

@@ -370,8 +370,8 @@ __device__ __forceinline__ void u8_check_run(const U8Args& a, U8Lds& T, uint4 (*
             // load overlaps the fold.
             const uint32_t r = lane >> 4;
             const U8Item xr = a.items[i0 + (r < cnt ? r : 0u)];
-            const uint32_t rlen = r == 0 ? xc.len[0] : r == 1 ? xc.len[1] : r == 2 ? xc.len[2] : xc.len[3];
-            const uint32_t rmask = r == 0 ? xc.mask[0] : r == 1 ? xc.mask[1] : r == 2 ? xc.mask[2] : xc.mask[3];
+            const uint32_t rlen = r < cnt ? xr.len : 0u;   // (row r's fields from its item: no selects)
+            const uint32_t rmask = xr.mask;
             u8_restage(sw, qc, lane);
             const uint32_t off = (lane & 15) * 64;
             bool plain;
