@@ -348,7 +348,9 @@ def main():
         out["configs3_dealt"] = config3_dealt(a, torch, dist, K, synth, world, rank, dev, cdev)
     if solo and not a.no_host_inclusive:
         out["host_inclusive"] = host_inclusive(codec, cfg, K)
-        out["host_inclusive_pipelined"] = host_inclusive_pipelined(torch, codecs, streams, cfg, K, dir_streams=True)
+        # one copy stream per direction and three piece-sized contexts: 42.3 GiB/s on both runs of
+        # profiles/r05/ab4_hi_*.log (2 contexts: 33.9-43.4; more copy streams per direction: slower)
+        out["host_inclusive_pipelined"] = host_inclusive_pipelined(torch, codecs, streams, cfg, K, dir_streams=True, nbuf=3)
         out["host_inclusive_zero_copy"] = host_inclusive_zero_copy(torch, codecs, streams, cfg, K)
     for c in codecs:
         c.close()

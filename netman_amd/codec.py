@@ -38,6 +38,7 @@ FF_UNMASKED, FF_CONT_MSG, FF_CTRL_ARENA, FF_HEAD_PREV = 0x01, 0x02, 0x40, 0x80
 
 SEG_OPEN, SEG_CLOSED, SEG_ERROR, SEG_STALLED = 0, 1, 2, 3
 F_COMPACT = 0x1
+SESSION_BLOCKING_WAIT = 0x100   # wsc_session_create: complete() sleeps on a blocking-sync event
 
 EV_NONE, EV_MESSAGE, EV_PONG, EV_CLOSE, EV_STALL = 0, 1, 2, 3, 4
 
@@ -472,11 +473,11 @@ class Event:
 class Session:
     """Many connections decoded in batches on one device (wsc_session_*)."""
 
-    def __init__(self, device: int = 0, compact: bool = False, **cfg_over):
+    def __init__(self, device: int = 0, compact: bool = False, flags: int = 0, **cfg_over):
         self.lib = load_library()
         self.cfg = default_config(**cfg_over)
         h = C.c_void_p()
-        _check(self.lib.wsc_session_create(device, C.byref(self.cfg), F_COMPACT if compact else 0,
+        _check(self.lib.wsc_session_create(device, C.byref(self.cfg), (F_COMPACT if compact else 0) | flags,
                                            C.byref(h)), "wsc_session_create")
         self.h = h
 

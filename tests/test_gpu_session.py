@@ -234,3 +234,31 @@ def test_submit_complete_double_buffered(codec_lib):
     for i, (c, s) in enumerate(zip(conns, streams)):
         assert got[c] == _oracle_keys(s), f"stream {i}"
     sess.close()
+
+
+@pytest.mark.parametrize("blocking", [False, True])
+def test_ready_poll_then_complete(codec_lib, blocking):
+    """wsc_session_ready (the batching thread's poll: it holds the session lock only for calls that
+    do not wait): ready before any submit, not ready while a large batch is on the device (at least
+    once, polled right after submit), ready afterwards; complete() then returns the oracle's
+    events.  Same with WSC_SESSION_BLOCKING_WAIT (complete sleeps on a blocking-sync event)."""
+    import time
+    sess = K.Session(0, max_batch_bytes=256 << 20, max_segs=256, max_frames=1 << 15,
+                     flags=K.SESSION_BLOCKING_WAIT if blocking else 0)
+    assert sess.ready()
+    rng = np.random.default_rng(3)
+    streams = [synth.frame(2, rng.bytes(1 << 20), mask=int(rng.integers(1, 1 << 32))) * 100 for _ in range(2)]
+    conns = [sess.open() for _ in streams]
+    for c, s in zip(conns, streams):
+        sess.feed(c, s)
+    sess.submit()
+    polls, t0 = 0, time.time()
+    while not sess.ready():
+        polls += 1
+        assert time.time() - t0 < 30
+    assert polls > 0          # 200 MiB of H2D alone takes milliseconds
+    sess.complete()
+    for c, s in zip(conns, streams):
+        assert events_of_session(sess, c) == _oracle_keys(s)
+    assert sess.ready()
+    sess.close()
