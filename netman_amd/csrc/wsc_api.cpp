@@ -106,6 +106,7 @@ struct wsc_ctx {
     bool walk_tiled = true;             // WSC_WALK_TILED=0: the three-launch walk for mode 3 (A/B)
     int hdr_nt = -1;                    // WSC_HDR_NT: the walk's header loads non-temporal: 0 never, 1 always, default COMPACT batches
     bool walk_hw_order = false;         // WSC_WALK_HW_ORDER=1: walk blocks ordered by workgroup index, not a ticket
+    bool enc_buf = false;               // WSC_ENC_BUF=1: the encode copy's stores as buffer stores (sc0 nt sc1)
     bool walk_prio = true;              // WSC_WALK_PRIO=0: the walk's waves keep the default issue priority
     bool quad_pre = true;               // WSC_QUAD_PRE=0: the fused walk without its quad pre-pass (A/B)
     uint32_t xcd_run = 8;               // WSC_XCD_RUN: unmask blocks per XCD run (1 = the hardware deal; one run
@@ -342,6 +343,7 @@ int wsc_create(int device, const wsc_config* cfg_in, wsc_ctx** out) {
     if (const char* e = std::getenv("WSC_WALK_HW_ORDER"); e && *e) c->walk_hw_order = e[0] == '1';
     if (const char* e = std::getenv("WSC_HDR_NT"); e && *e) c->hdr_nt = e[0] == '1' ? 1 : 0;
     if (const char* e = std::getenv("WSC_WALK_PRIO"); e && *e) c->walk_prio = e[0] == '1';
+    if (const char* e = std::getenv("WSC_ENC_BUF"); e && *e) c->enc_buf = e[0] == '1';
     if (const char* e = std::getenv("WSC_XCD_RUN"); e && *e) c->xcd_run = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("WSC_ENC_XCD_RUN"); e && *e) c->enc_xcd_run = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("WSC_WALK_MODE"); e && *e) {   // pin a walk geometry (tests, A/B): 16, 32, 64, 65, 66, 256, 257 or 3
@@ -849,7 +851,8 @@ static int launch_encode(wsc_ctx* c, const wsc_out_msg* msgs, uint32_t n, const 
     if (wins > c->enc_tile_entries) wins = c->enc_tile_entries;
     if (wins == 0) wins = 1;
     const dim3 cgrid((uint32_t)((wins + 3) / 4));
-    if ((c->cfg.unmask_nt & 3) == 3) hipLaunchKernelGGL(k_encode_copy<3>, cgrid, dim3(256), 0, st, ca);
+    if ((c->cfg.unmask_nt & 3) == 3 && c->enc_buf) hipLaunchKernelGGL(k_encode_copy<17>, cgrid, dim3(256), 0, st, ca);
+    else if ((c->cfg.unmask_nt & 3) == 3) hipLaunchKernelGGL(k_encode_copy<3>, cgrid, dim3(256), 0, st, ca);
     else hipLaunchKernelGGL(k_encode_copy<0>, cgrid, dim3(256), 0, st, ca);
     HIP_TRY(hipGetLastError());
     return WSC_OK;

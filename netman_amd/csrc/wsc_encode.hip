@@ -45,6 +45,14 @@ __device__ __forceinline__ uint4 enc_place(const uint32_t (&h)[4], int32_t d) {
     return make_uint4(o.x, o.y, o.z, o.w);
 }
 
+// An aligned 16-byte output store.  NT bit 4: a buffer store over the output window with the
+// in-place unmask's streaming policy (sc0 nt sc1) instead of a 64-bit global store.
+template <int NT>
+__device__ __forceinline__ void enc_st(uint8_t* out, uint64_t wbase, uint64_t pa, u32x4 v) {
+    if constexpr ((NT & 16) != 0) st16b<19>(win_rsrc(out + wbase, ENC_WIN), (uint32_t)(pa - wbase), v);
+    else st16v<NT>(out + pa, v);
+}
+
 __device__ __forceinline__ uint4 and4(const uint4& v, const uint32_t (&m)[4]) {
     return make_uint4(v.x & m[0], v.y & m[1], v.z & m[2], v.w & m[3]);
 }
@@ -225,7 +233,7 @@ __device__ __forceinline__ bool encode_window_lanes(const EncCopyArgs& a, uint32
     };
     auto store_piece = [&](uint64_t pa, const uint4& v) {
         if (pa + 16 <= limit) {
-            st16v<NT>(a.out + pa, u32x4{v.x, v.y, v.z, v.w});
+            enc_st<NT>(a.out, wbase, pa, u32x4{v.x, v.y, v.z, v.w});
         } else {   // the tail piece: never write at or past the total / out_cap
             const uint32_t d[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -246,7 +254,7 @@ __device__ __forceinline__ bool encode_window_lanes(const EncCopyArgs& a, uint32
         if (inside) {
             const int64_t sof = (int64_t)((uint64_t)sh << 32 | sl) + (int64_t)pa;
             const uint4 v = load16_unaligned(a.src, sof, a.src_bytes);
-            st16v<NT>(a.out + pa, u32x4{v.x, v.y, v.z, v.w});
+            enc_st<NT>(a.out, wbase, pa, u32x4{v.x, v.y, v.z, v.w});
         }
         const bool edge = !inside && pa < limit;
         const uint64_t em = __ballot(edge);
@@ -351,7 +359,7 @@ __global__ __launch_bounds__(256) void k_encode_copy(EncCopyArgs a) {
 #pragma unroll
         for (uint32_t k = 0; k < P; ++k) v[k] = load16u<NT>(a.src, so + (int64_t)(wbase + k * 1024u + lofs), a.src_bytes);
 #pragma unroll
-        for (uint32_t k = 0; k < P; ++k) st16v<NT>(a.out + wbase + k * 1024u + lofs, u32x4{v[k].x, v[k].y, v[k].z, v[k].w});
+        for (uint32_t k = 0; k < P; ++k) enc_st<NT>(a.out, wbase, wbase + k * 1024u + lofs, u32x4{v[k].x, v[k].y, v[k].z, v[k].w});
         return;
     }
     // general path: frame edges in the window -> lane-parallel frame lookup (serial walk over the
@@ -398,7 +406,7 @@ __global__ __launch_bounds__(256) void k_encode_copy(EncCopyArgs a) {
         const uint64_t pa = wbase + k * 1024u + lofs;
         if (pa >= limit) continue;
         if (pa + 16 <= limit) {
-            st16v<NT>(a.out + pa, u32x4{acc[k].x, acc[k].y, acc[k].z, acc[k].w});
+            enc_st<NT>(a.out, wbase, pa, u32x4{acc[k].x, acc[k].y, acc[k].z, acc[k].w});
         } else {   // the tail piece: never write at or past the total / out_cap
             const uint32_t d[4] = {acc[k].x, acc[k].y, acc[k].z, acc[k].w};
 #pragma unroll
@@ -410,5 +418,6 @@ __global__ __launch_bounds__(256) void k_encode_copy(EncCopyArgs a) {
 
 template __global__ void k_encode_copy<0>(EncCopyArgs);
 template __global__ void k_encode_copy<3>(EncCopyArgs);
+template __global__ void k_encode_copy<17>(EncCopyArgs);
 
 }  // namespace wsc
