@@ -498,6 +498,44 @@ static inline __device__ __attribute__((noinline)) void fold_staged4(U8Win u8w, 
     fold_staged<4>(nullptr, 0u, u8w, win, lane);
 }
 
+// A COMPACT window inside one span: its 4 KiB go to the arena at d0 (= arena offset of window byte
+// 0), which is 16-byte aligned only when the span's arena and wire offsets agree mod 16.  With
+// WSC_COMPACT_ALIGNED the wave stores aligned 16-byte chunks instead of byte-aligned ones: lane l's
+// chunk of slice k holds the last m bytes of the previous piece (lane l - 1, or lane 63 of slice
+// k - 1: a lane shuffle) and the first 16 - m of its own (m = d0 & 15); the window's first
+// 16 - m bytes and its last m bytes are byte runs (store_run).  Every arena byte is written once.
+#ifndef WSC_COMPACT_ALIGNED
+#define WSC_COMPACT_ALIGNED 0
+#endif
+template <int NT>
+__device__ __forceinline__ void compact_window_aligned(uint8_t* d0, const u32x4 (&v)[4], uint32_t key, uint32_t lane) {
+    const uint32_t m = (uint32_t)(reinterpret_cast<uintptr_t>(d0) & 15);
+    if (m == 0) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) st16v<NT>(d0 + 1024u * k + 16u * lane, v[k] ^ key);
+        return;
+    }
+    u32x4 x[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) x[k] = v[k] ^ key;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        u32x4 p;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t up = (uint32_t)__shfl_up((int)x[k][j], 1);
+            const uint32_t wrap = k ? (uint32_t)__builtin_amdgcn_readlane((int)x[k ? k - 1 : 0][j], 63) : 0u;
+            p[j] = lane == 0 ? wrap : up;
+        }
+        if (k == 0 && lane == 0) {
+            store_run<NT>(d0, x[0], 0u, 16u - m);   // the window's first bytes, up to the first boundary
+        } else {
+            st16v<NT>(d0 + 1024u * k + 16u * lane - m, funnel16(p, x[k], 16u - m));
+        }
+    }
+    if (lane == 63) store_run<NT>(d0 + 4096u - m, x[3], 16u - m, 16u);   // its last m bytes
+}
+
 // NT bit 0: non-temporal loads, bit 1: non-temporal stores.  In place `src` is unused (dst is
 // both source and destination) so the two restrict pointers never alias in an access; COMPACT
 // reads `src` (the wire) and writes `dst` (the arena).  `total` = wire bytes.
@@ -562,7 +600,9 @@ __device__ __forceinline__ void unmask_all(uint8_t* __restrict__ dst, const uint
         if (r >= n_spans) s0.src = ~0ull;   // no span starts before the window's end
         if (s0.src <= wbase && s0.src + s0.len >= wbase + WB) {
             // fast path: one span covers the whole window -> one rotated key for every dword
-            if constexpr (COMPACT) {
+            if constexpr (COMPACT && WSC_COMPACT_ALIGNED && P == 4) {
+                compact_window_aligned<NT>(dst + (s0.dst - s0.src) + wbase, v, s0.key, lane);
+            } else if constexpr (COMPACT) {
                 uint8_t* d = dst + (s0.dst - s0.src) + wbase + lofs;
 #pragma unroll
                 for (int k = 0; k < P; ++k) st16u<NT>(d + k * 1024u, v[k] ^ s0.key);
