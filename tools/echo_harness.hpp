@@ -262,7 +262,10 @@ inline Result run(const DecoderFactory& make_decoder, int pollers, int conns, in
         std::vector<ServerConn> sc;
         uint64_t served = 0, payload = 0, rounds = 0;
         std::string error;
+        double t[6] = {0, 0, 0, 0, 0, 0};   // ECHO_TIMING=1: epoll_wait, reads, decode/submit, echo, complete, sends
     };
+    const bool timing = [] { const char* e = std::getenv("ECHO_TIMING"); return e && e[0] == '1'; }();
+    auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
     if (pollers < 1) pollers = 1;
     if (pollers > conns) pollers = conns;
     std::vector<Poller> pl(pollers);
@@ -335,7 +338,15 @@ inline Result run(const DecoderFactory& make_decoder, int pollers, int conns, in
                 P.error = "server timeout";
                 break;
             }
+            double tm = timing ? now() : 0;
+            auto lap = [&](int i) {
+                if (!timing) return;
+                const double t2 = now();
+                P.t[i] += t2 - tm;
+                tm = t2;
+            };
             const int n = epoll_wait(P.ep, evs, 1024, pipe && !drain.empty() ? 0 : 100);
+            lap(0);
             fed.clear();
             for (int k = 0; k < n; ++k) {
                 const size_t q = evs[k].data.u64;
@@ -369,23 +380,29 @@ inline Result run(const DecoderFactory& make_decoder, int pollers, int conns, in
             // pipelined decoders pipeline only rounds of several connections: a round of one
             // connection waits for its own batch either way, and the synchronous call saves the
             // second staging set's hand-off
+            lap(1);
             const bool pipe_round = pipe && fed.size() > 1;
             if (pipe_round) {
                 if (!fed.empty() || dec.pending()) {
                     dec.submit();          // round r+1 on the device ...
                     P.rounds++;
                 }
+                lap(2);
                 echo_round(drain);         // ... while round r is echoed
+                lap(3);
                 dec.complete();
+                lap(4);
                 drain = fed;
             } else {
                 if (!fed.empty() || dec.pending()) {
                     dec.decode();          // (an earlier pipelined batch completes first)
                     P.rounds++;
                 }
+                lap(2);
                 echo_round(drain);
                 drain.clear();
                 echo_round(fed);
+                lap(3);
             }
             if (!eofs.empty()) {
                 echo_round(eofs);
@@ -424,7 +441,11 @@ inline Result run(const DecoderFactory& make_decoder, int pollers, int conns, in
                     c.want_out = need;
                 }
             }
+            lap(5);
         }
+        if (timing)
+            fprintf(stderr, "poller: %llu rounds; s in epoll_wait %.4f, reads %.4f, decode/submit %.4f, echo %.4f, complete %.4f, sends %.4f\n",
+                    (unsigned long long)P.rounds, P.t[0], P.t[1], P.t[2], P.t[3], P.t[4], P.t[5]);
         // flush what is left (the clients check every echo)
         for (auto& c : sc) {
             while (!c.closed && c.out_pos < c.out.size() && client_fail.load() == 0 && P.error.empty()) {

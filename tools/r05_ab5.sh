@@ -14,4 +14,7 @@ for rep in 1 2; do
   step c4_default_$rep 200 python3 tools/cfg_bench.py "configs[4]"
   step c4_aligned_$rep 200 env WSC_LIB=$PWD/tools/_var/libwscodec_ca.so python3 tools/cfg_bench.py "configs[4]"
 done
+step echo_timing_gpu 120 env ECHO_TIMING=1 WSC_SESSION_TIMING=1 tools/ws_echo --conns 64 --frames 200 --size 65536 --client-threads 4 --pollers 8
+step echo_timing_cpu 120 env ECHO_TIMING=1 oracle/_build/ws_echo_cpu --conns 64 --frames 200 --size 65536 --client-threads 4 --pollers 8
+step echo_timing_gpu4 120 env ECHO_TIMING=1 WSC_SESSION_TIMING=1 tools/ws_echo --conns 64 --frames 200 --size 65536 --client-threads 4 --pollers 4
 echo done
