@@ -100,6 +100,7 @@ struct Stage {                    // one staging set: pinned host buffers, devic
     hipStream_t stream = nullptr;
     hipEvent_t ev = nullptr;      // WSC_SESSION_BLOCKING_WAIT: a blocking-sync event complete() sleeps on
     hipEvent_t done_ev = nullptr; // recorded after the launch's last operation: wsc_session_ready
+    uint32_t frames_pre = 0;      // frame records already copied back with the launch (launch_stage)
     uint8_t* h_wire = nullptr;    // masked bytes as read (input)
     uint8_t* h_res = nullptr;     // results: unmasked wire (in place) or the arena (COMPACT)
     uint64_t* h_seg_off = nullptr;
@@ -172,6 +173,7 @@ struct wsc_session {
     // streamed payload bytes collected into messages
     uint64_t st_read = 0, st_h2d = 0, st_resent = 0, st_batches = 0, st_pieces = 0;
     uint64_t max_message = 0;     // wsc_session_set_max_message: 0 = no cap (the reference has none, Q4)
+    uint32_t frames_hint = 0;     // records of the last batch (+1/8): how many the next launch copies back up front
 };
 
 namespace {
@@ -502,6 +504,13 @@ int launch_stage(wsc_session* s, Stage& g) {
     // the launch instead of after complete()'s first wait, so it overlaps the host's work on the
     // previous round (views into h_res of this set were materialised by the complete() before)
     if (!compact) HT(hipMemcpyAsync(g.h_res, g.d_wire, g.bytes, hipMemcpyDeviceToHost, st));
+    // ... and, in place, as many frame records as the last batch had (+1/8): when this batch has no
+    // more, complete() needs no second copy and no second wait (the records cost 32 B each)
+    g.frames_pre = 0;
+    if (!compact && s->frames_hint) {
+        g.frames_pre = s->frames_hint < s->cfg.max_frames ? s->frames_hint : s->cfg.max_frames;
+        HT(hipMemcpyAsync(g.h_frames, g.d_frames, (uint64_t)g.frames_pre * sizeof(wsc_frame), hipMemcpyDeviceToHost, st));
+    }
     HT(hipEventRecord(g.done_ev, st));
 #undef HT
     return WSC_OK;
@@ -818,13 +827,15 @@ int wsc_session_complete(wsc_session* s) {
         auto D2H = [&](void* dst, const void* src, uint64_t bytes, const char* w) {
             if (e == hipSuccess && bytes && (e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st)) != hipSuccess) what = w;
         };
-        D2H(g.h_frames, g.d_frames, (uint64_t)nf * sizeof(wsc_frame), "hipMemcpyAsync frames");
+        const uint32_t pre = nf < g.frames_pre ? nf : g.frames_pre;   // (copied with the launch)
+        D2H(g.h_frames + pre, (const wsc_frame*)g.d_frames + pre, (uint64_t)(nf - pre) * sizeof(wsc_frame), "hipMemcpyAsync frames");
         if (compact) {
             D2H(g.h_res, g.d_arena, g.h_summary->data_bytes + g.h_summary->ctrl_bytes, "hipMemcpyAsync arena");
             D2H(g.h_frame_dst, g.d_frame_dst, (uint64_t)nf * sizeof(uint64_t), "hipMemcpyAsync frame_dst");
         }   // (in place the wire came back with the launch: launch_stage)
-        if (e == hipSuccess && (e = stage_wait(s, g)) != hipSuccess) what = "hipStreamSynchronize";
+        if (e == hipSuccess && (compact || nf > pre) && (e = stage_wait(s, g)) != hipSuccess) what = "hipStreamSynchronize";
         if (e != hipSuccess) rc = hip_fail(what, e);
+        s->frames_hint = nf + nf / 8;
     }
     const double t1 = s->timing ? now_s() : 0;
     materialize_views(s, set ^ 1);   // the other set is filled next: its views must not dangle
