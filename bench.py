@@ -1003,8 +1003,7 @@ def host_inclusive_zero_copy(torch, codecs, streams, cfg, K, chunks=16, iters=3)
         torch.cuda.synchronize()
         el = (time.perf_counter() - t0) / iters
         return {"gib_s": round(cfg["payload_bytes"] / el / 2**30, 2), "ms_per_batch": round(el * 1e3, 2),
-                "chunks": len(pieces), "streams": P, "copy_streams_per_direction": copy_streams if dir_streams else 0,
-            "parity_ok": ok,
+                "chunks": len(pieces), "streams": P, "parity_ok": ok,
                 "note": "pinned host wire -> H2D (copy engine) -> walk -> COMPACT unmask writing the messages "
                         "into a pinned host arena over PCIe (+ records D2H), pieces alternating over streams"}
     finally:
