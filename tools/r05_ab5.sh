@@ -17,4 +17,9 @@ done
 step echo_timing_gpu 120 env ECHO_TIMING=1 WSC_SESSION_TIMING=1 tools/ws_echo --conns 64 --frames 200 --size 65536 --client-threads 4 --pollers 8
 step echo_timing_cpu 120 env ECHO_TIMING=1 oracle/_build/ws_echo_cpu --conns 64 --frames 200 --size 65536 --client-threads 4 --pollers 8
 step echo_timing_gpu4 120 env ECHO_TIMING=1 WSC_SESSION_TIMING=1 tools/ws_echo --conns 64 --frames 200 --size 65536 --client-threads 4 --pollers 4
+for rep in 1 2; do
+  step text_base_$rep 200 python3 tools/cfg_bench.py TEXT
+  step text_cls_$rep 200 env WSC_LIB=$PWD/tools/_var/libwscodec_cls.so python3 tools/cfg_bench.py TEXT
+done
+step n2_rehearsal 300 env WSC_BENCH_BACKEND=gloo python3 bench.py --gpus 2 --steps 20 --warmup 3 --no-cpu --no-host-inclusive --no-echo --no-other-configs
 echo done
