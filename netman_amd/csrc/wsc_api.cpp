@@ -24,7 +24,7 @@ template <uint32_t NCH, uint32_t WPB> __global__ void k_u8_check(U8Args);
 template <bool COMPACT, int P, int NT, int MINW, bool U8>
 __global__ void k_unmask(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*,
                          const wsc_summary*, uint32_t*, uint32_t, uint32_t*, uint32_t*, uint32_t, U8Win);
-__global__ void k_encode_scan(EncArgs);
+template <uint32_t IPT> __global__ void k_encode_scan(EncArgs);
 template <int NT> __global__ void k_encode_copy(EncCopyArgs);
 }  // namespace wsc
 
@@ -106,6 +106,7 @@ struct wsc_ctx {
     bool walk_tiled = true;             // WSC_WALK_TILED=0: the three-launch walk for mode 3 (A/B)
     int hdr_nt = -1;                    // WSC_HDR_NT: the walk's header loads non-temporal: 0 never, 1 always, default COMPACT batches
     bool walk_hw_order = false;         // WSC_WALK_HW_ORDER=1: walk blocks ordered by workgroup index, not a ticket
+    uint32_t enc_ipt = 0;               // WSC_ENC_IPT=1|4|16: pin the encode scan's messages per thread (A/B)
     bool enc_buf = false;               // WSC_ENC_BUF=1: the encode copy's stores as buffer stores (sc0 nt sc1)
     bool walk_prio = true;              // WSC_WALK_PRIO=0: the walk's waves keep the default issue priority
     bool quad_pre = true;               // WSC_QUAD_PRE=0: the fused walk without its quad pre-pass (A/B)
@@ -344,6 +345,7 @@ int wsc_create(int device, const wsc_config* cfg_in, wsc_ctx** out) {
     if (const char* e = std::getenv("WSC_HDR_NT"); e && *e) c->hdr_nt = e[0] == '1' ? 1 : 0;
     if (const char* e = std::getenv("WSC_WALK_PRIO"); e && *e) c->walk_prio = e[0] == '1';
     if (const char* e = std::getenv("WSC_ENC_BUF"); e && *e) c->enc_buf = e[0] == '1';
+    if (const char* e = std::getenv("WSC_ENC_IPT"); e && *e) c->enc_ipt = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("WSC_XCD_RUN"); e && *e) c->xcd_run = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("WSC_ENC_XCD_RUN"); e && *e) c->enc_xcd_run = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("WSC_WALK_MODE"); e && *e) {   // pin a walk geometry (tests, A/B): 16, 32, 64, 65, 66, 256, 257 or 3
@@ -808,6 +810,15 @@ int wsc_error_flags(wsc_ctx* c, uint32_t* flags, int clear) {
 }
 
 // ---- encode ---------------------------------------------------------------------------------
+// messages per scan thread: the smallest of 1 / 4 / ENC_IPT that keeps the scan within 256 blocks
+// (one per CU); `forced` (WSC_ENC_IPT, A/B only) pins one
+static uint32_t enc_scan_ipt(uint32_t n, uint32_t forced) {
+    if (forced == 1 || forced == 4 || forced == ENC_IPT) return forced;
+    if (n <= 256u * 256u) return 1;
+    if (n <= 256u * 256u * 4u) return 4;
+    return ENC_IPT;
+}
+
 static int launch_encode(wsc_ctx* c, const wsc_out_msg* msgs, uint32_t n, const uint8_t* src, uint64_t src_bytes,
                          uint8_t* out, uint64_t out_cap, uint64_t* out_off, hipStream_t st) {
     if (!msgs || !out || !out_off || (!src && src_bytes)) return fail(WSC_E_INVAL, "NULL encode pointer");
@@ -831,8 +842,11 @@ static int launch_encode(wsc_ctx* c, const wsc_out_msg* msgs, uint32_t n, const 
     ea.lb_agg = c->enc_lb_agg;
     ea.lb_incl = c->enc_lb_incl;
     ea.sticky = c->sticky;
-    const uint32_t sblocks = (n + 256 * ENC_IPT - 1) / (256 * ENC_IPT);
-    hipLaunchKernelGGL(k_encode_scan, dim3(sblocks), dim3(256), 0, st, ea);
+    const uint32_t ipt = enc_scan_ipt(n, c->enc_ipt);
+    const uint32_t sblocks = (n + 256 * ipt - 1) / (256 * ipt);
+    if (ipt == 1) hipLaunchKernelGGL(k_encode_scan<1>, dim3(sblocks), dim3(256), 0, st, ea);
+    else if (ipt == 4) hipLaunchKernelGGL(k_encode_scan<4>, dim3(sblocks), dim3(256), 0, st, ea);
+    else hipLaunchKernelGGL(k_encode_scan<16>, dim3(sblocks), dim3(256), 0, st, ea);
     HIP_TRY(hipGetLastError());
     EncCopyArgs ca{};
     ca.msgs = msgs;

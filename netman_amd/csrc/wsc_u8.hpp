@@ -50,33 +50,10 @@ __device__ __forceinline__ uint32_t u8m_get(uint64_t m, uint32_t st) {   // st: 
 
 // LDS tables of one workgroup: tab[byte] = the map of that single byte; tab8[state][byte] = the
 // next state (8 = reject); stage = one 4 KiB restage buffer per wave (64 chunks padded to 80 B).
-// WSC_U8_CLASS (A/B): the chain step through byte classes instead of tab8 -- cls[byte] (12
-// classes, off the chain) then t2[state << 4 | class] (9 x 16 entries): both tables are at most
-// 256 B, one dword per LDS bank, so neither read can conflict (tab8's 2,304 B put 9 dwords in
-// every bank: 39-49 % of the check's LDS cycles conflicted, profiles/r04_pmc_text_sq.json).
-#ifndef WSC_U8_CLASS
-#define WSC_U8_CLASS 0
-#endif
 struct U8Lds {
     uint64_t tab[256];
     uint8_t tab8[9 * 256];
-    uint8_t cls[256];
-    uint8_t t2[9 * 16];
 };
-__host__ __device__ __forceinline__ uint32_t u8_class(uint32_t b) {
-    if (b < 0x80) return 0;
-    if (b < 0x90) return 1;
-    if (b < 0xA0) return 2;
-    if (b < 0xC0) return 3;
-    if (b < 0xC2 || b > 0xF4) return 4;
-    if (b < 0xE0) return 5;
-    if (b == 0xE0) return 6;
-    if (b == 0xED) return 8;
-    if (b < 0xF0) return 7;
-    if (b == 0xF0) return 9;
-    if (b < 0xF4) return 10;
-    return 11;   // 0xF4
-}
 constexpr uint32_t U8_STAGE = 64 * 5;   // uint4 per wave
 // every thread of a 256-thread workgroup fills its byte's entries (caller syncs)
 __device__ __forceinline__ void u8_tables_init(U8Lds& t, uint32_t byte) {
@@ -88,12 +65,6 @@ __device__ __forceinline__ void u8_tables_init(U8Lds& t, uint32_t byte) {
     }
     t.tab8[8 * 256 + byte] = 8;
     t.tab[byte] = m;
-    t.cls[byte] = (uint8_t)u8_class(byte);
-    if (byte < 9 * 16) {   // t2[state][class]: a representative byte of each class
-        constexpr uint8_t rep[16] = {0x41, 0x80, 0x90, 0xA0, 0xC0, 0xC2, 0xE0, 0xE1, 0xED, 0xF0, 0xF1, 0xF4, 0xFF, 0xFF, 0xFF, 0xFF};
-        const uint32_t st = byte >> 4, cl = byte & 15;
-        t.t2[byte] = (uint8_t)(st >= 8 ? 8u : u8_step(st, rep[cl]));
-    }
 }
 
 // one level of the in-row composition: lanes that are multiples of 2*DD take "own map, then the map
@@ -247,12 +218,7 @@ __device__ __forceinline__ uint64_t u8_chunk_map(const U8Lds& t, const V (&v)[4]
         for (uint32_t i = 0; i < 4; ++i) {
 #pragma unroll
             for (uint32_t c = 0; c < NCH; ++c) {
-#if WSC_U8_CLASS
-                const uint32_t cl = t.cls[(dw(c * CW + j) >> (8 * i)) & 0xFFu];   // independent of the state
-                const uint32_t ns = t.t2[st[c] << 4 | cl];
-#else
                 const uint32_t ns = t.tab8[__builtin_amdgcn_perm(st[c], dw(c * CW + j), i | 4u << 8 | 0x0Cu << 16 | 0x0Cu << 24)];
-#endif
                 st[c] = (!part || c * CB + 4 * j + i < nk) ? ns : st[c];
             }
         }

@@ -121,6 +121,20 @@ def test_gpu_encode_many_tiny_frames_per_window(codec):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n", [65536, 65537, 262144, 262145, 300000])
+def test_gpu_encode_scan_widths(codec_lib, n):
+    """the scan's messages per thread change with the batch (1 up to 64 Ki messages, 4 up to
+    256 Ki, 16 beyond: wsc_api.cpp enc_scan_ipt); each width, at its boundaries, equals the oracle"""
+    from netman_amd import codec as K
+    c = K.Codec(0, max_batch_bytes=64 << 20, max_segs=1024, max_frames=1 << 19)
+    try:
+        msgs, src = _batch(11 + n, n, [0, 3, 40, 125, 126, 300], src_bytes=1 << 16)
+        _check(c, msgs, src)
+    finally:
+        c.close()
+
+
+@pytest.mark.gpu
 def test_gpu_encode_large_frames(codec):
     msgs, src = _batch(8, 24, [1 << 20, (1 << 20) + 3, 3 * 65536 + 7, 131], src_bytes=8 << 20)
     _check(codec, msgs, src)

@@ -300,7 +300,9 @@ inline Result run(const DecoderFactory& make_decoder, int pollers, int conns, in
     auto poller_loop = [&](Poller& P) {
         Decoder& dec = *P.dec;
         std::vector<ServerConn>& sc = P.sc;
-        std::vector<uint8_t> rb(4 << 20);
+        // bytes one read(2) may take per connection and round (both servers): ECHO_READ_BYTES, 4 MiB
+        const size_t rb_bytes = [] { const char* e = std::getenv("ECHO_READ_BYTES"); return e && *e ? (size_t)atoll(e) : (size_t)4 << 20; }();
+        std::vector<uint8_t> rb(rb_bytes < 4096 ? 4096 : rb_bytes);
         std::vector<size_t> fed;
         epoll_event evs[1024];
         const uint64_t want = (uint64_t)sc.size() * (uint64_t)frames;
