@@ -18,15 +18,6 @@
 
 namespace wsc {
 
-// WSC_ENC_PRELOAD=1: the copy loads the window's frames into lanes with its first one (A/B)
-#ifndef WSC_ENC_PRELOAD
-#define WSC_ENC_PRELOAD 0
-#endif
-
-__device__ __forceinline__ uint64_t rfl64(uint64_t x) {
-    return (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)) << 32 | __builtin_amdgcn_readfirstlane((uint32_t)x);
-}
-
 __device__ __forceinline__ uint32_t enc_hlen(uint64_t len) { return len <= 125 ? 2u : (len <= 65535 ? 4u : 10u); }
 
 // The header of one frame as 16 little-endian bytes (only the first enc_hlen(len) are used).
@@ -80,14 +71,13 @@ __device__ __forceinline__ void piece_mask(uint32_t bl, uint32_t bh, uint32_t (&
 // Scan: frame sizes -> out_off (exclusive), window index.  Same look-back protocol as the
 // decoder's walk (wsc_kernels.hip): ticket block ids, agent-scope payload stores drained with
 // vmcnt(0) before the agent-scope flag store, readers poll with agent-scope atomics, bounded spin.
-// Each wave owns 64 * IPT consecutive messages and takes them 64 at a time (message base + 64 r +
-// lane in round r): descriptor loads, out_off stores and the window-index stores of consecutive
-// lanes land on consecutive addresses, and a round's exclusive offsets come from one wave scan
-// plus the running carry.  Round 4 gave each thread IPT consecutive messages instead (1 M
-// messages in 256 blocks at IPT 16: 68 -> 24 us), whose lanes were 384 B apart in every load and
-// store.  The host picks the smallest IPT that keeps the grid within 256 blocks (enc_scan_ipt):
-// with few, large messages the stores of the window index (16 per 64 KiB message) are the
-// scan's work, so 16 Ki messages run at IPT 1 on 64 CUs instead of on 4.
+// IPT consecutive messages per thread: 1 M messages in 256 blocks instead of 4,096 -- the scan
+// went 68 -> 24 us at IPT 16 (8 per thread: 28 us, 32: 30 us).  The host picks the smallest IPT
+// that keeps the grid within 256 blocks (wsc_api.cpp enc_scan_ipt): with few, large messages the
+// window-index stores (16 per 64 KiB message) are the scan's work, so 16 Ki messages run at IPT 1
+// on 64 CUs instead of IPT 16 on 4 (64 KiB encode 0.379 -> 0.360 ms, profiles/r05/ab6_enc_*.log;
+// lanes taking messages 64 apart for coalesced loads and stores measured no faster: 1 KiB 0.437
+// -> 0.442 ms).
 // ---------------------------------------------------------------------------------------------
 template <uint32_t IPT>
 __global__ __launch_bounds__(256) void k_encode_scan(EncArgs a) {
@@ -98,28 +88,26 @@ __global__ __launch_bounds__(256) void k_encode_scan(EncArgs a) {
         sh_bid = __hip_atomic_fetch_add(a.lb_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     const uint32_t bid = sh_bid;
+    const uint64_t i0 = ((uint64_t)bid * 256 + threadIdx.x) * IPT;
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint64_t w0 = ((uint64_t)bid * 4 + wave) * 64 * IPT;   // the wave's first message
-    uint64_t sz[IPT], ex[IPT];                                   // size, wave-exclusive offset
-    uint64_t carry = 0;
+    uint64_t sz[IPT];
+    uint64_t tsz = 0;
 #pragma unroll
-    for (uint32_t r = 0; r < IPT; ++r) {
-        const uint64_t i = w0 + 64 * r + lane;
-        sz[r] = 0;
-        if (i < a.n_msgs) {
-            const uint64_t len = a.msgs[i].len;
-            sz[r] = enc_hlen(len) + len;
+    for (uint32_t j = 0; j < IPT; ++j) {
+        sz[j] = 0;
+        if (i0 + j < a.n_msgs) {
+            const uint64_t len = a.msgs[i0 + j].len;
+            sz[j] = enc_hlen(len) + len;
         }
-        uint64_t inc = sz[r];
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint64_t o = __shfl_up(inc, d);
-            if (lane >= (uint32_t)d) inc += o;
-        }
-        ex[r] = carry + inc - sz[r];
-        carry += __shfl(inc, 63);
+        tsz += sz[j];
     }
-    if (lane == 0) sh_wave[wave] = carry;
+    uint64_t inc = tsz;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t o = __shfl_up(inc, d);
+        if (lane >= (uint32_t)d) inc += o;
+    }
+    if (lane == 63) sh_wave[wave] = inc;
     __syncthreads();
     uint64_t wpre = 0, btot = 0;
 #pragma unroll
@@ -171,20 +159,20 @@ __global__ __launch_bounds__(256) void k_encode_scan(EncArgs a) {
         }
     }
     __syncthreads();
-    const uint64_t base = sh_prefix + wpre;
+    uint64_t off = sh_prefix + wpre + (inc - tsz);
 #pragma unroll
-    for (uint32_t r = 0; r < IPT; ++r) {
-        const uint64_t i = w0 + 64 * r + lane;
+    for (uint32_t j = 0; j < IPT; ++j) {
+        const uint64_t i = i0 + j;
         if (i >= a.n_msgs) break;
-        const uint64_t off = base + ex[r];
         a.out_off[i] = off;
         // windows that start inside this frame: [ceil(off / W), floor((off + sz - 1) / W)]
         uint64_t w = (off + ENC_WIN - 1) >> ENC_WIN_SHIFT;
-        uint64_t w_end = ((off + sz[r] - 1) >> ENC_WIN_SHIFT) + 1;
+        uint64_t w_end = ((off + sz[j] - 1) >> ENC_WIN_SHIFT) + 1;
         if (w_end > a.tile_entries) w_end = a.tile_entries;
         for (; w < w_end; ++w) a.tile[w] = (uint32_t)i;
+        off += sz[j];
         if (i == a.n_msgs - 1) {
-            uint64_t total = off + sz[r];
+            uint64_t total = off;
             if (__hip_atomic_load(a.lb_err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
                 total = ~0ull;   // invalid
                 __hip_atomic_fetch_or(a.sticky, 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -215,7 +203,7 @@ __device__ __forceinline__ void pm_mask(const u32x4* __restrict__ pm, uint32_t l
 template <int NT>
 __device__ __forceinline__ bool encode_window_lanes(const EncCopyArgs& a, uint32_t m, uint64_t wbase, uint64_t limit,
                                                     uint32_t lane, const u32x4* __restrict__ pm,
-                                                    uint16_t* __restrict__ elist, const wsc_out_msg& ml, uint64_t ol) {
+                                                    uint16_t* __restrict__ elist) {
     constexpr uint32_t P = ENC_WIN / 1024;
     constexpr int64_t WB = ENC_WIN;
     auto clip = [](int64_t x) -> int32_t { return (int32_t)(x < -(1ll << 30) ? -(1ll << 30) : (x > WB + 64 ? WB + 64 : x)); };
@@ -224,13 +212,8 @@ __device__ __forceinline__ bool encode_window_lanes(const EncCopyArgs& a, uint32
     uint32_t h[4] = {0, 0, 0, 0};
     int64_t so = 0;                                    // source offset of output byte x: so + x
     if (fj < a.n_msgs) {
-#if WSC_ENC_PRELOAD
-        const wsc_out_msg& mj = ml;   // loaded by the caller with the window's first frame
-        const uint64_t o = ol;
-#else
         const wsc_out_msg mj = a.msgs[fj];
         const uint64_t o = a.out_off[fj];
-#endif
         const uint64_t p = o + enc_hlen(mj.len);
         ro = clip((int64_t)o - (int64_t)wbase);
         rp = clip((int64_t)p - (int64_t)wbase);
@@ -369,24 +352,8 @@ __global__ __launch_bounds__(256) void k_encode_copy(EncCopyArgs a) {
     if (wbase >= limit || gw >= a.tile_entries) return;
     const uint32_t lofs = lane * 16u;
     uint32_t m = a.tile[gw];
-    wsc_out_msg ml{};
-    uint64_t ol = 0;
-#if WSC_ENC_PRELOAD
-    // frames m + lane loaded at once: the window's first frame decides the fast path (lane 0) and
-    // a general window finds its frames already in lanes -- one dependent round trip fewer
-    if (m + lane < n) {
-        ml = a.msgs[m + lane];
-        ol = a.out_off[m + lane];
-    }
-    wsc_out_msg mm;
-    mm.src_off = rfl64(ml.src_off);
-    mm.len = rfl64(ml.len);
-    mm.first_byte = (uint8_t)__builtin_amdgcn_readfirstlane((uint32_t)ml.first_byte);
-    const uint64_t o = rfl64(ol);
-#else
     const wsc_out_msg mm = a.msgs[m];
     const uint64_t o = a.out_off[m];
-#endif
     const uint64_t p0 = o + enc_hlen(mm.len), p1 = p0 + mm.len;
     if (p0 <= wbase && p1 >= wbase + ENC_WIN && wbase + ENC_WIN <= limit) {
         // fast path: the window lies inside one payload -> shifted stream copy, non-temporal loads
@@ -403,7 +370,7 @@ __global__ __launch_bounds__(256) void k_encode_copy(EncCopyArgs a) {
     }
     // general path: frame edges in the window -> lane-parallel frame lookup (serial walk over the
     // frames only when more than 64 of them overlap the window)
-    if (encode_window_lanes<NT>(a, m, wbase, limit, lane, pm, elist[threadIdx.x >> 6], ml, ol)) return;
+    if (encode_window_lanes<NT>(a, m, wbase, limit, lane, pm, elist[threadIdx.x >> 6])) return;
     uint4 acc[P];
 #pragma unroll
     for (uint32_t k = 0; k < P; ++k) acc[k] = make_uint4(0, 0, 0, 0);

@@ -46,6 +46,11 @@
 
 namespace echo {
 
+// --read-bytes: the most one read(2) takes per connection and round, into the decoder's staging
+// (GPU) or the poller's buffer (CPU port)
+inline size_t g_read_bytes = (size_t)4 << 20;
+
+
 enum : int { EV_NONE = 0, EV_MESSAGE = 1, EV_CLOSE = 2 };
 
 struct Decoder {
@@ -300,9 +305,7 @@ inline Result run(const DecoderFactory& make_decoder, int pollers, int conns, in
     auto poller_loop = [&](Poller& P) {
         Decoder& dec = *P.dec;
         std::vector<ServerConn>& sc = P.sc;
-        // bytes one read(2) may take per connection and round (both servers): ECHO_READ_BYTES, 4 MiB
-        const size_t rb_bytes = [] { const char* e = std::getenv("ECHO_READ_BYTES"); return e && *e ? (size_t)atoll(e) : (size_t)4 << 20; }();
-        std::vector<uint8_t> rb(rb_bytes < 4096 ? 4096 : rb_bytes);
+        std::vector<uint8_t> rb(g_read_bytes < 4096 ? 4096 : g_read_bytes);   // one read(2) per connection and round
         std::vector<size_t> fed;
         epoll_event evs[1024];
         const uint64_t want = (uint64_t)sc.size() * (uint64_t)frames;
@@ -506,7 +509,8 @@ inline void parse_args(int argc, char** argv, int& conns, int& frames, size_t& f
                        int& pollers) {
     for (int i = 1; i + 1 < argc; ++i) {
         const std::string k = argv[i];
-        if (k == "--pollers") pollers = atoi(argv[i + 1]);
+        if (k == "--read-bytes") g_read_bytes = (size_t)atoll(argv[i + 1]);
+        else if (k == "--pollers") pollers = atoi(argv[i + 1]);
         else if (k == "--conns") conns = atoi(argv[i + 1]);
         else if (k == "--frames") frames = atoi(argv[i + 1]);
         else if (k == "--size") frame_bytes = (size_t)atoll(argv[i + 1]);

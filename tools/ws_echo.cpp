@@ -3,7 +3,7 @@
 // pass on the MI355X.  Harness: tools/echo_harness.hpp.  The CPU baseline twin is
 // oracle/ws_echo_cpu.cpp.  Prints one JSON line.
 //   ws_echo [--pollers P] [--devices G] [--conns C] [--frames N] [--size BYTES] [--client-threads T]
-//           [--sync] [--shutdown] [--blocking-wait] [--batcher]
+//           [--sync] [--shutdown] [--blocking-wait] [--batcher] [--read-bytes N]
 // --pollers P: P poller threads, each with its own wsc_session (netman runs NumCPU pollers,
 // eventloop/event.go:33-37); connection i belongs to poller i % P.
 // --devices G: poller p's session lives on device p % G (one host thread, stream and
