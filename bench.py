@@ -735,7 +735,8 @@ def echo_configs(with_cpu=True):
     the reference's frame-at-a-time decode ported to C++ (cpu_baseline leg, kind "port").  Each
     run is a separate process; msgs/s and GiB/s of echoed payload, every byte checked.  P pollers
     (netman runs NumCPU, eventloop/event.go:33-37): connection i on poller i % P, each poller its
-    own decoder -- for the GPU its own wsc_session on the one device."""
+    own decoder -- for the GPU its own wsc_session on the one device.  One read(2) takes at most
+    4 MiB per connection and round unless a row says otherwise (--read-bytes)."""
     import subprocess
     gpu = os.path.join(ROOT, "tools", "ws_echo")
     cpu = os.path.join(ROOT, "oracle", "_build", "ws_echo_cpu")
@@ -745,6 +746,13 @@ def echo_configs(with_cpu=True):
         runs.append((f"64 conns x 200 x 64 KiB, {P} poller(s)", ["--conns", "64", "--frames", "200", "--size", "65536",
                                                                   "--client-threads", "4", "--pollers", str(P)],
                      ["gpu", "gpu_blocking_wait", "cpu_port"] if P == 8 else ["gpu", "cpu_port"]))
+        # the same traffic with at most 512 KiB per read(2) (--read-bytes): more, smaller rounds.  The
+        # echo is client-bound from 4 pollers on (ECHO_TIMING: the pollers' loops are busy ~1/3 of
+        # the run), and how early the replies go out moves both servers by 10-40 %
+        runs.append((f"64 conns x 200 x 64 KiB, {P} poller(s), 512 KiB reads", ["--conns", "64", "--frames", "200", "--size", "65536",
+                                                                                "--client-threads", "4", "--pollers", str(P),
+                                                                                "--read-bytes", "524288"],
+                     ["gpu", "cpu_port"]))
         runs.append((f"64 conns x 2000 x 1 KiB, {P} poller(s)", ["--conns", "64", "--frames", "2000", "--size", "1024",
                                                                  "--client-threads", "4", "--pollers", str(P)],
                      ["gpu", "gpu_sync", "cpu_port"]))

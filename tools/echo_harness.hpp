@@ -337,6 +337,39 @@ inline Result run(const DecoderFactory& make_decoder, int pollers, int conns, in
                 }
             }
         };
+        // every connection's pending echo bytes, until its socket buffer is full; a connection whose
+        // close frame is out is closed (unix.Close, websocket_ctrl.go:117)
+        auto send_all = [&] {
+            for (size_t i = 0; i < sc.size(); ++i) {
+                ServerConn& c = sc[i];
+                if (c.closed) continue;
+                while (c.out_pos < c.out.size()) {   // until the socket buffer is full
+                    const ssize_t w = send(c.fd, c.out.data() + c.out_pos, c.out.size() - c.out_pos, MSG_NOSIGNAL);
+                    if (w <= 0) break;
+                    c.out_pos += (size_t)w;
+                }
+                if (c.out_pos == c.out.size()) {
+                    c.out.clear();
+                    c.out_pos = 0;
+                }
+                const bool need = c.out_pos < c.out.size();
+                if (c.closing && !need) {   // the close frame is out: unix.Close(fd) (websocket_ctrl.go:117)
+                    epoll_ctl(P.ep, EPOLL_CTL_DEL, c.fd, nullptr);
+                    close(c.fd);
+                    c.fd = -1;
+                    c.closed = true;
+                    ++n_closed;
+                    continue;
+                }
+                if (need != c.want_out) {
+                    epoll_event e{};
+                    e.events = (c.read_eof ? 0u : EPOLLIN) | (need ? EPOLLOUT : 0u);
+                    e.data.u64 = i;
+                    epoll_ctl(P.ep, EPOLL_CTL_MOD, c.fd, &e);
+                    c.want_out = need;
+                }
+            }
+        };
         auto all_done = [&] { return shutdown_wr ? n_closed == sc.size() : P.served >= want; };
         while (P.error.empty() && !all_done() && client_fail.load() == 0) {
             if (std::chrono::steady_clock::now() > deadline) {
@@ -394,6 +427,7 @@ inline Result run(const DecoderFactory& make_decoder, int pollers, int conns, in
                 }
                 lap(2);
                 echo_round(drain);         // ... while round r is echoed
+                send_all();                // and sent, before waiting for round r+1
                 lap(3);
                 dec.complete();
                 lap(4);
@@ -417,35 +451,7 @@ inline Result run(const DecoderFactory& make_decoder, int pollers, int conns, in
                 eofs.resize(w);
             }
             dec.drained();
-            for (size_t i = 0; i < sc.size(); ++i) {
-                ServerConn& c = sc[i];
-                if (c.closed) continue;
-                while (c.out_pos < c.out.size()) {   // until the socket buffer is full
-                    const ssize_t w = send(c.fd, c.out.data() + c.out_pos, c.out.size() - c.out_pos, MSG_NOSIGNAL);
-                    if (w <= 0) break;
-                    c.out_pos += (size_t)w;
-                }
-                if (c.out_pos == c.out.size()) {
-                    c.out.clear();
-                    c.out_pos = 0;
-                }
-                const bool need = c.out_pos < c.out.size();
-                if (c.closing && !need) {   // the close frame is out: unix.Close(fd) (websocket_ctrl.go:117)
-                    epoll_ctl(P.ep, EPOLL_CTL_DEL, c.fd, nullptr);
-                    close(c.fd);
-                    c.fd = -1;
-                    c.closed = true;
-                    ++n_closed;
-                    continue;
-                }
-                if (need != c.want_out) {
-                    epoll_event e{};
-                    e.events = (c.read_eof ? 0u : EPOLLIN) | (need ? EPOLLOUT : 0u);
-                    e.data.u64 = i;
-                    epoll_ctl(P.ep, EPOLL_CTL_MOD, c.fd, &e);
-                    c.want_out = need;
-                }
-            }
+            send_all();
             lap(5);
         }
         if (timing)
