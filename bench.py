@@ -627,8 +627,8 @@ def other_configs(torch, K, synth, only=None):
             def staged(k):
                 for i in range(k):
                     cx, bx = pair[i % 2]
-                    if wcus < 0:
-                        cx.decode(bx, us)
+                    if wcus < 0:   # serial order: stream order alone separates the two batches, so
+                        c.decode(bx, us)   # one context's scratch serves both (no second copy in the caches)
                         continue
                     cx.decode_walk(bx, ws)
                     cx.walk_wait()

@@ -107,6 +107,7 @@ SIGNATURES = {
     "wsc_dev_free": (_I, [_P, _P]),
     "wsc_host_alloc": (_I, [_U64, C.POINTER(_P)]),
     "wsc_host_free": (_I, [_P]),
+    "wsc_kcopy": (_I, [_P, _P, _P, _U64, _P]),
     "wsc_decode": (_I, [_P, C.POINTER(WscBatch), _P]),
     "wsc_sync": (_I, [_P, _P]),
     "wsc_summary_status": (_I, [_P]),
@@ -326,6 +327,12 @@ class Codec:
             arr = (C.c_uint32 * len(cu_mask))(*cu_mask)
             _check(self.lib.wsc_stream_create(self.h, arr, len(cu_mask), C.byref(out)), "wsc_stream_create")
         return out.value
+
+    def kcopy(self, dst, src, nbytes: int, stream=None):
+        """wsc_kcopy: nbytes between device and pinned host memory (tensors, arrays or int
+        addresses; host side from wsc_host_alloc) by a kernel on `stream`; returns once queued"""
+        a = lambda x: x if isinstance(x, int) else _ptr(x)
+        _check(self.lib.wsc_kcopy(self.h, a(dst), a(src), nbytes, self._stream(stream)), "wsc_kcopy")
 
     def stream_destroy(self, stream: int):
         _check(self.lib.wsc_stream_destroy(self.h, stream), "wsc_stream_destroy")

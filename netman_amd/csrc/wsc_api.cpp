@@ -25,6 +25,7 @@ template <bool COMPACT, int P, int NT, int MINW, bool U8>
 __global__ void k_unmask(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*,
                          const wsc_summary*, uint32_t*, uint32_t, uint32_t*, uint32_t*, uint32_t, U8Win);
 template <uint32_t IPT> __global__ void k_encode_scan(EncArgs);
+__global__ void k_kcopy(uint8_t*, const uint8_t*, uint64_t);
 template <int NT> __global__ void k_encode_copy(EncCopyArgs);
 }  // namespace wsc
 
@@ -413,6 +414,22 @@ int wsc_host_alloc(uint64_t bytes, void** out) {
 }
 int wsc_host_free(void* p) {
     if (p) HIP_TRY(hipHostFree(p));
+    return WSC_OK;
+}
+
+int wsc_kcopy(wsc_ctx* c, void* dst, const void* src, uint64_t bytes, void* hip_stream) {
+    if (!c || ((!dst || !src) && bytes)) return fail(WSC_E_INVAL, "NULL argument");
+    if ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15)
+        return fail(WSC_E_INVAL, "dst and src must be 16-byte aligned");
+    if (bytes == 0) return WSC_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    const uint64_t chunks = (bytes + 15) >> 4;
+    uint64_t blocks = (chunks + 4 * 256 - 1) / (4 * 256);
+    if (blocks > (uint64_t)c->n_cu) blocks = (uint64_t)c->n_cu;   // one block per CU: reads in flight, not occupancy
+    if (blocks == 0) blocks = 1;
+    hipLaunchKernelGGL(k_kcopy, dim3((uint32_t)blocks), dim3(256), 0, static_cast<hipStream_t>(hip_stream),
+                       static_cast<uint8_t*>(dst), static_cast<const uint8_t*>(src), bytes);
+    HIP_TRY(hipGetLastError());
     return WSC_OK;
 }
 

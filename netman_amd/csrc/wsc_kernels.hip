@@ -1849,4 +1849,27 @@ template __global__ void k_walk_count<true>(WalkArgs);
 template __global__ void k_walk_emit<false>(WalkArgs);
 template __global__ void k_walk_emit<true>(WalkArgs);
 
+// ---------------------------------------------------------------------------------------------
+// wsc_kcopy: device <-> pinned host by a kernel that reads or writes host memory over PCIe (no
+// copy engine, so the enqueue never holds the host thread).  Grid-stride over 16-byte chunks, 4
+// per lane in flight (a PCIe read round trip is ~1-2 us: 256 blocks x 256 lanes x 64 B keeps ~4 MB
+// outstanding); non-temporal reads, default stores (a device destination is read next).
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_kcopy(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, uint64_t bytes) {
+    const uint64_t n16 = bytes >> 4;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const u32x4* s4 = reinterpret_cast<const u32x4*>(src);
+    u32x4* d4 = reinterpret_cast<u32x4*>(dst);
+    for (; i + 3 * stride < n16; i += 4 * stride) {
+        u32x4 v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = __builtin_nontemporal_load(s4 + i + k * stride);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) d4[i + k * stride] = v[k];
+    }
+    for (; i < n16; i += stride) d4[i] = __builtin_nontemporal_load(s4 + i);
+    if (blockIdx.x == 0 && threadIdx.x < (bytes & 15)) dst[(n16 << 4) + threadIdx.x] = src[(n16 << 4) + threadIdx.x];
+}
+
 }  // namespace wsc

@@ -167,7 +167,10 @@ struct wsc_session {
     uint64_t fault_at = 0, n_submits = 0;
     // WSC_SESSION_TIMING=1: seconds per phase, printed at destroy
     bool timing = false;
-    double t_pack = 0, t_device = 0, t_harvest = 0;
+    int kcopy = 2;                // staging copies by wsc_kcopy: 2 all, 1 the wire's H2D only, 0 none
+                                  // (hipMemcpyAsync; WSC_SESSION_KCOPY, A/B)
+    double t_pack = 0, t_launch = 0, t_device = 0, t_harvest = 0;
+    double t_lh2d = 0, t_ldec = 0;   // parts of t_launch: the H2D enqueues, the decode's launches
     uint64_t n_batches = 0, n_bytes = 0;
     // wsc_session_stats: bytes read, sent to the device, of those sent again (carried), batches,
     // streamed payload bytes collected into messages
@@ -471,6 +474,17 @@ int hip_fail(const char* what, hipError_t e) {
     return wsc::set_last_error(WSC_E_DEVICE, std::string("wsc_session: ") + what + ": " + hipGetErrorString(e));
 }
 
+// one staging copy on the stage's stream: by a kernel (wsc_kcopy) at s->kcopy >= level, else by
+// the copy engine.  A hipMemcpyAsync to or from pinned memory held the poller thread for about the
+// copy (the session's launch took 6.6 ms per 20 MB round at 8 pollers, profiles/r05/ab9_timing_P8.log)
+int stage_copy(const wsc_session* s, const Stage& g, void* dst, const void* src, uint64_t bytes, hipMemcpyKind kind,
+               int level) {
+    if (bytes == 0) return WSC_OK;
+    if (s->kcopy >= level) return wsc_kcopy(g.ctx, dst, src, bytes, g.stream);
+    const hipError_t e = hipMemcpyAsync(dst, src, bytes, kind, g.stream);
+    return e == hipSuccess ? WSC_OK : hip_fail("hipMemcpyAsync", e);
+}
+
 int launch_stage(wsc_session* s, Stage& g) {
     const bool compact = (s->flags & WSC_F_COMPACT) != 0;
     const uint32_t n = (uint32_t)g.seg_conn.size();
@@ -478,9 +492,13 @@ int launch_stage(wsc_session* s, Stage& g) {
     s->st_h2d += g.bytes;
     s->st_batches += 1;
 #define HT(x) do { const hipError_t e_ = (x); if (e_ != hipSuccess) return hip_fail(#x, e_); } while (0)
-    HT(hipMemcpyAsync(g.d_wire, g.h_wire, g.bytes, hipMemcpyHostToDevice, st));
-    HT(hipMemcpyAsync(g.d_seg_off, g.h_seg_off, (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, st));
-    HT(hipMemcpyAsync(g.d_state_in, g.h_state_in, n * sizeof(wsc_conn_state), hipMemcpyHostToDevice, st));
+    const double t0 = s->timing ? now_s() : 0;
+#define CP(d, s_, n_, k, lvl) do { if (const int r_ = stage_copy(s, g, d, s_, n_, k, lvl)) return r_; } while (0)
+    CP(g.d_wire, g.h_wire, g.bytes, hipMemcpyHostToDevice, 1);
+    CP(g.d_seg_off, g.h_seg_off, (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, 2);
+    CP(g.d_state_in, g.h_state_in, n * sizeof(wsc_conn_state), hipMemcpyHostToDevice, 2);
+    const double ta = s->timing ? now_s() : 0;
+    if (s->timing) s->t_lh2d += ta - t0;
     wsc_batch b{};
     b.wire = (uint8_t*)g.d_wire;
     b.n_bytes = g.bytes;
@@ -497,21 +515,26 @@ int launch_stage(wsc_session* s, Stage& g) {
     b.summary = (wsc_summary*)g.d_summary;
     const int rc = wsc_decode(g.ctx, &b, st);
     if (rc) return rc;
-    HT(hipMemcpyAsync(g.h_summary, g.d_summary, sizeof(wsc_summary), hipMemcpyDeviceToHost, st));
-    HT(hipMemcpyAsync(g.h_state_out, g.d_state_out, n * sizeof(wsc_conn_state), hipMemcpyDeviceToHost, st));
-    HT(hipMemcpyAsync(g.h_seg_out, g.d_seg_out, n * sizeof(wsc_seg_result), hipMemcpyDeviceToHost, st));
+    if (s->timing) {
+        const double tb = now_s();
+        s->t_ldec += tb - ta;
+    }
+    CP(g.h_summary, g.d_summary, sizeof(wsc_summary), hipMemcpyDeviceToHost, 2);
+    CP(g.h_state_out, g.d_state_out, n * sizeof(wsc_conn_state), hipMemcpyDeviceToHost, 2);
+    CP(g.h_seg_out, g.d_seg_out, n * sizeof(wsc_seg_result), hipMemcpyDeviceToHost, 2);
     // in place the unmasked wire is the batch's whole input range, known now: its D2H goes out with
     // the launch instead of after complete()'s first wait, so it overlaps the host's work on the
     // previous round (views into h_res of this set were materialised by the complete() before)
-    if (!compact) HT(hipMemcpyAsync(g.h_res, g.d_wire, g.bytes, hipMemcpyDeviceToHost, st));
+    if (!compact) CP(g.h_res, g.d_wire, g.bytes, hipMemcpyDeviceToHost, 2);
     // ... and, in place, as many frame records as the last batch had (+1/8): when this batch has no
     // more, complete() needs no second copy and no second wait (the records cost 32 B each)
     g.frames_pre = 0;
     if (!compact && s->frames_hint) {
         g.frames_pre = s->frames_hint < s->cfg.max_frames ? s->frames_hint : s->cfg.max_frames;
-        HT(hipMemcpyAsync(g.h_frames, g.d_frames, (uint64_t)g.frames_pre * sizeof(wsc_frame), hipMemcpyDeviceToHost, st));
+        CP(g.h_frames, g.d_frames, (uint64_t)g.frames_pre * sizeof(wsc_frame), hipMemcpyDeviceToHost, 2);
     }
     HT(hipEventRecord(g.done_ev, st));
+#undef CP
 #undef HT
     return WSC_OK;
 }
@@ -598,6 +621,7 @@ int wsc_session_create(int device, const wsc_config* cfg, uint32_t flags, wsc_se
     if (rc) { wsc_session_destroy(s); return rc; }
     if (const char* e = std::getenv("WSC_SESSION_TIMING"); e && e[0] == '1') s->timing = true;
     if (const char* e = std::getenv("WSC_SESSION_FAULT"); e && *e) s->fault_at = std::strtoull(e, nullptr, 10);
+    if (const char* e = std::getenv("WSC_SESSION_KCOPY"); e && *e) s->kcopy = e[0] - '0';
     *out = s;
     return WSC_OK;
 }
@@ -605,8 +629,8 @@ int wsc_session_create(int device, const wsc_config* cfg, uint32_t flags, wsc_se
 int wsc_session_destroy(wsc_session* s) {
     if (!s) return WSC_OK;
     if (s->timing)
-        fprintf(stderr, "wsc_session: %llu batches, %llu bytes: pack %.4f s, device (H2D+kernels+D2H) %.4f s, harvest %.4f s\n",
-                (unsigned long long)s->n_batches, (unsigned long long)s->n_bytes, s->t_pack, s->t_device, s->t_harvest);
+        fprintf(stderr, "wsc_session: %llu batches, %llu bytes: pack %.4f s, launch (enqueue) %.4f s (H2D %.4f, decode %.4f), device wait (H2D+kernels+D2H) %.4f s, harvest %.4f s\n",
+                (unsigned long long)s->n_batches, (unsigned long long)s->n_bytes, s->t_pack, s->t_launch, s->t_lh2d, s->t_ldec, s->t_device, s->t_harvest);
     for (Stage& t : s->st) {
         if (t.stream) (void)hipStreamSynchronize(t.stream);
         void* hs[] = {t.h_wire, t.h_res, t.h_seg_off, t.h_state_in, t.h_state_out, t.h_seg_out, t.h_frames,
@@ -784,6 +808,7 @@ int wsc_session_submit(wsc_session* s) {
         f.launch_rc = wsc::set_last_error(WSC_E_DEVICE, "wsc_session: injected device failure (WSC_SESSION_FAULT)");
     else
         f.launch_rc = launch_stage(s, f);
+    const double t2 = s->timing ? now_s() : 0;
     f.in_flight = true;
     s->fill ^= 1;
     s->fill_epoch += 1;
@@ -791,6 +816,7 @@ int wsc_session_submit(wsc_session* s) {
     reset_stage(nf);
     if (s->timing) {
         s->t_pack += t1 - t0;
+        s->t_launch += t2 - t1;
         s->n_batches += 1;
         s->n_bytes += f.bytes;
     }
@@ -821,20 +847,19 @@ int wsc_session_complete(wsc_session* s) {
     uint32_t nf = 0;
     if (rc == WSC_OK && !split) {
         nf = g.h_summary->n_frames;
-        hipStream_t st = g.stream;
-        hipError_t e = hipSuccess;
-        const char* what = "";
-        auto D2H = [&](void* dst, const void* src, uint64_t bytes, const char* w) {
-            if (e == hipSuccess && bytes && (e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st)) != hipSuccess) what = w;
+        int crc = WSC_OK;
+        auto D2H = [&](void* dst, const void* src, uint64_t bytes) {
+            if (crc == WSC_OK) crc = stage_copy(s, g, dst, src, bytes, hipMemcpyDeviceToHost, 2);
         };
         const uint32_t pre = nf < g.frames_pre ? nf : g.frames_pre;   // (copied with the launch)
-        D2H(g.h_frames + pre, (const wsc_frame*)g.d_frames + pre, (uint64_t)(nf - pre) * sizeof(wsc_frame), "hipMemcpyAsync frames");
+        D2H(g.h_frames + pre, (const wsc_frame*)g.d_frames + pre, (uint64_t)(nf - pre) * sizeof(wsc_frame));
         if (compact) {
-            D2H(g.h_res, g.d_arena, g.h_summary->data_bytes + g.h_summary->ctrl_bytes, "hipMemcpyAsync arena");
-            D2H(g.h_frame_dst, g.d_frame_dst, (uint64_t)nf * sizeof(uint64_t), "hipMemcpyAsync frame_dst");
+            D2H(g.h_res, g.d_arena, g.h_summary->data_bytes + g.h_summary->ctrl_bytes);
+            D2H(g.h_frame_dst, g.d_frame_dst, (uint64_t)nf * sizeof(uint64_t));
         }   // (in place the wire came back with the launch: launch_stage)
-        if (e == hipSuccess && (compact || nf > pre) && (e = stage_wait(s, g)) != hipSuccess) what = "hipStreamSynchronize";
-        if (e != hipSuccess) rc = hip_fail(what, e);
+        if (crc == WSC_OK && (compact || nf > pre))
+            if (const hipError_t e = stage_wait(s, g); e != hipSuccess) crc = hip_fail("hipStreamSynchronize", e);
+        rc = crc;
         s->frames_hint = nf + nf / 8;
     }
     const double t1 = s->timing ? now_s() : 0;
@@ -894,8 +919,8 @@ int wsc_session_decode(wsc_session* s) {
     return WSC_E_CAPACITY;
 }
 
-// bytes fed but not yet submitted (the staging being filled + connections' spills): a poller calls
-// submit again while this is non-zero, even in a round without new reads
+// whether complete() would return without waiting: every launched set's last operation has
+// finished (or its launch failed, which complete() reports at once)
 int wsc_session_ready(wsc_session* s, int* ready) {
     if (!s || !ready) return WSC_E_INVAL;
     *ready = 1;
@@ -904,6 +929,8 @@ int wsc_session_ready(wsc_session* s, int* ready) {
     return WSC_OK;
 }
 
+// bytes fed but not yet submitted (the staging being filled + connections' spills): a poller calls
+// submit again while this is non-zero, even in a round without new reads
 int wsc_session_pending(wsc_session* s, uint64_t* bytes) {
     if (!s || !bytes) return WSC_E_INVAL;
     apply_removes(s);

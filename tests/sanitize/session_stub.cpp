@@ -234,6 +234,11 @@ static void walk_batch(const wsc_ctx* c, uint8_t* w, const uint64_t* off, uint32
 }
 
 extern "C" {
+int wsc_kcopy(wsc_ctx*, void* dst, const void* src, uint64_t bytes, void*) {   // "device" = host memory
+    if (bytes) std::memcpy(dst, src, bytes);
+    return WSC_OK;
+}
+
 int wsc_decode(wsc_ctx* c, const wsc_batch* b, void*) {
     if (b->flags & WSC_F_COMPACT) return WSC_E_INVAL;   // (the stand-in does in place only)
     walk_batch(c, b->wire, b->seg_off, b->n_segs, b->state_in, b->state_out, b->seg_out, b->frames, b->frames_cap,

@@ -262,3 +262,53 @@ def test_ready_poll_then_complete(codec_lib, blocking):
         assert events_of_session(sess, c) == _oracle_keys(s)
     assert sess.ready()
     sess.close()
+
+
+@pytest.mark.parametrize("nbytes", [1, 15, 16, 17, 4095, (1 << 20) + 3, (64 << 20) + 5])
+def test_kcopy_both_directions(codec_lib, nbytes):
+    """wsc_kcopy (the session's staging copies): pinned host -> device and device -> pinned host,
+    every byte arrives and nothing past the range is written, at sizes around the 16-byte chunks
+    and the grid's 4-chunk rounds; misaligned pointers are refused"""
+    import ctypes as C
+    import torch
+    lib = K.load_library()
+    c = K.Codec(0, max_batch_bytes=1 << 20, max_segs=16, max_frames=64)
+    hp, hq = C.c_void_p(), C.c_void_p()
+    assert lib.wsc_host_alloc(nbytes + 64, C.byref(hp)) == 0
+    assert lib.wsc_host_alloc(nbytes + 64, C.byref(hq)) == 0
+    try:
+        src = np.frombuffer((C.c_uint8 * (nbytes + 64)).from_address(hp.value), dtype=np.uint8)
+        back = np.frombuffer((C.c_uint8 * (nbytes + 64)).from_address(hq.value), dtype=np.uint8)
+        src[:] = np.random.default_rng(nbytes).integers(0, 256, nbytes + 64, dtype=np.uint8)
+        back[:] = 0x5A
+        dev = torch.full((nbytes + 64,), 0xEE, dtype=torch.uint8, device="cuda:0")
+        c.kcopy(dev, hp.value, nbytes)          # host -> device
+        c.kcopy(hq.value, dev, nbytes)          # device -> host (stream order: after the first)
+        c.sync()
+        got = dev.cpu().numpy()
+        assert np.array_equal(got[:nbytes], src[:nbytes]) and (got[nbytes:] == 0xEE).all()
+        assert np.array_equal(back[:nbytes], src[:nbytes]) and (back[nbytes:] == 0x5A).all()
+        with pytest.raises(K.WscError) as ei:
+            c.kcopy(dev, hp.value + 1, 16)
+        assert ei.value.rc == K.WSC_E_INVAL
+    finally:
+        lib.wsc_host_free(hp)
+        lib.wsc_host_free(hq)
+        c.close()
+
+
+@pytest.mark.parametrize("level", ["0", "1", "2"])
+@pytest.mark.parametrize("compact", [False, True])
+def test_session_staging_copy_paths(codec_lib, monkeypatch, level, compact):
+    """the session's staging copies by kernels (WSC_SESSION_KCOPY=2, default), the wire's H2D only
+    (1) or none (0, hipMemcpyAsync) decode the same random streams to the oracle's events"""
+    monkeypatch.setenv("WSC_SESSION_KCOPY", level)
+    rng = np.random.default_rng(77)
+    sess = K.Session(0, compact=compact, max_batch_bytes=4 << 20, max_segs=256, max_frames=1 << 15)
+    streams = [random_stream(77000 + i, n_units=25) for i in range(60)]
+    try:
+        conns, got = _drive(sess, streams, rng, zero_copy=True)
+    finally:
+        sess.close()
+    for i, (c, s) in enumerate(zip(conns, streams)):
+        assert got[c] == _oracle_keys(s), f"stream {i}"
