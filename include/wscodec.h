@@ -230,8 +230,9 @@ int wsc_host_free(void* p);
  * side, or both device) done by a kernel, which reads or writes the host buffer over PCIe: the
  * call returns once the kernel is queued.  On this platform a hipMemcpyAsync to or from pinned
  * memory can hold the calling thread for about the copy's duration (a poller then waited ~3-7 ms
- * per 20 MB round at 4-8 pollers), so wsc_session makes its copies with this.  `dst` and `src`
- * 16-byte aligned; the source must stay unchanged until the stream passes the copy.            */
+ * per 20 MB round at 4-8 pollers), so wsc_session makes its copies with this.  Any alignment
+ * (16-byte chunks between 16-byte aligned ends are fastest); the source must stay unchanged
+ * until the stream passes the copy.                                                            */
 int wsc_kcopy(wsc_ctx* ctx, void* dst, const void* src, uint64_t bytes, void* hip_stream);
 
 /* Enqueue the decode of one device-resident batch on `hip_stream` (a hipStream_t; NULL = the

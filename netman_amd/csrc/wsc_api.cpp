@@ -419,8 +419,6 @@ int wsc_host_free(void* p) {
 
 int wsc_kcopy(wsc_ctx* c, void* dst, const void* src, uint64_t bytes, void* hip_stream) {
     if (!c || ((!dst || !src) && bytes)) return fail(WSC_E_INVAL, "NULL argument");
-    if ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15)
-        return fail(WSC_E_INVAL, "dst and src must be 16-byte aligned");
     if (bytes == 0) return WSC_OK;
     HIP_TRY(hipSetDevice(c->device));
     const uint64_t chunks = (bytes + 15) >> 4;

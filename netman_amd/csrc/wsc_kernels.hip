@@ -1855,21 +1855,40 @@ template __global__ void k_walk_emit<true>(WalkArgs);
 // per lane in flight (a PCIe read round trip is ~1-2 us: 256 blocks x 256 lanes x 64 B keeps ~4 MB
 // outstanding); non-temporal reads, default stores (a device destination is read next).
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_kcopy(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, uint64_t bytes) {
-    const uint64_t n16 = bytes >> 4;
+// Any alignment: the head up to dst's first 16-byte boundary and the tail go byte by byte; the
+// body stores aligned 16-byte chunks, loading them aligned (nt) when src shares dst's alignment
+// and with unaligned 16-byte loads otherwise.
+template <bool SRC_ALIGNED>
+__device__ __forceinline__ void kcopy_body(u32x4* __restrict__ d4, const uint8_t* __restrict__ s, uint64_t n16) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const u32x4* s4 = reinterpret_cast<const u32x4*>(src);
-    u32x4* d4 = reinterpret_cast<u32x4*>(dst);
+    auto ld = [&](uint64_t k) -> u32x4 {
+        if constexpr (SRC_ALIGNED) return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(s) + k);
+        const u32x4u_ld t = __builtin_nontemporal_load(reinterpret_cast<const u32x4u_ld*>(s + 16 * k));
+        return u32x4{t.x, t.y, t.z, t.w};
+    };
     for (; i + 3 * stride < n16; i += 4 * stride) {
         u32x4 v[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) v[k] = __builtin_nontemporal_load(s4 + i + k * stride);
+        for (int k = 0; k < 4; ++k) v[k] = ld(i + k * stride);
 #pragma unroll
         for (int k = 0; k < 4; ++k) d4[i + k * stride] = v[k];
     }
-    for (; i < n16; i += stride) d4[i] = __builtin_nontemporal_load(s4 + i);
-    if (blockIdx.x == 0 && threadIdx.x < (bytes & 15)) dst[(n16 << 4) + threadIdx.x] = src[(n16 << 4) + threadIdx.x];
+    for (; i < n16; i += stride) d4[i] = ld(i);
+}
+
+__global__ __launch_bounds__(256) void k_kcopy(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, uint64_t bytes) {
+    uint64_t head = (16u - (uint32_t)(reinterpret_cast<uintptr_t>(dst) & 15u)) & 15u;
+    if (head > bytes) head = bytes;
+    const uint64_t n16 = (bytes - head) >> 4;
+    const uint64_t tail0 = head + (n16 << 4);
+    if (blockIdx.x == 0 && threadIdx.x < 16) {
+        if (threadIdx.x < head) dst[threadIdx.x] = src[threadIdx.x];
+        if (tail0 + threadIdx.x < bytes) dst[tail0 + threadIdx.x] = src[tail0 + threadIdx.x];
+    }
+    u32x4* d4 = reinterpret_cast<u32x4*>(dst + head);
+    if ((reinterpret_cast<uintptr_t>(src + head) & 15u) == 0) kcopy_body<true>(d4, src + head, n16);
+    else kcopy_body<false>(d4, src + head, n16);
 }
 
 }  // namespace wsc

@@ -167,8 +167,11 @@ struct wsc_session {
     uint64_t fault_at = 0, n_submits = 0;
     // WSC_SESSION_TIMING=1: seconds per phase, printed at destroy
     bool timing = false;
-    int kcopy = 2;                // staging copies by wsc_kcopy: 2 all, 1 the wire's H2D only, 0 none
-                                  // (hipMemcpyAsync; WSC_SESSION_KCOPY, A/B)
+    int kcopy = 1;                // staging copies by wsc_kcopy: 1 the wire's H2D (default), 2 all, 0
+                                  // none (hipMemcpyAsync); WSC_SESSION_KCOPY.  At 2 the small copies
+                                  // queue as kernels behind other pollers' decodes on the shared
+                                  // compute queues (profiles/r05/ab11_echo_*: 4 pollers, 512 KiB
+                                  // reads 4.24 -> 3.02 GiB/s), so they stay on the copy engines
     double t_pack = 0, t_launch = 0, t_device = 0, t_harvest = 0;
     double t_lh2d = 0, t_ldec = 0;   // parts of t_launch: the H2D enqueues, the decode's launches
     uint64_t n_batches = 0, n_bytes = 0;

@@ -267,8 +267,8 @@ def test_ready_poll_then_complete(codec_lib, blocking):
 @pytest.mark.parametrize("nbytes", [1, 15, 16, 17, 4095, (1 << 20) + 3, (64 << 20) + 5])
 def test_kcopy_both_directions(codec_lib, nbytes):
     """wsc_kcopy (the session's staging copies): pinned host -> device and device -> pinned host,
-    every byte arrives and nothing past the range is written, at sizes around the 16-byte chunks
-    and the grid's 4-chunk rounds; misaligned pointers are refused"""
+    every byte arrives and nothing outside the range is written, at sizes around the 16-byte
+    chunks and the grid's 4-chunk rounds, with both ends aligned and with either end misaligned"""
     import ctypes as C
     import torch
     lib = K.load_library()
@@ -288,9 +288,14 @@ def test_kcopy_both_directions(codec_lib, nbytes):
         got = dev.cpu().numpy()
         assert np.array_equal(got[:nbytes], src[:nbytes]) and (got[nbytes:] == 0xEE).all()
         assert np.array_equal(back[:nbytes], src[:nbytes]) and (back[nbytes:] == 0x5A).all()
-        with pytest.raises(K.WscError) as ei:
-            c.kcopy(dev, hp.value + 1, 16)
-        assert ei.value.rc == K.WSC_E_INVAL
+        for so, do in [(1, 0), (0, 5), (3, 7), (9, 9)]:   # misaligned source / destination / both
+            n = max(0, nbytes - 16)
+            dev.fill_(0xEE)
+            c.kcopy(dev.data_ptr() + do, hp.value + so, n)
+            c.sync()
+            got = dev.cpu().numpy()
+            assert np.array_equal(got[do:do + n], src[so:so + n]), (so, do)
+            assert (got[:do] == 0xEE).all() and (got[do + n:] == 0xEE).all(), (so, do)
     finally:
         lib.wsc_host_free(hp)
         lib.wsc_host_free(hq)
