@@ -616,6 +616,17 @@ def other_configs(torch, K, synth, only=None):
         torch.cuda.synchronize()
         c2, t2, b2 = one()
         pair = [(c, b), (c2, b2)]
+        # the one-batch leg re-decodes ONE buffer, whose tail the caches may still hold from the
+        # previous pass; the same back-to-back decodes alternating over two buffers (one context,
+        # one stream) show what that reuse is worth
+        for _ in range(10):
+            c.decode(b2, st.cuda_stream)
+        e0.record(st)
+        for i in range(100):
+            c.decode(b if i % 2 == 0 else b2, st.cuda_stream)
+        e1.record(st)
+        torch.cuda.synchronize()
+        two_ms = float(e0.elapsed_time(e1)) / 100
         best = None
         for wcus, rest in PIPELINE_SPLITS:
             if wcus < 0:
@@ -656,6 +667,7 @@ def other_configs(torch, K, synth, only=None):
                      "pipelined_walk_cus": wcus if wcus > 0 else ("all, high-priority stream" if wcus == 0 else
                                                                   "serial: walks and unmasks in order on one stream"),
                      "pipelined_unmask_cus": "the other CUs" if rest else "all",
+                     "two_buffers_ms": round(two_ms, 4),
                      "frames": int(cfg["n_frames"]), "payload_bytes": int(cfg["payload_bytes"]), "alg_bytes": alg,
                      "device_errors": not ok}
         c.close()

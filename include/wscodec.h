@@ -416,10 +416,11 @@ typedef struct wsc_event {
     uint32_t err;         /* CLOSE: WSC_ERR_* */
     uint32_t pad;
     const uint8_t* data;  /* MESSAGE / PONG payload.  Valid until the FIRST of: the next
-                             wsc_session_next on the same connection, the next
                              wsc_session_complete / wsc_session_decode, or the connection's
-                             removal being applied.  Copy it to keep it (the reference hands
-                             each handler a fresh buffer, websocket_frame.go:90).              */
+                             removal being applied -- so a round's replies can be sent straight
+                             from it (writev) while the next batch decodes.  Copy it to keep it
+                             longer (the reference hands each handler a fresh buffer,
+                             websocket_frame.go:90).                                           */
     uint64_t len;
 } wsc_event;
 

@@ -172,6 +172,7 @@ struct wsc_session {
                                   // queue as kernels behind other pollers' decodes on the shared
                                   // compute queues (profiles/r05/ab11_echo_*: 4 pollers, 512 KiB
                                   // reads 4.24 -> 3.02 GiB/s), so they stay on the copy engines
+    std::vector<std::vector<uint8_t>> retired;   // owned event bytes handed out this round (wsc_session_next)
     double t_pack = 0, t_launch = 0, t_device = 0, t_harvest = 0;
     double t_lh2d = 0, t_ldec = 0;   // parts of t_launch: the H2D enqueues, the decode's launches
     uint64_t n_batches = 0, n_bytes = 0;
@@ -831,6 +832,7 @@ int wsc_session_submit(wsc_session* s) {
 int wsc_session_complete(wsc_session* s) {
     if (!s) return WSC_E_INVAL;
     apply_removes(s);
+    s->retired.clear();   // event data handed out before this call is no longer valid
     const int set = s->st[0].in_flight ? 0 : (s->st[1].in_flight ? 1 : -1);
     if (set < 0) return WSC_OK;
     Stage& g = s->st[set];
@@ -981,6 +983,9 @@ int wsc_session_next(wsc_session* s, uint32_t conn, wsc_event* ev) {
     if (!c) return WSC_E_STATE;
     std::memset(ev, 0, sizeof(*ev));
     if (c->pending.empty()) { ev->type = WSC_EV_NONE; return WSC_OK; }   // (nil, EAGAIN)
+    // the previous event's owned bytes stay valid until the next complete (a server may still be
+    // sending them from a zero-copy reply queue): retired, not freed
+    if (!c->current.data.empty()) s->retired.push_back(std::move(c->current.data));
     c->current = std::move(c->pending.front());
     c->pending.pop_front();
     *ev = c->current.ev;

@@ -19,7 +19,9 @@ namespace {
 struct Conn {
     std::vector<uint8_t> buf;                 // bytes read, not yet decoded (the socket buffer)
     std::deque<std::vector<uint8_t>> msgs;    // delivered messages
-    std::vector<uint8_t> cur;                 // the message last returned by next()
+    // messages returned by next() since the last feed: like the Go []byte each DecodePacket
+    // returns, a message stays valid while the server still sends it (until the next feed/decode)
+    std::vector<std::vector<uint8_t>> held;
     bool eof = false, closed = false;         // read() returned 0 (io.EOF) / Close() handed out
 };
 
@@ -31,6 +33,7 @@ struct CpuDecoder : echo::Decoder {
         return (int)conns.size() - 1;
     }
     void feed(int c, const uint8_t* p, size_t n) override {
+        conns[c].held.clear();
         conns[c].buf.insert(conns[c].buf.end(), p, p + n);
         dirty.push_back(c);
     }
@@ -76,10 +79,10 @@ struct CpuDecoder : echo::Decoder {
             }
             return echo::EV_NONE;
         }
-        c.cur = std::move(c.msgs.front());
+        c.held.push_back(std::move(c.msgs.front()));   // (moving a vector keeps its bytes in place)
         c.msgs.pop_front();
-        *data = c.cur.data();
-        *len = c.cur.size();
+        *data = c.held.back().data();
+        *len = c.held.back().size();
         return echo::EV_MESSAGE;
     }
     void eof(int id) override { conns[id].eof = true; }

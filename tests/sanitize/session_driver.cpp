@@ -71,14 +71,24 @@ std::atomic<int> fails{0};
 
 void drain(wsc_session* s, Conn& c) {
     wsc_event ev;
+    // every payload handed out stays readable until the next complete (include/wscodec.h): the
+    // earlier ones are re-read after the later next() calls (ASan: no use after free)
+    std::vector<std::pair<const uint8_t*, uint64_t>> seen;
+    const size_t first = c.got.size();
     while (true) {
         const int rc = wsc_session_next(s, c.h, &ev);
         if (rc == WSC_E_STATE) { CHECK(c.removed); return; }
         CHECK(rc == WSC_OK);
-        if (ev.type == WSC_EV_NONE) return;
+        if (ev.type == WSC_EV_NONE) {
+            for (size_t i = 0; i < seen.size(); ++i)
+                CHECK(seen[i].second == c.got[first + i].size() &&
+                      (seen[i].second == 0 || std::memcmp(seen[i].first, c.got[first + i].data(), seen[i].second) == 0));
+            return;
+        }
         if (ev.type == WSC_EV_MESSAGE) {
             CHECK(!c.closed);
             c.got.emplace_back(ev.data, ev.data + ev.len);
+            seen.emplace_back(ev.data, ev.len);
         }
         if (ev.type == WSC_EV_CLOSE) {   // only the EOF's Close(), once, after every message
             CHECK(c.removed || (c.eof && ev.close_code == 1000 && ev.err == 0 && !c.closed));

@@ -28,6 +28,7 @@
 #include <netinet/tcp.h>
 #include <sys/epoll.h>
 #include <sys/socket.h>
+#include <sys/uio.h>
 #include <unistd.h>
 
 #include <atomic>
@@ -36,6 +37,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <functional>
 #include <memory>
 #include <mutex>
@@ -102,11 +104,79 @@ inline size_t put_header(uint8_t* h, uint8_t first, uint64_t n) {
     return 10;
 }
 
+// Reply bytes not yet written, in order: pieces that are views of the decoder's message data
+// (sent straight from it by sendmsg, no copy) or bytes owned here (headers, short payloads, and
+// views the decoder is about to invalidate, copied by materialize()).  Both servers reply this way.
+struct OutQueue {
+    struct Piece { const uint8_t* view; size_t off, n; };   // view == nullptr: own[off, off + n)
+    std::deque<Piece> q;
+    std::vector<uint8_t> own;
+    size_t front_done = 0;   // bytes of q.front() already written
+    bool empty() const { return q.empty(); }
+    void add_own(const uint8_t* p, size_t n) {
+        if (!q.empty() && !q.back().view && q.back().off + q.back().n == own.size()) q.back().n += n;
+        else q.push_back({nullptr, own.size(), n});
+        own.insert(own.end(), p, p + n);
+    }
+    void add(const uint8_t* p, size_t n) {   // short payloads are copied: an iovec costs more
+        if (n < 2048) add_own(p, n);
+        else q.push_back({p, 0, n});
+    }
+    // copy every view still queued into own storage (the decoder's data is about to change)
+    void materialize() {
+        bool any = false;
+        for (const Piece& pc : q) any |= pc.view != nullptr;
+        if (!any) return;
+        std::deque<Piece> nq;
+        std::vector<uint8_t> no;
+        bool first = true;
+        for (const Piece& pc : q) {
+            const size_t skip = first ? front_done : 0;
+            const uint8_t* src = pc.view ? pc.view : own.data() + pc.off;
+            nq.push_back({nullptr, no.size(), pc.n - skip});
+            no.insert(no.end(), src + skip, src + pc.n);
+            first = false;
+        }
+        q.swap(nq);
+        own.swap(no);
+        front_done = 0;
+    }
+    // one sendmsg of up to 256 pieces; bytes written, or <= 0 (EAGAIN / error)
+    ssize_t send_some(int fd) {
+        iovec iov[256];
+        int k = 0;
+        for (size_t i = 0; i < q.size() && k < 256; ++i, ++k) {
+            const Piece& pc = q[i];
+            const size_t skip = i == 0 ? front_done : 0;
+            iov[k].iov_base = const_cast<uint8_t*>((pc.view ? pc.view : own.data() + pc.off) + skip);
+            iov[k].iov_len = pc.n - skip;
+        }
+        msghdr m{};
+        m.msg_iov = iov;
+        m.msg_iovlen = (size_t)k;
+        const ssize_t w = sendmsg(fd, &m, MSG_NOSIGNAL);
+        if (w <= 0) return w;
+        size_t left = (size_t)w;
+        while (left && !q.empty()) {
+            const size_t avail = q.front().n - front_done;
+            if (left < avail) {
+                front_done += left;
+                left = 0;
+            } else {
+                left -= avail;
+                q.pop_front();
+                front_done = 0;
+            }
+        }
+        if (q.empty()) own.clear();
+        return w;
+    }
+};
+
 struct ServerConn {
     int fd = -1;
     int id = -1;
-    std::vector<uint8_t> out;   // echo bytes not yet written
-    size_t out_pos = 0;
+    OutQueue out;               // echo bytes not yet written
     bool want_out = false;
     bool read_eof = false;      // recv() returned 0: the decoder was told, EPOLLIN dropped
     bool closing = false;       // Close(): the close frame is queued, the fd closes once it is sent
@@ -324,14 +394,14 @@ inline Result run(const DecoderFactory& make_decoder, int pollers, int conns, in
                 int k;
                 while ((k = dec.next(c.id, &d, &len)) != EV_NONE) {
                     if (k == EV_CLOSE) {      // Close() -> CloseCode(1000, ""): close frame, then the fd
-                        c.out.insert(c.out.end(), CLOSE_1000, CLOSE_1000 + sizeof(CLOSE_1000));
+                        c.out.add_own(CLOSE_1000, sizeof(CLOSE_1000));
                         c.closing = true;
                         break;
                     }
                     uint8_t h[10];
                     const size_t hl = put_header(h, 0x82, len);
-                    c.out.insert(c.out.end(), h, h + hl);
-                    c.out.insert(c.out.end(), d, d + len);
+                    c.out.add_own(h, hl);
+                    c.out.add(d, len);   // a view: valid until the decoder's next call (materialize())
                     P.served++;
                     P.payload += len;
                 }
@@ -343,16 +413,10 @@ inline Result run(const DecoderFactory& make_decoder, int pollers, int conns, in
             for (size_t i = 0; i < sc.size(); ++i) {
                 ServerConn& c = sc[i];
                 if (c.closed) continue;
-                while (c.out_pos < c.out.size()) {   // until the socket buffer is full
-                    const ssize_t w = send(c.fd, c.out.data() + c.out_pos, c.out.size() - c.out_pos, MSG_NOSIGNAL);
-                    if (w <= 0) break;
-                    c.out_pos += (size_t)w;
-                }
-                if (c.out_pos == c.out.size()) {
-                    c.out.clear();
-                    c.out_pos = 0;
-                }
-                const bool need = c.out_pos < c.out.size();
+                while (!c.out.empty())   // until the socket buffer is full
+                    if (c.out.send_some(c.fd) <= 0) break;
+                c.out.materialize();     // what is left no longer points into the decoder
+                const bool need = !c.out.empty();
                 if (c.closing && !need) {   // the close frame is out: unix.Close(fd) (websocket_ctrl.go:117)
                     epoll_ctl(P.ep, EPOLL_CTL_DEL, c.fd, nullptr);
                     close(c.fd);
@@ -450,8 +514,8 @@ inline Result run(const DecoderFactory& make_decoder, int pollers, int conns, in
                     if (!sc[q].closing) eofs[w++] = q;
                 eofs.resize(w);
             }
+            send_all();      // (leaves no reply pointing into the decoder)
             dec.drained();
-            send_all();
             lap(5);
         }
         if (timing)
@@ -459,11 +523,8 @@ inline Result run(const DecoderFactory& make_decoder, int pollers, int conns, in
                     (unsigned long long)P.rounds, P.t[0], P.t[1], P.t[2], P.t[3], P.t[4], P.t[5]);
         // flush what is left (the clients check every echo)
         for (auto& c : sc) {
-            while (!c.closed && c.out_pos < c.out.size() && client_fail.load() == 0 && P.error.empty()) {
-                const ssize_t w = send(c.fd, c.out.data() + c.out_pos, c.out.size() - c.out_pos, MSG_NOSIGNAL);
-                if (w > 0) c.out_pos += (size_t)w;
-                else std::this_thread::yield();
-            }
+            while (!c.closed && !c.out.empty() && client_fail.load() == 0 && P.error.empty())
+                if (c.out.send_some(c.fd) <= 0) std::this_thread::yield();
         }
         if (!P.error.empty()) client_fail++;   // release the client threads
     };
