@@ -832,13 +832,15 @@ def host_inclusive(codec, cfg, K):
 
 
 def host_inclusive_pipelined(torch, codecs, streams, cfg, K, chunks=16, iters=3, dir_streams=False, nbuf=0,
-                             copy_streams=1):
+                             copy_streams=1, kcopy=0):
     """The same batch from pinned host memory, cut at segment boundaries into `chunks` pieces that
     alternate between the in-flight contexts/streams: H2D of piece i+1 overlaps the decode and
     the D2H of piece i (PCIe is full duplex).  Output: unmasked wire + frame records in pinned
     host memory.  Reported in DESIGN.md, never as `value`.  nbuf > len(codecs): that many piece-
     sized contexts of its own; copy_streams: streams per copy direction (dir_streams), piece i on
-    stream i % copy_streams (the copy engines a stream lands on decide whether H2D and D2H overlap)."""
+    stream i % copy_streams (the copy engines a stream lands on decide whether H2D and D2H overlap).
+    kcopy (each piece's copies on its decode stream): 1 = the wire's H2D by a kernel reading the
+    pinned host buffer (wsc_kcopy), 2 = also the D2H of the wire and the records by kernels."""
     own = []
     if nbuf > len(codecs):
         n_segs_all = len(cfg["seg_off"]) - 1
@@ -848,19 +850,32 @@ def host_inclusive_pipelined(torch, codecs, streams, cfg, K, chunks=16, iters=3,
         codecs = own
         streams = [torch.cuda.Stream() for _ in range(nbuf)]
     try:
-        return _host_inclusive_pipelined(torch, codecs, streams, cfg, K, chunks, iters, dir_streams, copy_streams)
+        return _host_inclusive_pipelined(torch, codecs, streams, cfg, K, chunks, iters, dir_streams, copy_streams, kcopy)
     finally:
         for c in own:
             c.close()
 
 
-def _host_inclusive_pipelined(torch, codecs, streams, cfg, K, chunks, iters, dir_streams, copy_streams):
+def _host_inclusive_pipelined(torch, codecs, streams, cfg, K, chunks, iters, dir_streams, copy_streams, kcopy=0):
     P = len(codecs)
     if P < 2:
         return None
     dev = torch.device("cuda", torch.cuda.current_device())
-    wire_h = torch.from_numpy(cfg["wire"]).pin_memory()
-    out_h = torch.empty_like(wire_h).pin_memory()
+    hold = []   # wsc_host_alloc blocks (kcopy: buffers a kernel reads / writes by their host address)
+
+    def host_buf(nbytes):
+        if not kcopy:
+            return torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+        lib = K.load_library()
+        p = C.c_void_p()
+        if lib.wsc_host_alloc(nbytes, C.byref(p)) != 0:
+            raise RuntimeError("wsc_host_alloc")
+        hold.append(p)
+        return torch.from_numpy(np.frombuffer((C.c_uint8 * nbytes).from_address(p.value), dtype=np.uint8))
+
+    wire_h = host_buf(len(cfg["wire"]))
+    wire_h.copy_(torch.from_numpy(cfg["wire"]))
+    out_h = host_buf(len(cfg["wire"]))
     so = cfg["seg_off"].astype(np.int64)
     n_segs = len(so) - 1
     cuts = [int(round(i * n_segs / chunks)) for i in range(chunks + 1)]
@@ -882,7 +897,7 @@ def _host_inclusive_pipelined(torch, codecs, streams, cfg, K, chunks, iters, dir
                          so=torch.empty(max_segs * 32, dtype=torch.uint8, device=dev),
                          fr=torch.empty(max_frames * 32, dtype=torch.uint8, device=dev),
                          sm=torch.empty(32, dtype=torch.uint8, device=dev)))
-    rec_h = [torch.empty(max_frames * 32, dtype=torch.uint8).pin_memory() for _ in pieces]
+    rec_h = [host_buf(max_frames * 32) for _ in pieces]
     rec_n = [0] * len(pieces)
     for i, (a0, a1, k, _) in enumerate(pieces):
         rec_n[i] = int(np.count_nonzero((cfg["payload_off"] >= a0) & (cfg["payload_off"] < a1)))
@@ -921,11 +936,18 @@ def _host_inclusive_pipelined(torch, codecs, streams, cfg, K, chunks, iters, dir
                     ev_free[j].record(d2h)
                 continue
             with torch.cuda.stream(st):
-                b["wire"][: a1 - a0].copy_(wire_h[a0:a1], non_blocking=True)
+                if kcopy:
+                    codecs[j].kcopy(b["wire"], wire_h.data_ptr() + a0, a1 - a0, st.cuda_stream)
+                else:
+                    b["wire"][: a1 - a0].copy_(wire_h[a0:a1], non_blocking=True)
                 b["seg_off"][: k + 1].copy_(rel, non_blocking=True)
                 codecs[j].decode(batch, st.cuda_stream)
-                out_h[a0:a1].copy_(b["wire"][: a1 - a0], non_blocking=True)
-                rec_h[i][: rec_n[i] * 32].copy_(b["fr"][: rec_n[i] * 32], non_blocking=True)
+                if kcopy >= 2:
+                    codecs[j].kcopy(out_h.data_ptr() + a0, b["wire"], a1 - a0, st.cuda_stream)
+                    codecs[j].kcopy(rec_h[i], b["fr"], rec_n[i] * 32, st.cuda_stream)
+                else:
+                    out_h[a0:a1].copy_(b["wire"][: a1 - a0], non_blocking=True)
+                    rec_h[i][: rec_n[i] * 32].copy_(b["fr"][: rec_n[i] * 32], non_blocking=True)
 
     one_pass()
     torch.cuda.synchronize()
@@ -936,9 +958,12 @@ def _host_inclusive_pipelined(torch, codecs, streams, cfg, K, chunks, iters, dir
         one_pass()
     torch.cuda.synchronize()
     el = (time.perf_counter() - t0) / iters
+    lib = K.load_library() if hold else None
+    for p in hold:
+        lib.wsc_host_free(p)
     return {"gib_s": round(cfg["payload_bytes"] / el / 2**30, 2), "ms_per_batch": round(el * 1e3, 2),
             "chunks": len(pieces), "streams": P, "copy_streams_per_direction": copy_streams if dir_streams else 0,
-            "parity_ok": ok,
+            "kcopy": kcopy, "parity_ok": ok,
             "note": "pinned host wire -> H2D -> decode -> D2H wire+records, pieces alternating over streams"
                     + (" (one stream per copy direction, events between them)" if dir_streams else " (each piece's copies on its decode stream)")}
 
