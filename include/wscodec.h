@@ -232,7 +232,8 @@ int wsc_host_free(void* p);
  * memory can hold the calling thread for about the copy's duration (a poller then waited ~3-7 ms
  * per 20 MB round at 4-8 pollers), so wsc_session makes its copies with this.  Any alignment
  * (16-byte chunks between 16-byte aligned ends are fastest); the source must stay unchanged
- * until the stream passes the copy.                                                            */
+ * until the stream passes the copy.  WSC_E_INVAL for memory the device cannot reach (pageable
+ * host memory): checked on the host, never faulted on.                                          */
 int wsc_kcopy(wsc_ctx* ctx, void* dst, const void* src, uint64_t bytes, void* hip_stream);
 
 /* Enqueue the decode of one device-resident batch on `hip_stream` (a hipStream_t; NULL = the

@@ -417,10 +417,32 @@ int wsc_host_free(void* p) {
     return WSC_OK;
 }
 
+// the address a kernel uses for p: device memory as is, pinned host memory through its device
+// mapping; nullptr for memory the device cannot reach (pageable host memory would fault the GPU)
+static const void* device_view(const void* p) {
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    if (a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged) return p;
+    if (a.type == hipMemoryTypeHost) {   // (offset from the reported host address: interior pointers)
+        if (!a.devicePointer) return p;
+        if (!a.hostPointer) return a.devicePointer;
+        return static_cast<const uint8_t*>(a.devicePointer) + (static_cast<const uint8_t*>(p) - static_cast<const uint8_t*>(a.hostPointer));
+    }
+    return nullptr;
+}
+
 int wsc_kcopy(wsc_ctx* c, void* dst, const void* src, uint64_t bytes, void* hip_stream) {
     if (!c || ((!dst || !src) && bytes)) return fail(WSC_E_INVAL, "NULL argument");
     if (bytes == 0) return WSC_OK;
     HIP_TRY(hipSetDevice(c->device));
+    const void* dv = device_view(dst);
+    const void* sv = device_view(src);
+    if (!dv || !sv) return fail(WSC_E_INVAL, "wsc_kcopy: dst and src must be device memory or pinned host memory");
+    dst = const_cast<void*>(dv);
+    src = sv;
     const uint64_t chunks = (bytes + 15) >> 4;
     uint64_t blocks = (chunks + 4 * 256 - 1) / (4 * 256);
     if (blocks > (uint64_t)c->n_cu) blocks = (uint64_t)c->n_cu;   // one block per CU: reads in flight, not occupancy

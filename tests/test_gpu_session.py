@@ -288,6 +288,18 @@ def test_kcopy_both_directions(codec_lib, nbytes):
         got = dev.cpu().numpy()
         assert np.array_equal(got[:nbytes], src[:nbytes]) and (got[nbytes:] == 0xEE).all()
         assert np.array_equal(back[:nbytes], src[:nbytes]) and (back[nbytes:] == 0x5A).all()
+        # memory the device cannot reach is refused on the host, never faulted on: first check that
+        # the runtime reports pageable memory as unregistered (what the guard tests), and only then
+        # hand it to wsc_kcopy (a kernel must never see it)
+        pageable = np.zeros(64, np.uint8)
+        hip = C.CDLL("libamdhip64.so")
+        attr = (C.c_uint8 * 64)()
+        rc = hip.hipPointerGetAttributes(attr, C.c_void_p(pageable.ctypes.data))
+        assert rc != 0 or int.from_bytes(bytes(attr[:4]), "little") == 0, "pageable memory reported as registered"
+        hip.hipGetLastError()
+        with pytest.raises(K.WscError) as ei:
+            c.kcopy(dev, pageable, 64)
+        assert ei.value.rc == K.WSC_E_INVAL
         for so, do in [(1, 0), (0, 5), (3, 7), (9, 9)]:   # misaligned source / destination / both
             n = max(0, nbytes - 16)
             dev.fill_(0xEE)
