@@ -200,29 +200,50 @@ __device__ __forceinline__ void pm_mask(const u32x4* __restrict__ pm, uint32_t l
 // edge are compacted into lanes (LDS list, in window order) and assembled together -- one pass
 // of the costly header placement per window instead of one per 1 KiB slice (PMC: the slice-wise
 // version issued ~600 VALU per window at 1 KiB frames, past the HBM budget).
+// Frames base + lane in lanes, absolute output offsets: header start o, payload start p, end e
+// (all ~0 past the last frame), source offset of output byte x = so + x, the header's bytes.
+struct EncLanes {
+    uint64_t o, p, e;
+    int64_t so;
+    uint32_t h[3];
+};
+__device__ __forceinline__ EncLanes enc_lanes_load(const EncCopyArgs& a, uint32_t base, uint32_t lane) {
+    EncLanes L;
+    L.o = L.p = L.e = ~0ull;
+    L.so = 0;
+    L.h[0] = L.h[1] = L.h[2] = 0;
+    if (base + lane < a.n_msgs) {
+        const wsc_out_msg mj = a.msgs[base + lane];
+        L.o = a.out_off[base + lane];
+        L.p = L.o + enc_hlen(mj.len);
+        L.e = L.p + mj.len;
+        uint32_t h[4];
+        enc_header(mj.first_byte, mj.len, h);
+        L.h[0] = h[0];
+        L.h[1] = h[1];
+        L.h[2] = h[2];
+        L.so = (int64_t)mj.src_off - (int64_t)L.p;
+    }
+    return L;
+}
+
 template <int NT>
-__device__ __forceinline__ bool encode_window_lanes(const EncCopyArgs& a, uint32_t m, uint64_t wbase, uint64_t limit,
-                                                    uint32_t lane, const u32x4* __restrict__ pm,
+__device__ __forceinline__ bool encode_window_lanes(const EncCopyArgs& a, const EncLanes& L, uint32_t base, uint64_t wbase,
+                                                    uint64_t limit, uint32_t lane, const u32x4* __restrict__ pm,
                                                     uint16_t* __restrict__ elist) {
     constexpr uint32_t P = ENC_WIN / 1024;
     constexpr int64_t WB = ENC_WIN;
-    auto clip = [](int64_t x) -> int32_t { return (int32_t)(x < -(1ll << 30) ? -(1ll << 30) : (x > WB + 64 ? WB + 64 : x)); };
-    const uint32_t fj = m + lane;
-    int32_t ro = (int32_t)WB + 64, rp = ro, re = ro;   // window-relative header start, payload start, end
-    uint32_t h[4] = {0, 0, 0, 0};
-    int64_t so = 0;                                    // source offset of output byte x: so + x
-    if (fj < a.n_msgs) {
-        const wsc_out_msg mj = a.msgs[fj];
-        const uint64_t o = a.out_off[fj];
-        const uint64_t p = o + enc_hlen(mj.len);
-        ro = clip((int64_t)o - (int64_t)wbase);
-        rp = clip((int64_t)p - (int64_t)wbase);
-        re = clip((int64_t)(p + mj.len) - (int64_t)wbase);
-        enc_header(mj.first_byte, mj.len, h);
-        so = (int64_t)mj.src_off - (int64_t)p;
-    }
+    auto clip = [](uint64_t x, uint64_t wb) -> int32_t {   // x - wb clamped to [-2^30, WB + 64]
+        if (x == ~0ull || x > wb + (uint64_t)(WB + 64)) return (int32_t)WB + 64;
+        return x + (1ull << 30) < wb ? -(1 << 30) : (int32_t)((int64_t)x - (int64_t)wb);
+    };
+    // window-relative header start, payload start, end (lanes before the window's first frame lie
+    // before it: the search below never lands on them)
+    const int32_t ro = clip(L.o, wbase), rp = clip(L.p, wbase), re = clip(L.e, wbase);
+    const uint32_t h[4] = {L.h[0], L.h[1], L.h[2], 0u};
+    const int64_t so = L.so;
     const uint32_t nl = (uint32_t)__builtin_popcountll(__ballot(ro < (int32_t)WB));
-    if (nl == 64 && __shfl(re, 63) < (int32_t)WB && m + 64 < a.n_msgs) return false;
+    if (nl == 64 && __shfl(re, 63) < (int32_t)WB && base + 64 < a.n_msgs) return false;
     const uint32_t so_lo = (uint32_t)so, so_hi = (uint32_t)((uint64_t)so >> 32);
 
     // binary search: the last frame (lane) whose header starts at or before window byte pr; first
@@ -322,62 +343,19 @@ __device__ __forceinline__ bool encode_window_lanes(const EncCopyArgs& a, uint32
     return true;
 }
 
-// ---------------------------------------------------------------------------------------------
-// Copy: one ENC_WIN-byte output window per wave.
-// ---------------------------------------------------------------------------------------------
+// A window with more than 64 frames: frame by frame from m, every lane assembling its P pieces.
 template <int NT>
-__global__ __launch_bounds__(256) void k_encode_copy(EncCopyArgs a) {
+__device__ __forceinline__ void encode_window_serial(const EncCopyArgs& a, uint32_t m, uint64_t wbase, uint64_t limit,
+                                                  uint32_t lane) {
     constexpr uint32_t P = ENC_WIN / 1024;
-    __shared__ u32x4 pm[17];
-    __shared__ uint16_t elist[4][ENC_WIN / 16];   // per wave: the window's edge pieces (pass 2)
-    if (threadIdx.x < 17) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t L = threadIdx.x;
-            const uint32_t nb = L > 4u * j ? (L - 4u * j > 4u ? 4u : L - 4u * j) : 0u;
-            pm[threadIdx.x][j] = nb == 4 ? 0xFFFFFFFFu : ((1u << (8 * nb)) - 1u);
-        }
-    }
-    __syncthreads();
-    // re-arm the scan's look-back state for the next encode (this launch is ordered after it)
-    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < a.n_lb; t += gridDim.x * blockDim.x) a.lb_state[t] = 0;
-    const uint32_t n = a.n_msgs;
-    if (n == 0) return;
-    const uint32_t lane = threadIdx.x & 63;
-    const uint64_t gw = __builtin_amdgcn_readfirstlane(xcd_run_block(blockIdx.x, gridDim.x, a.xcd_run) * 4 +
-                                                       (threadIdx.x >> 6));
-    uint64_t limit = a.out_off[n];
-    if (limit > a.out_cap) limit = a.out_cap;
-    const uint64_t wbase = gw << ENC_WIN_SHIFT;
-    if (wbase >= limit || gw >= a.tile_entries) return;
-    const uint32_t lofs = lane * 16u;
-    uint32_t m = a.tile[gw];
-    const wsc_out_msg mm = a.msgs[m];
-    const uint64_t o = a.out_off[m];
-    const uint64_t p0 = o + enc_hlen(mm.len), p1 = p0 + mm.len;
-    if (p0 <= wbase && p1 >= wbase + ENC_WIN && wbase + ENC_WIN <= limit) {
-        // fast path: the window lies inside one payload -> shifted stream copy, non-temporal loads
-        // (A/B, tools/lib_ab.py: 64 KiB echo batch 0.411 -> 0.396 ms; the lane-parallel windows
-        // keep default loads: their pieces at frame edges re-read lines a neighbour piece loaded,
-        // and nt loads made the 1 KiB batch 3.5 % slower)
-        const int64_t so = (int64_t)mm.src_off - (int64_t)p0;
-        uint4 v[P];
-#pragma unroll
-        for (uint32_t k = 0; k < P; ++k) v[k] = load16u<NT>(a.src, so + (int64_t)(wbase + k * 1024u + lofs), a.src_bytes);
-#pragma unroll
-        for (uint32_t k = 0; k < P; ++k) enc_st<NT>(a.out, wbase, wbase + k * 1024u + lofs, u32x4{v[k].x, v[k].y, v[k].z, v[k].w});
-        return;
-    }
-    // general path: frame edges in the window -> lane-parallel frame lookup (serial walk over the
-    // frames only when more than 64 of them overlap the window)
-    if (encode_window_lanes<NT>(a, m, wbase, limit, lane, pm, elist[threadIdx.x >> 6])) return;
+    const uint32_t lofs = lane * 16u, n = a.n_msgs;
     uint4 acc[P];
 #pragma unroll
     for (uint32_t k = 0; k < P; ++k) acc[k] = make_uint4(0, 0, 0, 0);
     for (uint32_t j = m; j < n; ++j) {
-        const uint64_t oj = j == m ? o : a.out_off[j];
+        const uint64_t oj = a.out_off[j];
         if (oj >= wbase + ENC_WIN) break;
-        const wsc_out_msg mj = j == m ? mm : a.msgs[j];
+        const wsc_out_msg mj = a.msgs[j];
         const uint32_t hl = enc_hlen(mj.len);
         uint32_t h[4];
         enc_header(mj.first_byte, mj.len, h);
@@ -420,6 +398,67 @@ __global__ __launch_bounds__(256) void k_encode_copy(EncCopyArgs a) {
                 if (pa + b < limit) a.out[pa + b] = (uint8_t)(d[b >> 2] >> (8 * (b & 3)));
         }
     }
+}
+
+// fast path: the window lies inside one payload -> shifted stream copy, non-temporal loads (A/B,
+// tools/lib_ab.py: 64 KiB echo batch 0.411 -> 0.396 ms; the lane-parallel windows keep default
+// loads: their pieces at frame edges re-read lines a neighbour piece loaded, and nt loads made the
+// 1 KiB batch 3.5 % slower)
+template <int NT>
+__device__ __forceinline__ void encode_window_inside(const EncCopyArgs& a, int64_t so, uint64_t wbase, uint32_t lane) {
+    constexpr uint32_t P = ENC_WIN / 1024;
+    const uint32_t lofs = lane * 16u;
+    uint4 v[P];
+#pragma unroll
+    for (uint32_t k = 0; k < P; ++k) v[k] = load16u<NT>(a.src, so + (int64_t)(wbase + k * 1024u + lofs), a.src_bytes);
+#pragma unroll
+    for (uint32_t k = 0; k < P; ++k) enc_st<NT>(a.out, wbase, wbase + k * 1024u + lofs, u32x4{v[k].x, v[k].y, v[k].z, v[k].w});
+}
+
+__device__ __forceinline__ void enc_pm_init(u32x4* pm) {
+    if (threadIdx.x < 17) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t L = threadIdx.x;
+            const uint32_t nb = L > 4u * j ? (L - 4u * j > 4u ? 4u : L - 4u * j) : 0u;
+            pm[threadIdx.x][j] = nb == 4 ? 0xFFFFFFFFu : ((1u << (8 * nb)) - 1u);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Copy: one ENC_WIN-byte output window per wave.
+// ---------------------------------------------------------------------------------------------
+template <int NT>
+__global__ __launch_bounds__(256) void k_encode_copy(EncCopyArgs a) {
+    __shared__ u32x4 pm[17];
+    __shared__ uint16_t elist[4][ENC_WIN / 16];   // per wave: the window's edge pieces (pass 2)
+    enc_pm_init(pm);
+    __syncthreads();
+    // re-arm the scan's look-back state for the next encode (this launch is ordered after it)
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < a.n_lb; t += gridDim.x * blockDim.x) a.lb_state[t] = 0;
+    const uint32_t n = a.n_msgs;
+    if (n == 0) return;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t gw = __builtin_amdgcn_readfirstlane(xcd_run_block(blockIdx.x, gridDim.x, a.xcd_run) * 4 +
+                                                       (threadIdx.x >> 6));
+    uint64_t limit = a.out_off[n];
+    if (limit > a.out_cap) limit = a.out_cap;
+    const uint64_t wbase = gw << ENC_WIN_SHIFT;
+    if (wbase >= limit || gw >= a.tile_entries) return;
+    const uint32_t m = a.tile[gw];
+    const wsc_out_msg mm = a.msgs[m];
+    const uint64_t o = a.out_off[m];
+    const uint64_t p0 = o + enc_hlen(mm.len), p1 = p0 + mm.len;
+    if (p0 <= wbase && p1 >= wbase + ENC_WIN && wbase + ENC_WIN <= limit) {
+        encode_window_inside<NT>(a, (int64_t)mm.src_off - (int64_t)p0, wbase, lane);
+        return;
+    }
+    // general path: frame edges in the window -> lane-parallel frame lookup (serial walk over the
+    // frames only when more than 64 of them overlap the window)
+    const EncLanes L = enc_lanes_load(a, m, lane);
+    if (encode_window_lanes<NT>(a, L, m, wbase, limit, lane, pm, elist[threadIdx.x >> 6])) return;
+    encode_window_serial<NT>(a, m, wbase, limit, lane);
 }
 
 template __global__ void k_encode_scan<1>(EncArgs);
