@@ -65,7 +65,14 @@ def test_cpu_echo_shutdown(cpu_echo, pollers):
                                   ("--conns", "64", "--frames", "60", "--size", "65536", "--client-threads", "4",
                                    "--pollers", "4"),
                                   ("--conns", "64", "--frames", "400", "--size", "1024", "--client-threads", "4",
-                                   "--pollers", "4", "--sync")])
+                                   "--pollers", "4", "--sync"),
+                                  # one batching thread per device sharing one session among the pollers
+                                  ("--conns", "64", "--frames", "60", "--size", "65536", "--client-threads", "4",
+                                   "--pollers", "4", "--batcher"),
+                                  # blocking-sync completion, reads cut at an odd size (frames split
+                                  # across reads and rounds)
+                                  ("--conns", "64", "--frames", "60", "--size", "65536", "--client-threads", "4",
+                                   "--pollers", "8", "--blocking-wait", "--read-bytes", "100003")])
 def test_gpu_echo_roundtrip(codec_lib, args):
     from netman_amd import _build
     exe = _build.build_tools()
