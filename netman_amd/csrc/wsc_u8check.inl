@@ -166,11 +166,6 @@ __device__ __forceinline__ void u8_remask(const U8Args& a, uint32_t seg, uint64_
 #ifndef WSC_CHECK_PREFETCH
 #define WSC_CHECK_PREFETCH 0
 #endif
-// WSC_U8_DIRECT 1 (A/B): a small unit's lanes load their own 64-byte chunk (row r = item r, lane
-// 64 B apart) instead of coalesced 1 KiB pieces restaged through LDS
-#ifndef WSC_U8_DIRECT
-#define WSC_U8_DIRECT 0
-#endif
 // WPB: waves per workgroup (4: 256-thread workgroups; 16: one 1024-thread workgroup per CU, a
 // quarter of the workgroups to dispatch for the same waves)
 template <uint32_t NCH, uint32_t WPB = 4>
@@ -339,18 +334,6 @@ __device__ __forceinline__ void u8_check_run(const U8Args& a, U8Lds& T, uint4 (*
     };
     // piece k of a small unit's step = item k's KiB (16 B per lane, coalesced)
     auto unit_data = [&](const UnitS& x, u32x4 (&q)[4]) {
-        if constexpr (WSC_U8_DIRECT != 0) {
-            const uint32_t r = lane >> 4, j = lane & 15;
-            const uint64_t src = r == 0 ? x.src[0] : (r == 1 ? x.src[1] : (r == 2 ? x.src[2] : x.src[3]));
-            const uint32_t len = r == 0 ? x.len[0] : (r == 1 ? x.len[1] : (r == 2 ? x.len[2] : x.len[3]));
-#pragma unroll
-            for (uint32_t k = 0; k < 4; ++k) {
-                const uint32_t off = 64u * j + 16u * k;
-                const uint4 t = off < len ? load16_unaligned(a.wire, (int64_t)(src + off), a.n_bytes) : make_uint4(0, 0, 0, 0);
-                q[k] = u32x4{t.x, t.y, t.z, t.w};
-            }
-            return;
-        }
 #pragma unroll
         for (uint32_t k = 0; k < 4; ++k) {
             const uint4 t = 16u * lane < x.len[k] ? load16_unaligned(a.wire, (int64_t)(x.src[k] + 16u * lane), a.n_bytes)
@@ -389,7 +372,7 @@ __device__ __forceinline__ void u8_check_run(const U8Args& a, U8Lds& T, uint4 (*
             const U8Item xr = a.items[i0 + (r < cnt ? r : 0u)];
             const uint32_t rlen = r < cnt ? xr.len : 0u;   // (row r's fields from its item: no selects)
             const uint32_t rmask = xr.mask;
-            if (!WSC_U8_DIRECT) u8_restage(sw, qc, lane);
+            u8_restage(sw, qc, lane);
             const uint32_t off = (lane & 15) * 64;
             bool plain;
             const uint64_t pm = u8_chunk_map<NCH, U8P_LANE>(T, qc, a.unmasked ? 0u : rmask, chunk_len(rlen, off), plain);
