@@ -14,8 +14,10 @@
 //   WSC_EV_NONE     (nil, syscall.EAGAIN)
 //
 // Data path (per poller round): socket -> pinned staging (the one host copy, done by recv) -> H2D
-// -> header walk + unmask (HBM) -> D2H into a pinned result buffer -> messages handed out as views
-// into it.  Two staging sets, each with its own device context and HIP stream, so round r+1's
+// (a kernel reading the staging over PCIe, wsc_kcopy: a hipMemcpyAsync held the poller thread for
+// the copy) -> header walk + unmask (HBM) -> D2H into a pinned result buffer -> messages handed
+// out as views into it, valid until the next complete (a server can send replies straight from
+// them).  Two staging sets, each with its own device context and HIP stream, so round r+1's
 // H2D + kernels run while the poller sends round r's replies (submit/complete).  A connection's
 // undecoded tail (an incomplete frame) is kept on the host (Conn::carry) and placed in front of
 // its next bytes.
