@@ -46,7 +46,6 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-host-inclusive", action="store_true")
-    ap.add_argument("--window", type=int, default=0, help="unmask window bytes (0 = library default)")
     ap.add_argument("--waves-per-cu", type=int, default=0)
     ap.add_argument("--pipeline", type=int, default=2,
                     help="batches in flight: each has its own context, wire buffer and HIP stream, so the "
@@ -175,8 +174,6 @@ def main():
     n_bytes = len(cfg["wire"])
     n_segs = len(cfg["seg_off"]) - 1
     over = dict(max_batch_bytes=n_bytes + 4096, max_segs=n_segs, max_frames=a.frames + 16)
-    if a.window:
-        over["unmask_window"] = a.window
     if a.waves_per_cu:
         over["unmask_waves_per_cu"] = a.waves_per_cu
     P = max(1, a.pipeline)
@@ -627,7 +624,7 @@ def other_configs(torch, K, synth, only=None):
         e1.record(st)
         torch.cuda.synchronize()
         two_ms = float(e0.elapsed_time(e1)) / 100
-        best = None
+        best, serial_ms = None, float("nan")
         for wcus, rest in PIPELINE_SPLITS:
             if wcus < 0:
                 ws = us = c.stream_create(None)
@@ -654,6 +651,8 @@ def other_configs(torch, K, synth, only=None):
             c.stream_destroy(ws)
             if us != ws:
                 c.stream_destroy(us)
+            if wcus < 0:
+                serial_ms = pms
             if best is None or pms < best[0]:
                 best = (pms, wcus, rest)
         pms, wcus, rest = best
@@ -667,6 +666,10 @@ def other_configs(torch, K, synth, only=None):
                      "pipelined_walk_cus": wcus if wcus > 0 else ("all, high-priority stream" if wcus == 0 else
                                                                   "serial: walks and unmasks in order on one stream"),
                      "pipelined_unmask_cus": "the other CUs" if rest else "all",
+                     # the best candidate can be the serial order (no overlap at all): say so, and
+                     # give the serial time on its own (round-5 ADVICE)
+                     "pipelined_is_serial": wcus < 0,
+                     "serial_ms_per_batch": round(serial_ms, 4),
                      "two_buffers_ms": round(two_ms, 4),
                      "frames": int(cfg["n_frames"]), "payload_bytes": int(cfg["payload_bytes"]), "alg_bytes": alg,
                      "device_errors": not ok}

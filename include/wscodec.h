@@ -28,10 +28,13 @@
 extern "C" {
 #endif
 
-#define WSC_ABI_VERSION 4   /* 2: wsc_frame.payload_len_hi (40-bit payload lengths), staged split;
+#define WSC_ABI_VERSION 5   /* 2: wsc_frame.payload_len_hi (40-bit payload lengths), staged split;
                                3: payloads streamed across batches (wsc_conn_state.frame_*, WSC_FK_PIECE);
                                4: PONG payloads stream too (wsc_conn_state.frame_utf8), session EOF,
-                                  no-progress guard and per-connection message cap */
+                                  no-progress guard and per-connection message cap;
+                               5: no environment variable is read: the walk variants the tests pin are
+                                  wsc_config fields (walk_mode, u8_inline_max, walk_flags), the
+                                  session's are wsc_session_create flags; wsc_session_inject_fault */
 
 /* ---- return codes --------------------------------------------------------------------------- */
 #define WSC_OK 0
@@ -119,6 +122,11 @@ extern "C" {
                                              spinning in hipStreamSynchronize: the poller's core is
                                              free for recv/send while the device works (many pollers
                                              on few cores)                                          */
+#define WSC_SESSION_TIMING 0x200          /* diagnostics: seconds per phase (pack, launch, device
+                                             wait, harvest) printed to stderr at destroy            */
+#define WSC_SESSION_COPY_ENGINE 0x400     /* every staging copy by hipMemcpyAsync (the copy engines);
+                                             by default the wire's H2D is a wsc_kcopy kernel        */
+#define WSC_SESSION_KCOPY_ALL 0x800       /* every staging copy by wsc_kcopy kernels                */
 
 /* Decoder state carried between batches for one connection (subset of websocket.go:38-56).   */
 typedef struct wsc_conn_state {
@@ -206,12 +214,27 @@ typedef struct wsc_config {
                                   default: the record width; the reference has no limit until
                                   make() fails, Q4).  Independent of max_batch_bytes: payloads
                                   stream across batches                                          */
-    uint32_t unmask_window;    /* bytes per wave-window in the unmask kernel: 4096 / 8192 (0 = 4096) */
-    uint32_t unmask_waves_per_cu; /* unmask grid sizing (0 = default)                            */
-    uint32_t unmask_nt;        /* in place: bit0 non-temporal payload loads, bit1 non-temporal    */
-                               /* stores; COMPACT: bits 2 and 3 likewise                          */
+    uint32_t unmask_window;    /* bytes per wave-window in the unmask kernel: 4096 (0 = 4096)       */
+    uint32_t unmask_waves_per_cu; /* unmask grid sizing (0 = one window per wave, the default)    */
+    uint32_t unmask_nt;        /* cache policy of the unmask: 0 or the default (in place: non-temporal
+                                  loads and stores; COMPACT: non-temporal loads); other policies were
+                                  measured slower and are not built (WSC_E_INVAL)                  */
     uint32_t unmask_minw;      /* reserved (0); was an occupancy hint, measured no gain        */
+    /* ABI 5: the header-walk variants (same results; tests pin them, wsc_walk_info reports them) */
+    uint32_t walk_mode;        /* 0 = automatic; 16, 32, 64, 65, 66, 256, 257 (fused walks) or 3 (the
+                                  tiled walk) pins the geometry                                    */
+    uint32_t u8_inline_max;    /* TEXT payloads up to this many bytes are UTF-8 validated inside the
+                                  walk, larger ones chip-wide after the unmask (default 256; 0 = all
+                                  chip-wide; values above 4095 act as 4095)                        */
+    uint32_t walk_flags;       /* WSC_WALK_* below (default 0)                                      */
+    uint32_t pad;
 } wsc_config;
+
+#define WSC_WALK_NO_QUAD_PRE 0x1   /* the fused walk without its quad pre-pass (modes 65, 16)        */
+#define WSC_WALK_NO_HDR_CACHE 0x2  /* the tiled walk re-reads each segment's first header          */
+#define WSC_WALK_HDR_NT 0x4        /* non-temporal header loads for in-place batches too (COMPACT
+                                      batches always use them)                                      */
+#define WSC_WALK_DEBUG_STAMPS 0x8  /* per-block s_memrealtime stamps of the walk (wsc_debug_stamps) */
 
 typedef struct wsc_ctx wsc_ctx;
 
@@ -330,14 +353,14 @@ int wsc_encode_host(wsc_ctx* ctx, const wsc_out_msg* msgs, uint32_t n_msgs, cons
  * [5] = whole decode.  A context runs one decode at a time (its scratch is shared). */
 int wsc_profile(wsc_ctx* ctx, const wsc_batch* batch, int iters, double* out_ms);
 
-/* Diagnostics: with WSC_DEBUG_STAMPS=1 in the environment at wsc_create, the header-walk kernel
+/* Diagnostics: with WSC_WALK_DEBUG_STAMPS in wsc_config.walk_flags at wsc_create, the header-walk kernel
  * records per block 8 u64 slots of s_memrealtime stamps (100 MHz): start, counted, look-back done,
  * emitted, quad pre-pass done (0 if none), 3 reserved.  `out` has room for 8 * max_blocks.     */
 int wsc_debug_stamps(wsc_ctx* ctx, uint64_t* out, uint32_t max_blocks);
 
 /* Diagnostics: the header-walk geometry the context's last decode launched (*mode: 16, 32, 64, 65,
  * 66, 256, 257 = fused walks, 3 = tiled or three-launch; 0 before any decode) and its block count.
- * Tests use it to check that a geometry pinned with WSC_WALK_MODE really ran.                   */
+ * Tests use it to check that a geometry pinned with wsc_config.walk_mode really ran.            */
 int wsc_walk_info(wsc_ctx* ctx, uint32_t* mode, uint32_t* blocks);
 
 /* ---- session: the per-connection DecodePacket() mirror (C++ host side above the ABI) ---------
@@ -462,6 +485,9 @@ int wsc_session_state(wsc_session* s, uint32_t conn, wsc_conn_state* st, uint64_
  * control frames), out[3] batches, out[4] bytes of streamed payload pieces delivered into
  * messages.  n = how many of these to write (<= 5).                                            */
 int wsc_session_stats(wsc_session* s, uint64_t* out, uint32_t n);
+/* Test hook: the session's k-th device submission from now (k >= 1; 0 = off) fails as a failed
+ * launch would (WSC_E_DEVICE): its connections get the 1011 closes of the device-failure rule.    */
+int wsc_session_inject_fault(wsc_session* s, uint64_t k);
 
 #ifdef __cplusplus
 }

@@ -19,8 +19,7 @@ from dataclasses import dataclass
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-# WSC_LIB: an alternative build of the same library (A/B timing experiments in tools/ only)
-LIB_PATH = os.environ.get("WSC_LIB") or os.path.join(HERE, "libwscodec.so")
+LIB_PATH = os.path.join(HERE, "libwscodec.so")
 
 # ---- constants (include/wscodec.h) -------------------------------------------------------------
 WSC_OK = 0
@@ -39,6 +38,11 @@ FF_UNMASKED, FF_CONT_MSG, FF_CTRL_ARENA, FF_HEAD_PREV = 0x01, 0x02, 0x40, 0x80
 SEG_OPEN, SEG_CLOSED, SEG_ERROR, SEG_STALLED = 0, 1, 2, 3
 F_COMPACT = 0x1
 SESSION_BLOCKING_WAIT = 0x100   # wsc_session_create: complete() sleeps on a blocking-sync event
+SESSION_TIMING = 0x200          # ... seconds per phase printed to stderr at destroy
+SESSION_COPY_ENGINE = 0x400     # ... every staging copy by hipMemcpyAsync
+SESSION_KCOPY_ALL = 0x800       # ... every staging copy by wsc_kcopy kernels
+# wsc_config.walk_flags (header-walk variants with the same results; tests pin them)
+WALK_NO_QUAD_PRE, WALK_NO_HDR_CACHE, WALK_HDR_NT, WALK_DEBUG_STAMPS = 0x1, 0x2, 0x4, 0x8
 
 EV_NONE, EV_MESSAGE, EV_PONG, EV_CLOSE, EV_STALL = 0, 1, 2, 3, 4
 
@@ -71,7 +75,9 @@ assert OUT_MSG_DTYPE.itemsize == 24
 class WscConfig(C.Structure):
     _fields_ = [("max_batch_bytes", C.c_uint64), ("max_segs", C.c_uint32), ("max_frames", C.c_uint32),
                 ("max_frame_len", C.c_uint64), ("unmask_window", C.c_uint32),
-                ("unmask_waves_per_cu", C.c_uint32), ("unmask_nt", C.c_uint32), ("unmask_minw", C.c_uint32)]
+                ("unmask_waves_per_cu", C.c_uint32), ("unmask_nt", C.c_uint32), ("unmask_minw", C.c_uint32),
+                ("walk_mode", C.c_uint32), ("u8_inline_max", C.c_uint32), ("walk_flags", C.c_uint32),
+                ("pad", C.c_uint32)]
 
 
 class WscBatch(C.Structure):
@@ -142,10 +148,11 @@ SIGNATURES = {
     "wsc_session_set_max_message": (_I, [_P, _U64]),
     "wsc_session_state": (_I, [_P, _U32, C.POINTER(WscConnState), C.POINTER(_U64)]),
     "wsc_session_stats": (_I, [_P, C.POINTER(_U64), _U32]),
+    "wsc_session_inject_fault": (_I, [_P, _U64]),
 }
 
 _lib = None
-ABI_VERSION = 4   # include/wscodec.h WSC_ABI_VERSION: the record layouts above
+ABI_VERSION = 5   # include/wscodec.h WSC_ABI_VERSION: the record layouts above
 
 
 def load_library(path: str = LIB_PATH):
@@ -186,11 +193,17 @@ def _check(rc: int, where: str):
         raise WscError(rc, where)
 
 
+# Process-wide overrides of wsc_config fields applied by default_config() under its own keyword
+# arguments: lets a test pin a walk variant (walk_mode, u8_inline_max, walk_flags) for every context
+# it creates, helpers included.  An explicit Python API -- nothing reads the environment.
+CFG_DEFAULTS: dict = {}
+
+
 def default_config(**over) -> WscConfig:
     lib = load_library()
     cfg = WscConfig()
     _check(lib.wsc_config_default(C.byref(cfg)), "wsc_config_default")
-    for k, v in over.items():
+    for k, v in {**CFG_DEFAULTS, **over}.items():
         setattr(cfg, k, v)
     return cfg
 
@@ -560,6 +573,10 @@ class Session:
     def eof(self, conn: int):
         """the peer closed (a read returned 0): wsc_session_eof -- queued events first, then Close()"""
         _check(self.lib.wsc_session_eof(self.h, conn), "wsc_session_eof")
+
+    def inject_fault(self, k: int):
+        """test hook: the k-th device submission from now fails as a device error would"""
+        _check(self.lib.wsc_session_inject_fault(self.h, int(k)), "wsc_session_inject_fault")
 
     def set_max_message(self, nbytes: int):
         _check(self.lib.wsc_session_set_max_message(self.h, int(nbytes)), "wsc_session_set_max_message")

@@ -17,9 +17,6 @@
 namespace wsc {
 template <bool COMPACT, uint32_t KR, uint32_t NT, uint32_t G, uint32_t WL, uint32_t SPREAD> __global__ void k_walk_fused(WalkArgs);
 template <bool COMPACT, uint32_t KR, uint32_t NT> __global__ void k_walk_tiled(WalkArgs, uint32_t);
-template <bool COMPACT> __global__ void k_walk_count(WalkArgs);
-__global__ void k_walk_scan(WalkArgs, uint32_t);
-template <bool COMPACT> __global__ void k_walk_emit(WalkArgs);
 template <uint32_t NCH, uint32_t WPB> __global__ void k_u8_check(U8Args);
 template <bool COMPACT, int P, int NT, int MINW, bool U8>
 __global__ void k_unmask(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*,
@@ -74,11 +71,14 @@ struct wsc_ctx {
     bool fin_pending = false;         // a staged unmask was enqueued without ev_done
     hipStream_t fin_stream = nullptr; // ... on this stream
     bool walk_waited = false;         // wsc_walk_wait saw the last walk complete
-    int u8_chains = 4;                // WSC_U8_CHAINS: independent byte chains per 64-byte lane chunk (1, 2, 4);
-                                      // 4: 1 KiB TEXT 0.241 -> 0.238 ms (A/B, one box), 64 KiB TEXT unchanged
-    int unmask_buf = 3;               // WSC_UNMASK_BUF: in-place windows through buffer ops (1 nt, 2 nt sc1, 3 sc0 nt sc1
-                                      // stores; 0 = 64-bit global addresses).  3: headline 2,890-2,898 -> 2,911-2,918
-                                      // GiB/s (A/B on one box, profiles/r02_unmask_policy.log)
+    // Measured-and-rejected variants are not built into this library (tools/build_variant.sh builds
+    // them for A/B runs); nothing here reads the environment.  The fixed choices, with their A/Bs:
+    //  - k_u8_check: 4 independent byte chains per 64-byte lane chunk, 256-lane workgroups, 4 per CU
+    //    (1 KiB TEXT 0.241 -> 0.238 ms vs 2 chains; 1,024-lane workgroups slower on text, round 5)
+    //  - in-place unmask windows through buffer ops, sc0 nt sc1 stores (headline 2,890-2,898 ->
+    //    2,911-2,918 GiB/s, profiles/r02_unmask_policy.log); 4 KiB windows (r01_tune_*)
+    //  - walk look-back order by ticket (hardware order measured slower, r04_walk_hw_order_ab.log);
+    //    walk waves at raised issue priority (neutral, round 5)
     wsc_config cfg{};
     uint32_t pieces = 8;          // 16 B pieces per lane -> window = pieces KiB
     uint32_t* sticky = nullptr;      // error bits of every decode/encode (wsc_error_flags), never re-armed
@@ -86,7 +86,7 @@ struct wsc_ctx {
     uint32_t* u8info = nullptr;      // per segment {utf8-failing frame ordinal, DFA state}
     uint64_t* lb_agg = nullptr;
     uint64_t* lb_incl = nullptr;
-    uint64_t* dbg = nullptr;         // WSC_DEBUG_STAMPS=1: per-block walk timestamps
+    uint64_t* dbg = nullptr;         // WSC_WALK_DEBUG_STAMPS: per-block walk timestamps
     Span* spans = nullptr;
     uint32_t* tile = nullptr;
     // chip-wide UTF-8 (k_u8_check): deferred items, their maps, per-segment lists
@@ -101,28 +101,18 @@ struct wsc_ctx {
     uint32_t u8par = 0;                 // parity of the decode the last walk belongs to
     bool u8_dirty = false;              // a walk was launched whose unmask (which zeroes the next decode's item
                                         // counter) was not: the next walk zeroes its counter itself
-    uint32_t u8_inline_max = 256;
-    uint32_t u8_grid = 0;               // WSC_U8_GRID: k_u8_check workgroups (A/B experiments; 0 = 5 per CU)
-    uint32_t u8_wpb = 4;                // WSC_U8_WPB: k_u8_check waves per workgroup (4, or 16 = 1024-thread workgroups)
-    bool walk_tiled = true;             // WSC_WALK_TILED=0: the three-launch walk for mode 3 (A/B)
-    int hdr_nt = -1;                    // WSC_HDR_NT: the walk's header loads non-temporal: 0 never, 1 always, default COMPACT batches
-    bool walk_hw_order = false;         // WSC_WALK_HW_ORDER=1: walk blocks ordered by workgroup index, not a ticket
-    uint32_t enc_ipt = 0;               // WSC_ENC_IPT=1|4|16: pin the encode scan's messages per thread (A/B)
-    bool enc_buf = false;               // WSC_ENC_BUF=1: the encode copy's stores as buffer stores (sc0 nt sc1)
-    bool walk_prio = true;              // WSC_WALK_PRIO=0: the walk's waves keep the default issue priority
-    bool quad_pre = true;               // WSC_QUAD_PRE=0: the fused walk without its quad pre-pass (A/B)
-    uint32_t xcd_run = 8;               // WSC_XCD_RUN: unmask blocks per XCD run (1 = the hardware deal; one run
-                                        // per XCD over the whole grid measured slower: headline 0.347 -> 0.359 ms)
-    uint32_t enc_xcd_run = 1;           // WSC_ENC_XCD_RUN: the same for the encode copy (8 measured 0.381 ->
-                                        // 0.383-0.399 ms at 64 KiB, no change at 1 KiB: off)
-    bool ab_no_u8 = false;              // WSC_AB_NO_U8=1: A/B timing only -- binary unmask, no UTF-8 launches
-                                        // (wrong for text batches; never set in tests or the bench)
-    int walk_mode = 0;                  // WSC_WALK_MODE: 16, 32, 64, 65, 66, 256 or 3 pins the walk geometry (A/B, tests); 0 = auto
+    uint32_t u8_inline_max = 256;       // wsc_config.u8_inline_max
+    bool hdr_nt_all = false;            // WSC_WALK_HDR_NT: non-temporal header loads in place too (COMPACT always)
+    bool quad_pre = true;               // !WSC_WALK_NO_QUAD_PRE
+    static constexpr uint32_t xcd_run = 8;       // unmask blocks per XCD run (1 = the hardware deal; one run per
+                                                 // XCD over the whole grid measured slower: 0.347 -> 0.359 ms)
+    static constexpr uint32_t enc_xcd_run = 1;   // the same for the encode copy (8 measured 0.381 -> 0.383-0.399
+                                                 // ms at 64 KiB, no change at 1 KiB: off)
+    int walk_mode = 0;                  // wsc_config.walk_mode: 16, 32, 64, 65, 66, 256, 257 or 3 pins the geometry; 0 = auto
     uint32_t walk_used = 0;             // geometry (64 / 256 / 3) and block count of the last walk launched:
     uint32_t walk_blocks = 0;           // the staged unmask re-arms exactly that walk's look-back flags
     uint32_t max_walk_blocks = 0;       // look-back state allocated for this many walk blocks
-    SegCount* counts = nullptr;         // three-launch walk: per-segment counts
-    uint4* hdr_cache = nullptr;         // tiled walk: per segment, its first 16 header bytes (WSC_HDR_CACHE=0: off)
+    uint4* hdr_cache = nullptr;         // tiled walk: per segment, its first 16 header bytes (WSC_WALK_NO_HDR_CACHE: off)
     uint32_t* stride_hint = nullptr;    // quad pre-pass: the frame stride the last decode ended with
     uint64_t tile_entries = 0;
     // host-staged path buffers (lazily allocated)
@@ -227,8 +217,12 @@ int wsc_config_default(wsc_config* cfg) {
                                      // those partial lines to HBM separately: configs[4] wrote 2,570 MB for
                                      // 2,419 MB of payload, default stores 2,426 MB, decode time unchanged
                                      // (0.999 vs 1.001 ms back to back, profiles/r04_compact_store_policy.log)
+    cfg->walk_mode = 0;
+    cfg->u8_inline_max = 256;
+    cfg->walk_flags = 0;
     return WSC_OK;
 }
+static constexpr uint32_t UNMASK_NT_DEFAULT = 3 | 1 << 2;
 
 static int alloc_host_path(wsc_ctx* c) {
     if (c->d_wire) return WSC_OK;
@@ -261,9 +255,17 @@ int wsc_create(int device, const wsc_config* cfg_in, wsc_ctx** out) {
     if (cfg.max_segs == 0 || cfg.max_frames == 0 || cfg.max_batch_bytes == 0)
         return fail(WSC_E_INVAL, "zero capacity in config");
     if (cfg.max_frame_len > 0xFFFFFFFFFFull) return fail(WSC_E_INVAL, "max_frame_len > 2^40-1");
-    uint32_t win = cfg.unmask_window ? cfg.unmask_window : 4096;
-    if (win != 4096 && win != 8192) return fail(WSC_E_INVAL, "unmask_window must be 4096 or 8192");
+    // only the measured defaults are built (8 KiB windows and the other cache policies: A/B builds)
+    const uint32_t win = cfg.unmask_window ? cfg.unmask_window : 4096;
+    if (win != 4096) return fail(WSC_E_INVAL, "unmask_window must be 4096 (or 0)");
     cfg.unmask_window = win;
+    if (cfg.unmask_nt == 0) cfg.unmask_nt = UNMASK_NT_DEFAULT;
+    if (cfg.unmask_nt != UNMASK_NT_DEFAULT) return fail(WSC_E_INVAL, "unmask_nt must be the default (or 0)");
+    const uint32_t wm = cfg.walk_mode;
+    if (!(wm == 0 || wm == 16 || wm == 32 || wm == 64 || wm == 65 || wm == 66 || wm == 256 || wm == 257 || wm == 3))
+        return fail(WSC_E_INVAL, "walk_mode must be 0, 16, 32, 64, 65, 66, 256, 257 or 3");
+    if (cfg.walk_flags & ~(uint32_t)(WSC_WALK_NO_QUAD_PRE | WSC_WALK_NO_HDR_CACHE | WSC_WALK_HDR_NT | WSC_WALK_DEBUG_STAMPS))
+        return fail(WSC_E_INVAL, "unknown walk_flags bits");
 
     HIP_TRY(hipSetDevice(device));
     wsc_ctx* c = new wsc_ctx();
@@ -280,11 +282,7 @@ int wsc_create(int device, const wsc_config* cfg_in, wsc_ctx** out) {
     // record (which writes back and invalidates caches; measured ~13 us between one batch's unmask
     // and the next -- as long as the walk the split was meant to hide).  Kernel ends still release
     // at device scope, which is what the other stream's kernels need.
-    unsigned ev_flags = hipEventDisableTiming | hipEventDisableSystemFence;
-    if (const char* e = std::getenv("WSC_EVENT_FENCE"); e && *e) {   // A/B: 0 system, 1 device, 2 no system fence
-        const int f = std::atoi(e);
-        ev_flags = hipEventDisableTiming | (f == 1 ? hipEventReleaseToDevice : (f == 2 ? hipEventDisableSystemFence : 0u));
-    }
+    const unsigned ev_flags = hipEventDisableTiming | hipEventDisableSystemFence;
     chk(hipEventCreateWithFlags(&c->ev_walked, ev_flags), "hipEventCreate");
     chk(hipEventCreateWithFlags(&c->ev_done, ev_flags), "hipEventCreate");
     chk(hipHostMalloc(&c->hflag, 64, hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc hflag");
@@ -296,8 +294,7 @@ int wsc_create(int device, const wsc_config* cfg_in, wsc_ctx** out) {
     chk(hipMalloc(&c->sticky, sizeof(uint32_t)), "hipMalloc sticky");
     chk(hipMalloc(&c->stride_hint, sizeof(uint32_t)), "hipMalloc stride_hint");
     if (rc == WSC_OK) chk(hipMemsetAsync(c->stride_hint, 0, sizeof(uint32_t), c->stream), "hipMemset stride_hint");
-    chk(hipMalloc(&c->counts, (uint64_t)cfg.max_segs * sizeof(SegCount)), "hipMalloc counts");
-    if (const char* e = std::getenv("WSC_HDR_CACHE"); !(e && e[0] == '0'))
+    if (!(cfg.walk_flags & WSC_WALK_NO_HDR_CACHE))
         chk(hipMalloc(&c->hdr_cache, (uint64_t)cfg.max_segs * sizeof(uint4)), "hipMalloc hdr_cache");
     if (rc == WSC_OK) chk(hipMemsetAsync(c->sticky, 0, sizeof(uint32_t), c->stream), "hipMemset sticky");
     // the most walk blocks (64 segments per block; 16 per block for up to 64 segments per CU); the
@@ -309,7 +306,7 @@ int wsc_create(int device, const wsc_config* cfg_in, wsc_ctx** out) {
     chk(hipMalloc(&c->u8info, (uint64_t)cfg.max_segs * 2 * sizeof(uint32_t)), "hipMalloc u8info");
     chk(hipMalloc(&c->lb_agg, max_blocks * 4 * sizeof(uint64_t)), "hipMalloc lb_agg");
     chk(hipMalloc(&c->lb_incl, max_blocks * 4 * sizeof(uint64_t)), "hipMalloc lb_incl");
-    if (const char* e = std::getenv("WSC_DEBUG_STAMPS"); e && e[0] == '1')
+    if (cfg.walk_flags & WSC_WALK_DEBUG_STAMPS)
         chk(hipMalloc(&c->dbg, max_blocks * 8 * sizeof(uint64_t)), "hipMalloc dbg");
     if (rc == WSC_OK) {
         chk(hipMemsetAsync(c->lb_state, 0, (max_blocks + 3) * sizeof(uint32_t), c->stream), "hipMemset lb_state");
@@ -333,28 +330,10 @@ int wsc_create(int device, const wsc_config* cfg_in, wsc_ctx** out) {
         chk(hipMemsetAsync(c->u8ctr, 0, 64 * sizeof(uint32_t), c->stream), "hipMemset u8ctr");
         chk(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
     }
-    if (const char* e = std::getenv("WSC_UNMASK_BUF"); e && *e) c->unmask_buf = std::atoi(e);
-    if (const char* e = std::getenv("WSC_UNMASK_WPC"); e && *e)   // A/B: persistent unmask grid, waves per CU
-        c->cfg.unmask_waves_per_cu = (uint32_t)std::strtoul(e, nullptr, 10);
-    if (const char* e = std::getenv("WSC_U8_CHAINS"); e && *e) c->u8_chains = std::atoi(e);
-    if (const char* e = std::getenv("WSC_U8_GRID"); e && *e) c->u8_grid = (uint32_t)std::strtoul(e, nullptr, 10);
-    if (const char* e = std::getenv("WSC_U8_WPB"); e && *e) c->u8_wpb = std::atoi(e) == 16 ? 16u : 4u;
-    if (const char* e = std::getenv("WSC_AB_NO_U8"); e && e[0] == '1') c->ab_no_u8 = true;
-    if (const char* e = std::getenv("WSC_WALK_TILED"); e && e[0] == '0') c->walk_tiled = false;
-    if (const char* e = std::getenv("WSC_QUAD_PRE"); e && e[0] == '0') c->quad_pre = false;
-    if (const char* e = std::getenv("WSC_WALK_HW_ORDER"); e && *e) c->walk_hw_order = e[0] == '1';
-    if (const char* e = std::getenv("WSC_HDR_NT"); e && *e) c->hdr_nt = e[0] == '1' ? 1 : 0;
-    if (const char* e = std::getenv("WSC_WALK_PRIO"); e && *e) c->walk_prio = e[0] == '1';
-    if (const char* e = std::getenv("WSC_ENC_BUF"); e && *e) c->enc_buf = e[0] == '1';
-    if (const char* e = std::getenv("WSC_ENC_IPT"); e && *e) c->enc_ipt = (uint32_t)std::strtoul(e, nullptr, 10);
-    if (const char* e = std::getenv("WSC_XCD_RUN"); e && *e) c->xcd_run = (uint32_t)std::strtoul(e, nullptr, 10);
-    if (const char* e = std::getenv("WSC_ENC_XCD_RUN"); e && *e) c->enc_xcd_run = (uint32_t)std::strtoul(e, nullptr, 10);
-    if (const char* e = std::getenv("WSC_WALK_MODE"); e && *e) {   // pin a walk geometry (tests, A/B): 16, 32, 64, 65, 66, 256, 257 or 3
-        const int m = std::atoi(e);
-        c->walk_mode = (m == 16 || m == 32 || m == 64 || m == 65 || m == 66 || m == 256 || m == 257 || m == 3) ? m : 0;
-    }
-    if (const char* e = std::getenv("WSC_U8_INLINE_MAX"); e && *e)   // test knob: 0 sends all text chip-wide
-        c->u8_inline_max = (uint32_t)std::strtoul(e, nullptr, 10);
+    c->quad_pre = !(cfg.walk_flags & WSC_WALK_NO_QUAD_PRE);
+    c->hdr_nt_all = (cfg.walk_flags & WSC_WALK_HDR_NT) != 0;
+    c->walk_mode = (int)cfg.walk_mode;
+    c->u8_inline_max = cfg.u8_inline_max;
     if (c->u8_inline_max >= 4096) c->u8_inline_max = 4095;   // a payload holding a whole window is deferred
     c->enc_blocks = (cfg.max_frames + 255) / 256 + 1;
     c->enc_cap = cfg.max_batch_bytes + 16ull * cfg.max_frames;
@@ -380,7 +359,7 @@ int wsc_destroy(wsc_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     (void)fin_wait(c);
-    void* ptrs[] = {c->fin_ctr, c->dbg, c->sticky, c->counts, c->hdr_cache, c->stride_hint, c->lb_state, c->u8info, c->lb_agg, c->lb_incl, c->spans, c->tile, c->d_wire, c->d_arena,
+    void* ptrs[] = {c->fin_ctr, c->dbg, c->sticky, c->hdr_cache, c->stride_hint, c->lb_state, c->u8info, c->lb_agg, c->lb_incl, c->spans, c->tile, c->d_wire, c->d_arena,
                     c->d_seg_off, c->d_state_in, c->d_state_out, c->d_seg_out, c->d_frames,
                     c->d_frame_dst, c->d_summary, c->enc_lb_state, c->enc_lb_agg, c->enc_lb_incl, c->enc_tile,
                     c->d_enc_msgs, c->d_enc_src, c->d_enc_out, c->d_enc_off, c->u8items, c->u8maps, c->u8seg,
@@ -479,7 +458,6 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     wa.frames_cap = b->frames_cap;
     wa.state_in = b->state_in;
     wa.max_frame_len = c->cfg.max_frame_len;
-    wa.counts = c->counts;
     wa.lb_ticket = c->lb_state;
     wa.lb_flag = c->lb_state + 3;
     wa.u8info = c->u8info;
@@ -511,13 +489,11 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     wa.quad_pre = c->quad_pre ? 1u : 0u;
     wa.hdr_cache = c->hdr_cache;
     wa.stride_hint = c->stride_hint;
-    wa.hw_order = c->walk_hw_order ? 1u : 0u;
-    wa.hdr_nt = (c->hdr_nt < 0 ? compact : c->hdr_nt != 0) ? 1u : 0u;
-    wa.prio = c->walk_prio ? 1u : 0u;
+    wa.hdr_nt = (compact || c->hdr_nt_all) ? 1u : 0u;
 
     // walk geometry: the fused walk with blocks that fill the CUs once (64 lanes for up to 64
     // segments per CU, else 256), or -- for more segments than the chip holds lanes at once -- the
-    // three-launch walk, which never waits on another block
+    // tiled walk (a persistent grid of contiguous segment ranges)
     // (phase 2 -- the staged unmask -- re-arms the look-back state of the walk phase 1 launched,
     // whose geometry followed ITS stream's CUs: recomputing it here from another stream could pick
     // fewer flags and leave stale inclusive prefixes for the next walk)
@@ -551,7 +527,7 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
         HIP_TRY(hipMemsetAsync(c->lb_state, 0, (c->max_walk_blocks + 3) * sizeof(uint32_t), ws));
     }
     // fused: 16 frame records per lane in LDS (segments with more frames re-walk their headers)
-    if (mode == 3 && c->walk_tiled) {
+    if (mode == 3) {
         // tiled: a persistent grid (2 blocks per CU of the walk's stream), contiguous segment ranges
         const uint32_t nb = std::max<uint32_t>(1u, std::min<uint32_t>(2u * stream_cus(c, ws), (n + 255) / 256));
         const uint32_t per = ((n + nb - 1) / nb + 255) / 256 * 256;
@@ -559,14 +535,6 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
         c->walk_blocks = used;
         if (compact) hipLaunchKernelGGL((k_walk_tiled<true, 4, 256>), dim3(used), dim3(256), 0, ws, wa, per);
         else hipLaunchKernelGGL((k_walk_tiled<false, 4, 256>), dim3(used), dim3(256), 0, ws, wa, per);
-    } else if (mode == 3) {
-        if (compact) hipLaunchKernelGGL((k_walk_count<true>), wgrid, wblk, 0, ws, wa);
-        else hipLaunchKernelGGL((k_walk_count<false>), wgrid, wblk, 0, ws, wa);
-        HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL(k_walk_scan, dim3(1), dim3(256), 0, ws, wa, wgrid.x);
-        HIP_TRY(hipGetLastError());
-        if (compact) hipLaunchKernelGGL((k_walk_emit<true>), wgrid, wblk, 0, ws, wa);
-        else hipLaunchKernelGGL((k_walk_emit<false>), wgrid, wblk, 0, ws, wa);
     } else if (compact) {
         if (mode == 65) hipLaunchKernelGGL((k_walk_fused<true, 16, 256, 1, 64, 0>), wgrid, wblk, 0, ws, wa);
         else if (mode == 66) hipLaunchKernelGGL((k_walk_fused<true, 16, 256, 1, 64, 16>), wgrid, wblk, 0, ws, wa);
@@ -588,8 +556,8 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     if (split) HIP_TRY(hipEventRecord(c->ev_walked, ws));
     }   // phase != 2
     if (phase == 1) return WSC_OK;
-    // look-back flags the walk used (the three-launch walk has none): ticket, timeout, flags
-    rearm = (mode == 3 && !c->walk_tiled) ? 1u : c->walk_blocks + 1;
+    // look-back flags the walk used: ticket, timeout, flags
+    rearm = c->walk_blocks + 1;
     // a stream wait is a barrier packet between this unmask and the previous one on st: skipped
     // when the host already knows the walk has finished (the staged pipeline waits for it)
     const bool walked = split && (c->walk_waited || hipEventQuery(c->ev_walked) == hipSuccess);
@@ -599,7 +567,7 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     // deferred UTF-8 (large text) runs after the unmask (which folds the text windows it unmasks):
     // both the fold and the check are skipped when the walk has completed and its host-visible
     // flag says it deferred nothing -- the check would still be a launch between two unmasks
-    const bool need_u8 = !c->ab_no_u8 && !(walked && __atomic_load_n(&c->hflag[0], __ATOMIC_ACQUIRE) == 0);
+    const bool need_u8 = !(walked && __atomic_load_n(&c->hflag[0], __ATOMIC_ACQUIRE) == 0);
     const bool signal = phase == 2;   // staged: the decode's last kernel signals the host, no ev_done
 
     uint8_t* udst = compact ? b->arena : b->wire;
@@ -612,24 +580,12 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     const dim3 ublk(256), ugrid((uint32_t)((waves + 3) / 4));
     using UK = void (*)(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Span*, const uint32_t*,
                         const wsc_summary*, uint32_t*, uint32_t, uint32_t*, uint32_t*, uint32_t, U8Win);
-    // [U8 fold][compact][pieces 4/8][nt 0..3]
-#define WSC_UK(C, P, N, U) k_unmask<C, P, N, 1, U>
-#define WSC_UK4(C, P, U) {WSC_UK(C, P, 0, U), WSC_UK(C, P, 1, U), WSC_UK(C, P, 2, U), WSC_UK(C, P, 3, U)}
-    static const UK table[2][2][2][4] = {
-        {{WSC_UK4(false, 4, false), WSC_UK4(false, 8, false)}, {WSC_UK4(true, 4, false), WSC_UK4(true, 8, false)}},
-        {{WSC_UK4(false, 4, true), WSC_UK4(false, 8, true)}, {WSC_UK4(true, 4, true), WSC_UK4(true, 8, true)}}};
-    const int pi = c->pieces == 4 ? 0 : 1;
-    static const UK table_buf[2][2][3] = {
-        {{WSC_UK(false, 4, 35, false), WSC_UK(false, 4, 291, false), WSC_UK(false, 4, 307, false)},
-         {WSC_UK(false, 8, 35, false), WSC_UK(false, 8, 291, false), WSC_UK(false, 8, 307, false)}},
-        {{WSC_UK(false, 4, 35, true), WSC_UK(false, 4, 291, true), WSC_UK(false, 4, 307, true)},
-         {WSC_UK(false, 8, 35, true), WSC_UK(false, 8, 291, true), WSC_UK(false, 8, 307, true)}}};
-#undef WSC_UK4
-#undef WSC_UK
+    // [U8 fold][compact]: 4 KiB windows; in place through buffer ops with nt loads and sc0 nt sc1
+    // stores (NT = 307), COMPACT with nt loads and default-policy stores (NT = 1)
+    static const UK table[2][2] = {{k_unmask<false, 4, 307, 1, false>, k_unmask<true, 4, 1, 1, false>},
+                                   {k_unmask<false, 4, 307, 1, true>, k_unmask<true, 4, 1, 1, true>}};
     const int ui = need_u8 ? 1 : 0;
-    UK kern = table[ui][compact ? 1 : 0][pi][compact ? (c->cfg.unmask_nt >> 2) & 3 : c->cfg.unmask_nt & 3];
-    if (!compact && (c->cfg.unmask_nt & 3) == 3 && c->unmask_buf > 0 && c->unmask_buf <= 3)
-        kern = table_buf[ui][pi][c->unmask_buf - 1];
+    const UK kern = table[ui][compact ? 1 : 0];
     const bool sig_unmask = signal && !need_u8;
     U8Win uw{};
     uw.rearm = c->u8ctr + 32 * (c->u8par ^ 1u);
@@ -669,13 +625,9 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
         ua.fin_ctr = c->fin_ctr;
         ua.fin_host = signal ? c->hflag + 1 : nullptr;
         ua.fin_seq = c->fin_seq + 1;
-        const dim3 ug(c->u8_grid ? c->u8_grid : (uint32_t)c->n_cu * 4);   // resident: 4 waves/SIMD (128 VGPRs;
-        // 3 waves/SIMD without the large path's spills measured slower: 64 KiB TEXT check 79 -> 95 us)
-        if (c->u8_wpb == 16 && c->u8_chains == 4) hipLaunchKernelGGL((k_u8_check<4, 16>), dim3((ug.x + 3) / 4), dim3(1024), 0, st, ua);
-        else if (c->u8_chains == 1) hipLaunchKernelGGL((k_u8_check<1, 4>), ug, dim3(256), 0, st, ua);
-        else if (c->u8_chains == 4) hipLaunchKernelGGL((k_u8_check<4, 4>), ug, dim3(256), 0, st, ua);
-        else if (c->u8_chains == 8) hipLaunchKernelGGL((k_u8_check<8, 4>), ug, dim3(256), 0, st, ua);
-        else hipLaunchKernelGGL((k_u8_check<2, 4>), ug, dim3(256), 0, st, ua);
+        const dim3 ug((uint32_t)c->n_cu * 4);   // resident: 4 waves/SIMD (128 VGPRs; 3 waves/SIMD without
+        // the large path's spills measured slower: 64 KiB TEXT check 79 -> 95 us)
+        hipLaunchKernelGGL((k_u8_check<4, 4>), ug, dim3(256), 0, st, ua);
         HIP_TRY(hipGetLastError());
     }
     rec(3);
@@ -848,9 +800,8 @@ int wsc_error_flags(wsc_ctx* c, uint32_t* flags, int clear) {
 
 // ---- encode ---------------------------------------------------------------------------------
 // messages per scan thread: the smallest of 1 / 4 / ENC_IPT that keeps the scan within 256 blocks
-// (one per CU); `forced` (WSC_ENC_IPT, A/B only) pins one
-static uint32_t enc_scan_ipt(uint32_t n, uint32_t forced) {
-    if (forced == 1 || forced == 4 || forced == ENC_IPT) return forced;
+// (one per CU)
+static uint32_t enc_scan_ipt(uint32_t n) {
     if (n <= 256u * 256u) return 1;
     if (n <= 256u * 256u * 4u) return 4;
     return ENC_IPT;
@@ -879,7 +830,7 @@ static int launch_encode(wsc_ctx* c, const wsc_out_msg* msgs, uint32_t n, const 
     ea.lb_agg = c->enc_lb_agg;
     ea.lb_incl = c->enc_lb_incl;
     ea.sticky = c->sticky;
-    const uint32_t ipt = enc_scan_ipt(n, c->enc_ipt);
+    const uint32_t ipt = enc_scan_ipt(n);
     const uint32_t sblocks = (n + 256 * ipt - 1) / (256 * ipt);
     if (ipt == 1) hipLaunchKernelGGL(k_encode_scan<1>, dim3(sblocks), dim3(256), 0, st, ea);
     else if (ipt == 4) hipLaunchKernelGGL(k_encode_scan<4>, dim3(sblocks), dim3(256), 0, st, ea);
@@ -902,9 +853,7 @@ static int launch_encode(wsc_ctx* c, const wsc_out_msg* msgs, uint32_t n, const 
     if (wins > c->enc_tile_entries) wins = c->enc_tile_entries;
     if (wins == 0) wins = 1;
     const dim3 cgrid((uint32_t)((wins + 3) / 4));
-    if ((c->cfg.unmask_nt & 3) == 3 && c->enc_buf) hipLaunchKernelGGL(k_encode_copy<17>, cgrid, dim3(256), 0, st, ca);
-    else if ((c->cfg.unmask_nt & 3) == 3) hipLaunchKernelGGL(k_encode_copy<3>, cgrid, dim3(256), 0, st, ca);
-    else hipLaunchKernelGGL(k_encode_copy<0>, cgrid, dim3(256), 0, st, ca);
+    hipLaunchKernelGGL(k_encode_copy<3>, cgrid, dim3(256), 0, st, ca);   // nt loads and stores
     HIP_TRY(hipGetLastError());
     return WSC_OK;
 }
@@ -971,7 +920,7 @@ int wsc_profile(wsc_ctx* c, const wsc_batch* b, int iters, double* out_ms) {
 
 int wsc_debug_stamps(wsc_ctx* c, uint64_t* out, uint32_t max_blocks) {
     if (!c || !out) return fail(WSC_E_INVAL, "NULL argument");
-    if (!c->dbg) return fail(WSC_E_STATE, "context created without WSC_DEBUG_STAMPS=1");
+    if (!c->dbg) return fail(WSC_E_STATE, "context created without WSC_WALK_DEBUG_STAMPS");
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipDeviceSynchronize());
     if (max_blocks > c->max_walk_blocks) max_blocks = c->max_walk_blocks;

@@ -464,8 +464,6 @@ __global__ __launch_bounds__(256) void k_encode_copy(EncCopyArgs a) {
 template __global__ void k_encode_scan<1>(EncArgs);
 template __global__ void k_encode_scan<4>(EncArgs);
 template __global__ void k_encode_scan<16>(EncArgs);
-template __global__ void k_encode_copy<0>(EncCopyArgs);
 template __global__ void k_encode_copy<3>(EncCopyArgs);
-template __global__ void k_encode_copy<17>(EncCopyArgs);
 
 }  // namespace wsc

@@ -953,134 +953,6 @@ __device__ __forceinline__ SegCount lb_load(uint64_t* p) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Three-launch walk for batches of many (short) segments -- more lanes than the chip holds at once,
-// where the fused walk's look-back would wait on blocks that have not started:
-//   k_walk_count  one lane per segment: the counting pass (no LDS records), the segment's counts
-//                 and each block's total
-//   k_walk_scan   one block: exclusive scan of the block totals, batch summary
-//   k_walk_emit   one lane per segment: block prefix + in-block scan of the counts = the segment's
-//                 output offsets; re-walks its (cache-warm) headers and emits
-// No inter-block waiting anywhere; the kernel boundaries order the phases.
-// ---------------------------------------------------------------------------------------------
-template <uint32_t NT>
-__device__ __forceinline__ SegCount block_excl_scan(const SegCount& v, SegCount& total, SegCount* sh_wave) {
-    const uint32_t wl = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const SegCount zero = {};
-    SegCount inc = v;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const SegCount o = sc_shfl_up(inc, d);
-        if (wl >= (uint32_t)d) inc = sc_add(o, inc);
-    }
-    SegCount excl = sc_shfl_up(inc, 1);
-    if (wl == 0) excl = zero;
-    if (wl == 63) sh_wave[wave] = inc;
-    __syncthreads();
-    total = zero;
-#pragma unroll
-    for (uint32_t w = 0; w < NT / 64; ++w) {
-        if (w < wave) excl = sc_add(excl, sh_wave[w]);
-        total = sc_add(total, sh_wave[w]);
-    }
-    return excl;
-}
-
-__device__ __forceinline__ SegCount agg_load(const uint64_t* p) {
-    SegCount v;
-    v.frames = (uint32_t)p[0];
-    v.spans0 = (uint32_t)(p[0] >> 32);
-    v.spans1 = (uint32_t)p[1];
-    v.flags = (uint32_t)(p[1] >> 32);
-    v.bytes0 = p[2];
-    v.bytes1 = p[3];
-    return v;
-}
-__device__ __forceinline__ void agg_store(uint64_t* q, const SegCount& v) {
-    q[0] = (uint64_t)v.frames | ((uint64_t)v.spans0 << 32);
-    q[1] = (uint64_t)v.spans1 | ((uint64_t)v.flags << 32);
-    q[2] = v.bytes0;
-    q[3] = v.bytes1;
-}
-template <bool COMPACT>
-__global__ __launch_bounds__(256) void k_walk_count(WalkArgs a) {
-    __shared__ SegCount sh_wave[4];
-    const uint32_t s = blockIdx.x * 256 + threadIdx.x;
-    const SegCount zero = {};
-    SegCount own = zero;
-    if (s < a.n_segs) {
-        WalkEnd we;
-        own = walk_segment<false, COMPACT, 256>(a, s, zero, zero, nullptr, &we);
-        a.counts[s] = own;
-    }
-    SegCount tot;
-    (void)block_excl_scan<256>(own, tot, sh_wave);
-    if (threadIdx.x == 0) agg_store(a.lb_agg + 4ull * blockIdx.x, tot);   // read by the next launch
-}
-
-// one block: thread t owns the SCAN_PER consecutive block totals starting at t * SCAN_PER (all its
-// loads in flight at once), scans them in registers, then one block-wide scan of the threads' sums
-constexpr uint32_t SCAN_PER = 16;
-__global__ __launch_bounds__(256) void k_walk_scan(WalkArgs a, uint32_t n_blocks) {
-    __shared__ SegCount sh_wave[4];
-    __shared__ SegCount sh_carry;
-    const SegCount zero = {};
-    if (threadIdx.x == 0) sh_carry = zero;
-    __syncthreads();
-    for (uint32_t b0 = 0; b0 < n_blocks; b0 += 256 * SCAN_PER) {
-        const uint32_t first = b0 + threadIdx.x * SCAN_PER;
-        SegCount v[SCAN_PER];
-#pragma unroll
-        for (uint32_t i = 0; i < SCAN_PER; ++i) v[i] = first + i < n_blocks ? agg_load(a.lb_agg + 4ull * (first + i)) : zero;
-        SegCount sum = zero;
-#pragma unroll
-        for (uint32_t i = 0; i < SCAN_PER; ++i) sum = sc_add(sum, v[i]);
-        SegCount tot;
-        SegCount ex = sc_add(sh_carry, block_excl_scan<256>(sum, tot, sh_wave));
-#pragma unroll
-        for (uint32_t i = 0; i < SCAN_PER; ++i) {
-            if (first + i < n_blocks) agg_store(a.lb_incl + 4ull * (first + i), ex);   // exclusive prefix
-            ex = sc_add(ex, v[i]);
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) sh_carry = sc_add(sh_carry, tot);
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-        const SegCount tt = sh_carry;
-        wsc_summary sm;
-        const bool compact = a.compact != 0;   // (as the fused walk reports: arena bytes, COMPACT only)
-        sm.data_bytes = compact ? tt.bytes0 : 0;
-        sm.ctrl_bytes = compact ? tt.bytes1 : 0;
-        sm.n_frames = tt.frames;
-        // spans past the capacity were never written: the unmask must not read them (an overflowed
-        // batch unmasks the spans that fit; n_spans = spans unmasked)
-        sm.n_spans = tt.spans0 + tt.spans1 < a.spans_cap ? tt.spans0 + tt.spans1 : a.spans_cap;
-        sm.overflow = (tt.frames > a.frames_cap || tt.spans0 + tt.spans1 > a.spans_cap) ? 1u : 0u;
-        sm.pad = 0;
-        *a.summary = sm;
-        if (sm.overflow) __hip_atomic_fetch_or(a.sticky, sm.overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-
-template <bool COMPACT>
-__global__ __launch_bounds__(256) void k_walk_emit(WalkArgs a) {
-    __shared__ SegCount sh_wave[4];
-    const uint32_t s = blockIdx.x * 256 + threadIdx.x;
-    const SegCount zero = {};
-    const SegCount own = s < a.n_segs ? a.counts[s] : zero;
-    SegCount tot;
-    const SegCount ex = block_excl_scan<256>(own, tot, sh_wave);
-    if (s >= a.n_segs) return;
-    const SegCount base = sc_add(agg_load(a.lb_incl + 4ull * blockIdx.x), ex);
-    if (own.flags & SEGF_U8DEFER) {
-        a.u8seg[s].sbase = base.spans0 + base.spans1;
-        a.u8seg[s].nspans = own.spans0 + own.spans1;
-        a.u8seg[s].fbase = base.frames;
-    }
-    walk_segment<true, COMPACT, 256>(a, s, base, own, nullptr, nullptr);
-}
-
-// ---------------------------------------------------------------------------------------------
 // Quad pre-pass of the fused walk (one segment per 4 lanes, every wave of the block).  The serial
 // walk spends its time on the header chain: one lane walks its segment's frames one after another,
 // each a dependent memory round trip plus the state machine's instructions on one wave per SIMD
@@ -1608,14 +1480,10 @@ __device__ __forceinline__ void write_summary(const WalkArgs& a, const SegCount&
 // decode, and at context creation.
 // SPREAD (> 0): the WL walking columns are spread SPREAD per wave over WL / SPREAD waves, so several
 // SIMDs issue the header chains (same blocks, same look-back as SPREAD = 0).
-// A walk block's position in the look-back order.  With a.hw_order the hardware workgroup index:
-// workgroups are dispatched in index order (each XCD takes its share in order), so every block a
-// block waits on has been dispatched before it, and only work that never waits on the walk can
-// delay a dispatch -- no ticket atomic, whose same-address serialisation spread block starts over
-// 3 us (256 blocks) to 8 us (512 blocks) in the stamps.  Otherwise a ticket in start order.  The
-// look-back's bounded spin backs both.
+// A walk block's position in the look-back order: a ticket in start order, so every block a block
+// waits on has started (the hardware workgroup index, without the ticket atomic, measured slower:
+// profiles/r04_walk_hw_order_ab.log).  The look-back's bounded spin backs it.
 __device__ __forceinline__ uint32_t walk_block_id(const WalkArgs& a) {
-    if (a.hw_order) return blockIdx.x;
     return __hip_atomic_fetch_add(a.lb_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -1625,7 +1493,7 @@ __global__ __launch_bounds__(NT) void k_walk_fused(WalkArgs a) {
     __shared__ uint32_t sh_bid;
     __shared__ WalkLds<COMPACT, KR, NT, G, WL> L;
     const uint32_t lane = threadIdx.x, wl = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (a.prio) __builtin_amdgcn_s_setprio(3);   // a latency-bound chain beside streaming unmask waves
+    __builtin_amdgcn_s_setprio(3);   // a latency-bound chain beside streaming unmask waves (neutral, round 5)
     if (lane == 0) sh_bid = walk_block_id(a);
     __syncthreads();
     const uint32_t bid = sh_bid;
@@ -1708,14 +1576,14 @@ __global__ __launch_bounds__(NT) void k_walk_tiled(WalkArgs a, uint32_t per_bloc
     __shared__ uint32_t sh_bid;
     __shared__ WalkLds<COMPACT, KR, NT, 1> L;
     const uint32_t lane = threadIdx.x, wl = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (a.prio) __builtin_amdgcn_s_setprio(3);   // a latency-bound chain beside streaming unmask waves
+    __builtin_amdgcn_s_setprio(3);   // a latency-bound chain beside streaming unmask waves (neutral, round 5)
     if (lane == 0) sh_bid = walk_block_id(a);
     __syncthreads();
     const uint32_t bid = sh_bid;
     const uint32_t sb = bid * per_block < a.n_segs ? bid * per_block : a.n_segs;
     const uint32_t se = a.n_segs - sb < per_block ? a.n_segs : sb + per_block;
     const SegCount zero = {};
-    uint64_t t0 = 0, t1 = 0, t2 = 0;   // diagnostic stamps (WSC_DEBUG_STAMPS=1)
+    uint64_t t0 = 0, t1 = 0, t2 = 0;   // diagnostic stamps (WSC_WALK_DEBUG_STAMPS)
     if (a.dbg && lane == 0) t0 = __builtin_amdgcn_s_memrealtime();
     // Inputs are pipelined across tiles: while tile t is walked, tile t+1's first headers and
     // tile t+2's bounds and carried states are already in flight (phase 1); tile t+1's bounds,
@@ -1820,14 +1688,11 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(WSC_CH
     }
 }
 
-template __global__ void k_u8_check<1, 4>(U8Args);
-template __global__ void k_u8_check<2, 4>(U8Args);
 template __global__ void k_u8_check<4, 4>(U8Args);
-template __global__ void k_u8_check<8, 4>(U8Args);
-template __global__ void k_u8_check<4, 16>(U8Args);
 
-// explicit instantiations used by the host code: 16 frame records per lane, one segment per
-// lane, blocks of 64 or 256 lanes; batches of more segments use the three-launch walk below
+// explicit instantiations used by the host code (every one reached by test_fuzz_walk_geometries):
+// 16 frame records per lane (4 in mode 257), one segment per walking lane, blocks of 64 or 256
+// lanes; batches of more segments use the tiled walk
 template __global__ void k_walk_fused<false, 16, 64, 1, 64, 0>(WalkArgs);
 template __global__ void k_walk_fused<false, 16, 64, 1, 16, 0>(WalkArgs);
 template __global__ void k_walk_fused<true, 16, 64, 1, 16, 0>(WalkArgs);
@@ -1844,10 +1709,6 @@ template __global__ void k_walk_fused<false, 16, 256, 1, 64, 16>(WalkArgs);
 template __global__ void k_walk_fused<true, 16, 256, 1, 64, 16>(WalkArgs);
 template __global__ void k_walk_tiled<false, 4, 256>(WalkArgs, uint32_t);
 template __global__ void k_walk_tiled<true, 4, 256>(WalkArgs, uint32_t);
-template __global__ void k_walk_count<false>(WalkArgs);
-template __global__ void k_walk_count<true>(WalkArgs);
-template __global__ void k_walk_emit<false>(WalkArgs);
-template __global__ void k_walk_emit<true>(WalkArgs);
 
 // ---------------------------------------------------------------------------------------------
 // wsc_kcopy: device <-> pinned host by a kernel that reads or writes host memory over PCIe (no

@@ -92,7 +92,6 @@ struct WalkArgs {
     uint32_t frames_cap;
     const wsc_conn_state* state_in;
     uint64_t max_frame_len;
-    SegCount* counts;            // three-launch walk: per segment counts
     wsc_frame* frames;
     Span* spans;
     uint32_t spans_cap;
@@ -107,7 +106,7 @@ struct WalkArgs {
     uint64_t* lb_agg;            // per block: SegCount as 4 x u64
     uint64_t* lb_incl;
     uint32_t* lb_err;            // bounded-spin timeout
-    uint64_t* dbg;               // optional per-block timestamps (WSC_DEBUG_STAMPS=1)
+    uint64_t* dbg;               // optional per-block timestamps (WSC_WALK_DEBUG_STAMPS)
     uint32_t* u8info;            // per segment: {first utf8-failing frame ordinal, DFA state}
     U8Item* u8items;             // deferred UTF-8 items
     uint32_t u8items_cap;
@@ -117,13 +116,11 @@ struct WalkArgs {
     uint32_t* sticky;            // context error bits, never re-armed by a kernel (wsc_error_flags)
     uint32_t* u8host;            // host-visible word set when any UTF-8 item is deferred (cleared by the host)
     uint32_t* win_flag;          // per unmask window: 1 = inside a deferred text item (k_unmask folds its map)
-    uint32_t compact;            // WSC_F_COMPACT (k_walk_scan: the other kernels are templated on it)
-    uint32_t quad_pre;           // fused walk with one walking wave per 4: the quad pre-pass (WSC_QUAD_PRE=0: off, A/B)
+    uint32_t compact;            // WSC_F_COMPACT (the kernels are also templated on it)
+    uint32_t quad_pre;           // fused walk with one walking wave per 4: the quad pre-pass (WSC_WALK_NO_QUAD_PRE: off)
     uint4* hdr_cache;            // tiled walk: per segment, the 16 bytes at its first frame (null: off)
     uint32_t* stride_hint;       // quad pre-pass: the stride the last decode ended with (first speculation)
-    uint32_t hw_order;           // look-back order = hardware workgroup index (no ticket atomic), walk_block_id
-    uint32_t hdr_nt;             // non-temporal header loads (hdr_load): COMPACT batches by default
-    uint32_t prio;               // walk waves raise their issue priority (s_setprio) over the unmask waves they share SIMDs with
+    uint32_t hdr_nt;             // non-temporal header loads (hdr_load): COMPACT batches (and WSC_WALK_HDR_NT)
 };
 
 // k_u8_check runs AFTER the unmask: the unmask has already folded every text window that lies

@@ -165,12 +165,12 @@ struct wsc_session {
     std::mutex rm_mu;
     std::vector<uint32_t> rm_q;
     std::atomic<uint32_t> rm_pending{0};
-    // test knob: WSC_SESSION_FAULT=k fails the k-th device batch as a device error would
+    // test hook (wsc_session_inject_fault): the fault_at-th device batch fails as a device error would
     uint64_t fault_at = 0, n_submits = 0;
-    // WSC_SESSION_TIMING=1: seconds per phase, printed at destroy
+    // WSC_SESSION_TIMING: seconds per phase, printed at destroy
     bool timing = false;
-    int kcopy = 1;                // staging copies by wsc_kcopy: 1 the wire's H2D (default), 2 all, 0
-                                  // none (hipMemcpyAsync); WSC_SESSION_KCOPY.  At 2 the small copies
+    int kcopy = 1;                // staging copies by wsc_kcopy: 1 the wire's H2D (default), 2 all
+                                  // (WSC_SESSION_KCOPY_ALL), 0 none (WSC_SESSION_COPY_ENGINE).  At 2 the small copies
                                   // queue as kernels behind other pollers' decodes on the shared
                                   // compute queues (profiles/r05/ab11_echo_*: 4 pollers, 512 KiB
                                   // reads 4.24 -> 3.02 GiB/s), so they stay on the copy engines
@@ -435,9 +435,6 @@ int decode_sync_part(wsc_session* s, int set, uint32_t a, uint32_t b, uint64_t p
     const int rc = wsc_decode_host(g.ctx, wire, end, off.data(), n, s->flags, sin.data(), sout.data(), sres.data(),
                                    fr.data(), s->cfg.max_frames, compact ? res : nullptr,
                                    compact ? fd.data() : nullptr, &sm);
-    if (std::getenv("WSC_DEBUG_SPLIT"))
-        std::fprintf(stderr, "decode_sync_part a=%u b=%u prefix=%llu end=%llu rc=%d ovf=%u nf=%u ns=%u\n", a, b,
-                     (unsigned long long)prefix_limit, (unsigned long long)end, rc, sm.overflow, sm.n_frames, sm.n_spans);
     if (rc == WSC_E_CAPACITY && (sm.overflow & 1u)) {
         if (n > 1) {
             const uint32_t mid = a + n / 2;
@@ -575,7 +572,12 @@ int wsc_session_create(int device, const wsc_config* cfg, uint32_t flags, wsc_se
     wsc_config& g = s->cfg;
     if (g.max_frames < 2 || g.max_segs < 2 || g.max_batch_bytes < 64) { delete s; return WSC_E_INVAL; }
     // (no clamp of max_frame_len to the batch: payloads stream across batches)
+    if (flags & ~(uint32_t)(WSC_F_COMPACT | WSC_SESSION_BLOCKING_WAIT | WSC_SESSION_TIMING | WSC_SESSION_COPY_ENGINE |
+                            WSC_SESSION_KCOPY_ALL)) { delete s; return WSC_E_INVAL; }
+    if ((flags & WSC_SESSION_COPY_ENGINE) && (flags & WSC_SESSION_KCOPY_ALL)) { delete s; return WSC_E_INVAL; }
     s->flags = flags & (WSC_F_COMPACT | WSC_SESSION_BLOCKING_WAIT);
+    s->timing = (flags & WSC_SESSION_TIMING) != 0;
+    s->kcopy = (flags & WSC_SESSION_COPY_ENGINE) ? 0 : (flags & WSC_SESSION_KCOPY_ALL) ? 2 : 1;
     s->device = device;
     int rc = WSC_OK;
     for (Stage& t : s->st) {
@@ -625,9 +627,6 @@ int wsc_session_create(int device, const wsc_config* cfg, uint32_t flags, wsc_se
         t.d_summary = D(sizeof(wsc_summary));
     }
     if (rc) { wsc_session_destroy(s); return rc; }
-    if (const char* e = std::getenv("WSC_SESSION_TIMING"); e && e[0] == '1') s->timing = true;
-    if (const char* e = std::getenv("WSC_SESSION_FAULT"); e && *e) s->fault_at = std::strtoull(e, nullptr, 10);
-    if (const char* e = std::getenv("WSC_SESSION_KCOPY"); e && *e) s->kcopy = e[0] - '0';
     *out = s;
     return WSC_OK;
 }
@@ -739,6 +738,14 @@ int wsc_session_commit(wsc_session* s, uint32_t conn, uint64_t n) {
     Conn* c = lookup(s, conn);
     if (!c) return WSC_E_STATE;
     if (n > c->reserved) return WSC_E_INVAL;
+    // a staging reservation belongs to the staging set being filled when it was made: if a submit
+    // switched sets since (a misuse: commit must come first), c->seg indexes the other set's vectors
+    // -- nothing is read into the batch; an empty commit (wsc_session_eof's) just drops it (round-5
+    // ADVICE)
+    if (c->reserved && !c->reserved_spill && c->fill_epoch != s->fill_epoch) {
+        c->reserved = 0;
+        return n == 0 ? WSC_OK : WSC_E_STATE;
+    }
     s->st_read += n;
     if (c->reserved_spill) {
         c->spill.resize(c->spill.size() - (c->reserved - n));
@@ -782,6 +789,13 @@ int wsc_session_submit(wsc_session* s) {
     Stage& f = s->st[s->fill];
     for (uint32_t slot = 0; slot < s->conns.size(); ++slot) {   // spilled bytes ride in this batch if they fit
         Conn& c = s->conns[slot];
+        // a reservation still open (a misuse: commit comes first) reads nothing into this batch: it
+        // is dropped, so a spill region held open is not packed as data and a later commit(0) --
+        // wsc_session_eof's -- finds nothing to shrink (round-5 ADVICE)
+        if (c.reserved) {
+            if (c.reserved_spill) c.spill.resize(c.spill.size() - c.reserved);
+            c.reserved = 0;
+        }
         if (!c.live || c.failed || c.st.status != WSC_SEG_OPEN || c.spill.empty()) continue;
         if (c.fill_epoch == s->fill_epoch) {
             if (c.seg + 1 != f.seg_conn.size()) continue;   // not last: next batch
@@ -810,8 +824,8 @@ int wsc_session_submit(wsc_session* s) {
         if (Conn* c = f.seg_conn[q] == DEAD_SEG ? nullptr : lookup(s, f.seg_conn[q])) c->in_flight = true;
     const double t1 = s->timing ? now_s() : 0;
     s->n_submits += 1;
-    if (s->fault_at && s->n_submits == s->fault_at)   // test knob: as a failed launch would
-        f.launch_rc = wsc::set_last_error(WSC_E_DEVICE, "wsc_session: injected device failure (WSC_SESSION_FAULT)");
+    if (s->fault_at && s->n_submits == s->fault_at)   // test hook: as a failed launch would
+        f.launch_rc = wsc::set_last_error(WSC_E_DEVICE, "wsc_session: injected device failure (wsc_session_inject_fault)");
     else
         f.launch_rc = launch_stage(s, f);
     const double t2 = s->timing ? now_s() : 0;
@@ -998,6 +1012,12 @@ int wsc_session_next(wsc_session* s, uint32_t conn, wsc_event* ev) {
         ev->data = c->current.data.empty() ? nullptr : c->current.data.data();
         ev->len = c->current.data.size();
     }
+    return WSC_OK;
+}
+
+int wsc_session_inject_fault(wsc_session* s, uint64_t k) {
+    if (!s) return WSC_E_INVAL;
+    s->fault_at = k ? s->n_submits + k : 0;
     return WSC_OK;
 }
 

@@ -158,13 +158,20 @@ void phase(uint64_t batch_bytes, uint32_t max_frames, int mode, size_t n_conns, 
             c.fed += n;
             if (c.fed == c.wire.size() && i % 2 == 1 && !c.removed) {   // the peer closes after its last byte
                 // a poller reserves room, then recv() returns 0; some commit(0) only after the eof
-                // (reserve -> eof -> commit(0): round-4 ADVICE, Close() must still come)
+                // (reserve -> eof -> commit(0): round-4 ADVICE, Close() must still come); in mode 1
+                // some submit between the reserve and the eof, which then drops a reservation made
+                // in the other staging set (reserve -> submit -> eof: round-5 ADVICE)
                 const bool late = mode != 0 && i % 4 == 3;
+                const bool mid_submit = mode == 1 && i % 4 == 1;
                 uint8_t* p = nullptr;
                 uint64_t room = 0;
                 if (mode != 0) {
                     CHECK(wsc_session_reserve(s, c.h, 4096, &p, &room) == WSC_OK);
-                    if (p && !late) CHECK(wsc_session_commit(s, c.h, 0) == WSC_OK);
+                    if (p && mid_submit) {   // (WSC_E_STATE: a batch is in flight already, complete() first)
+                        const int r = wsc_session_submit(s);
+                        CHECK(r == WSC_OK || r == WSC_E_STATE);
+                    }
+                    else if (p && !late) CHECK(wsc_session_commit(s, c.h, 0) == WSC_OK);
                 }
                 const int rc = wsc_session_eof(s, c.h);
                 CHECK(rc == WSC_OK);
@@ -217,7 +224,6 @@ void phase(uint64_t batch_bytes, uint32_t max_frames, int mode, size_t n_conns, 
 }
 
 void fault_phase() {
-    setenv("WSC_SESSION_FAULT", "2", 1);
     wsc_config cfg;
     wsc_config_default(&cfg);
     cfg.max_batch_bytes = 1 << 16;
@@ -225,7 +231,7 @@ void fault_phase() {
     cfg.max_frames = 256;
     wsc_session* s = nullptr;
     CHECK(wsc_session_create(0, &cfg, 0, &s) == WSC_OK);
-    unsetenv("WSC_SESSION_FAULT");
+    CHECK(wsc_session_inject_fault(s, 2) == WSC_OK);   // the second submission fails
     uint32_t a = 0, b = 0;
     wsc_session_open(s, &a);
     wsc_session_open(s, &b);

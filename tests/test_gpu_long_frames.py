@@ -39,7 +39,7 @@ def _mask_tile(torch, dev, mask, n):
 @pytest.mark.parametrize("compact,walk_mode", [(False, "0"), (True, "0"), (False, "3")])
 def test_frame_over_4gib(codec_lib, monkeypatch, compact, walk_mode):
     torch = pytest.importorskip("torch")
-    monkeypatch.setenv("WSC_WALK_MODE", walk_mode)
+    monkeypatch.setitem(K.CFG_DEFAULTS, "walk_mode", int(walk_mode))
     dev = torch.device("cuda:0")
     big = (4 << 30) + 12345            # > 2^32: 3 spans (2 GiB, 2 GiB, 12345 B)
     mask_big = 0xA1B2C3D4

@@ -72,7 +72,7 @@ def test_fuzz_walk_geometries(codec_lib, monkeypatch, compact, mode):
     walking waves per CU), 256-lane blocks whose 64 walking columns are spread 16 per wave (mode
     66), one segment per lane with 4 LDS records per lane (mode 257: 3 blocks per CU), and the tiled
     walk for many segments (mode 3)."""
-    monkeypatch.setenv("WSC_WALK_MODE", str(mode))
+    monkeypatch.setitem(K.CFG_DEFAULTS, "walk_mode", mode)
     c = K.Codec(0, max_batch_bytes=64 << 20, max_segs=1 << 14, max_frames=1 << 18)
     try:
         streams = [random_stream(7000 + i, n_units=int(5 + i % 40), text_p=0.5) for i in range(400)]
@@ -111,11 +111,11 @@ def _run_streams(seed, n):
 
 @pytest.mark.parametrize("compact,pre", [(False, "1"), (True, "1"), (False, "0")])
 def test_quad_prepass_runs(codec_lib, monkeypatch, compact, pre):
-    """The fused walk's quad pre-pass (mode 65, WSC_QUAD_PRE) on runs of equal frames, stride
-    changes, non-BIN frames that end a run, and segments cut mid-frame: records, bytes and carried
-    state equal the oracle's, and equal the serial walk's (WSC_QUAD_PRE=0)."""
-    monkeypatch.setenv("WSC_WALK_MODE", "65")
-    monkeypatch.setenv("WSC_QUAD_PRE", pre)
+    """The fused walk's quad pre-pass (mode 65) on runs of equal frames, stride changes, non-BIN
+    frames that end a run, and segments cut mid-frame: records, bytes and carried state equal the
+    oracle's, and equal the serial walk's (walk_flags WSC_WALK_NO_QUAD_PRE)."""
+    monkeypatch.setitem(K.CFG_DEFAULTS, "walk_mode", 65)
+    monkeypatch.setitem(K.CFG_DEFAULTS, "walk_flags", 0 if pre == "1" else K.WALK_NO_QUAD_PRE)
     c = K.Codec(0, max_batch_bytes=64 << 20, max_segs=1 << 14, max_frames=1 << 18)
     try:
         for rep in range(2):   # the second decode starts from the first one's stride hint
@@ -126,10 +126,10 @@ def test_quad_prepass_runs(codec_lib, monkeypatch, compact, pre):
 
 @pytest.mark.parametrize("cache", ["1", "0"])
 def test_tiled_walk_header_cache(codec_lib, monkeypatch, cache):
-    """The tiled walk (mode 3) with and without its per-segment header cache (WSC_HDR_CACHE), on
-    the fuzz corpus and on runs of equal frames."""
-    monkeypatch.setenv("WSC_WALK_MODE", "3")
-    monkeypatch.setenv("WSC_HDR_CACHE", cache)
+    """The tiled walk (mode 3) with and without its per-segment header cache (walk_flags
+    WSC_WALK_NO_HDR_CACHE), on the fuzz corpus and on runs of equal frames."""
+    monkeypatch.setitem(K.CFG_DEFAULTS, "walk_mode", 3)
+    monkeypatch.setitem(K.CFG_DEFAULTS, "walk_flags", 0 if cache == "1" else K.WALK_NO_HDR_CACHE)
     c = K.Codec(0, max_batch_bytes=64 << 20, max_segs=1 << 14, max_frames=1 << 18)
     try:
         _check_batch(c, [random_stream(8000 + i, n_units=int(1 + i % 9), text_p=0.3) for i in range(500)])
@@ -141,9 +141,9 @@ def test_tiled_walk_header_cache(codec_lib, monkeypatch, cache):
 @pytest.mark.parametrize("mode", ["65", "3"])
 def test_nontemporal_header_loads(codec_lib, monkeypatch, mode):
     """The walk's non-temporal header loads (COMPACT batches by default) forced on in-place
-    batches too (WSC_HDR_NT=1): the same records and bytes as the oracle's."""
-    monkeypatch.setenv("WSC_WALK_MODE", mode)
-    monkeypatch.setenv("WSC_HDR_NT", "1")
+    batches too (walk_flags WSC_WALK_HDR_NT): the same records and bytes as the oracle's."""
+    monkeypatch.setitem(K.CFG_DEFAULTS, "walk_mode", int(mode))
+    monkeypatch.setitem(K.CFG_DEFAULTS, "walk_flags", K.WALK_HDR_NT)
     c = K.Codec(0, max_batch_bytes=64 << 20, max_segs=1 << 14, max_frames=1 << 18)
     try:
         _check_batch(c, [random_stream(9100 + i, n_units=int(1 + i % 30), text_p=0.3) for i in range(400)])
@@ -166,7 +166,7 @@ def test_close_inside_text_and_bin_chains(codec_lib, monkeypatch, compact, inlin
     """FIN=1 CLOSE frames inside TEXT / BIN chains (and outside any): the reason rule depends on
     messageMode (websocket.go:153-172 + websocket_frame.go:49,71-73).  inline_max 0 defers every
     other text check to the chip-wide UTF-8 kernel (the CLOSE itself is always checked in the walk)."""
-    monkeypatch.setenv("WSC_U8_INLINE_MAX", str(inline_max))
+    monkeypatch.setitem(K.CFG_DEFAULTS, "u8_inline_max", inline_max)
     c = K.Codec(0, max_batch_bytes=16 << 20, max_segs=1 << 12, max_frames=1 << 16)
     try:
         _check_batch(c, _close_streams(), compact=compact)
@@ -567,15 +567,8 @@ def test_decode_split_pipeline_matches_oracle(codec_lib, compact, layout, inline
     ctxs, bats, ts, packed = [], [], [], []
     for streams in sets:
         wire, off = pack_streams(streams)
-        old = os.environ.get("WSC_U8_INLINE_MAX")
-        os.environ["WSC_U8_INLINE_MAX"] = str(inline_max)
-        try:
-            c = K.Codec(0, max_batch_bytes=len(wire) + 4096, max_segs=len(streams), max_frames=1 << 15)
-        finally:
-            if old is None:
-                del os.environ["WSC_U8_INLINE_MAX"]
-            else:
-                os.environ["WSC_U8_INLINE_MAX"] = old
+        c = K.Codec(0, max_batch_bytes=len(wire) + 4096, max_segs=len(streams), max_frames=1 << 15,
+                    u8_inline_max=inline_max)
         n = len(streams)
         t = dict(wire=torch.from_numpy(wire.copy()).to(dev), seg_off=torch.from_numpy(off.view(np.int64)).to(dev),
                  st_out=torch.zeros(n * K.STATE_BYTES, dtype=torch.uint8, device=dev),
@@ -640,7 +633,7 @@ def test_staged_pipeline_back_to_back(codec_lib, monkeypatch, inline_max):
     host synchronisation between them: each context's next walk must wait (on the host, for the
     unmask's pinned done word) until its previous unmask has read the spans and window index it
     overwrites.  A race would corrupt the arena; the last decode of each is checked with the oracle."""
-    monkeypatch.setenv("WSC_U8_INLINE_MAX", str(inline_max))
+    monkeypatch.setitem(K.CFG_DEFAULTS, "u8_inline_max", inline_max)
     torch = pytest.importorskip("torch")
     dev = torch.device("cuda:0")
     ctxs, bats, ts, packed = [], [], [], []

@@ -61,7 +61,7 @@ def test_pong_streams_across_batches(codec_lib, monkeypatch, compact, inline_max
     """every stream cut into 3 device batches at many offsets (inside PONG headers and payloads,
     at odd mask phases, one byte into a 4-byte character); inline_max 0 sends every text piece --
     the PONG's too -- to the chip-wide UTF-8 path"""
-    monkeypatch.setenv("WSC_U8_INLINE_MAX", str(inline_max))
+    monkeypatch.setitem(K.CFG_DEFAULTS, "u8_inline_max", inline_max)
     c = K.Codec(0, max_batch_bytes=64 << 20, max_segs=1 << 12, max_frames=1 << 16)
     try:
         streams, cuts, refs = [], [], []
@@ -89,7 +89,7 @@ def test_pong_streams_across_batches(codec_lib, monkeypatch, compact, inline_max
 def test_pong_piece_carries_its_utf8_state(codec_lib, monkeypatch):
     """the PONG's own DFA state (frame_utf8) is carried between batches while the message's
     (cont_utf8) is kept apart: cut one byte into a 4-byte character of the PONG"""
-    monkeypatch.setenv("WSC_U8_INLINE_MAX", "256")
+    monkeypatch.setitem(K.CFG_DEFAULTS, "u8_inline_max", 256)
     s = _pong_streams(41)[5]
     pong_at = len(synth.frame(1, b"x", fin=False, mask=8))
     cut = pong_at + 8 + 4093 + 1                         # 1 byte into the 4-byte character

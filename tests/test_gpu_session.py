@@ -174,11 +174,11 @@ def test_remove_from_another_thread(codec_lib):
 
 
 def test_device_failure_closes_only_that_batch(codec_lib, monkeypatch):
-    """WSC_SESSION_FAULT=2 fails the second device batch as a device error would: decode()
+    """wsc_session_inject_fault(2) fails the second device batch as a device error would: decode()
     reports it, exactly that batch's connections get CLOSE 1011 / WSC_ERR_DEVICE with their
     bytes kept, every later batch and every other connection decodes normally"""
-    monkeypatch.setenv("WSC_SESSION_FAULT", "2")
     sess = K.Session(0, max_batch_bytes=4 << 20, max_segs=256, max_frames=1 << 14)
+    sess.inject_fault(2)
     a = [sess.open() for _ in range(4)]
     for c in a:
         sess.feed(c, synth.frame(2, b"round1", mask=1))
@@ -317,11 +317,12 @@ def test_kcopy_both_directions(codec_lib, nbytes):
 @pytest.mark.parametrize("level", ["0", "1", "2"])
 @pytest.mark.parametrize("compact", [False, True])
 def test_session_staging_copy_paths(codec_lib, monkeypatch, level, compact):
-    """the session's staging copies by kernels (WSC_SESSION_KCOPY=2, default), the wire's H2D only
-    (1) or none (0, hipMemcpyAsync) decode the same random streams to the oracle's events"""
-    monkeypatch.setenv("WSC_SESSION_KCOPY", level)
+    """the session's staging copies: the wire's H2D by a kernel (1, the default), every copy by
+    kernels (2, WSC_SESSION_KCOPY_ALL) or none (0, hipMemcpyAsync: WSC_SESSION_COPY_ENGINE) decode
+    the same random streams to the oracle's events"""
+    flags = {"0": K.SESSION_COPY_ENGINE, "1": 0, "2": K.SESSION_KCOPY_ALL}[level]
     rng = np.random.default_rng(77)
-    sess = K.Session(0, compact=compact, max_batch_bytes=4 << 20, max_segs=256, max_frames=1 << 15)
+    sess = K.Session(0, compact=compact, flags=flags, max_batch_bytes=4 << 20, max_segs=256, max_frames=1 << 15)
     streams = [random_stream(77000 + i, n_units=25) for i in range(60)]
     try:
         conns, got = _drive(sess, streams, rng, zero_copy=True)

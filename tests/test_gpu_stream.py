@@ -159,7 +159,7 @@ def test_cut_at_every_4k_boundary_across_3_batches(codec_lib, monkeypatch, compa
     """every base stream as many connections, connection j cut at 4096 * (j + 1) and 36 KiB later
     (so every 4 KiB boundary is a cut of some connection), 3 device batches; inline_max 0 sends
     every text piece to the chip-wide UTF-8 path"""
-    monkeypatch.setenv("WSC_U8_INLINE_MAX", str(inline_max))
+    monkeypatch.setitem(K.CFG_DEFAULTS, "u8_inline_max", inline_max)
     c = K.Codec(0, max_batch_bytes=64 << 20, max_segs=1 << 12, max_frames=1 << 17)
     try:
         streams, cuts, refs = [], [], []

@@ -1,7 +1,6 @@
 """Chip-wide UTF-8 validation (k_u8_check) for text the walk defers: bit-exact against the oracle.
 
-By default text payloads above 256 B are deferred; WSC_U8_INLINE_MAX=0 (read at context creation)
-sends EVERY text check through k_u8_check, so the fuzz corpus (fragmented text chains, multi-byte
+By default text payloads above 256 B are deferred; wsc_config.u8_inline_max = 0 sends EVERY text check through k_u8_check, so the fuzz corpus (fragmented text chains, multi-byte
 characters split across fragments, PINGs inside text messages (Q6), close reasons, invalid
 sequences) exercises the deferred path end to end, including chains that span batches.
 Full-size: 64 KiB TEXT frames of 1-4 byte characters, valid and with injected errors."""
@@ -20,15 +19,15 @@ pytestmark = pytest.mark.gpu
 
 
 def _with_inline_max(v, make):
-    old = os.environ.get("WSC_U8_INLINE_MAX")
-    os.environ["WSC_U8_INLINE_MAX"] = str(v)
+    old = K.CFG_DEFAULTS.get("u8_inline_max")
+    K.CFG_DEFAULTS["u8_inline_max"] = v
     try:
         return make()
     finally:
         if old is None:
-            del os.environ["WSC_U8_INLINE_MAX"]
+            del K.CFG_DEFAULTS["u8_inline_max"]
         else:
-            os.environ["WSC_U8_INLINE_MAX"] = old
+            K.CFG_DEFAULTS["u8_inline_max"] = old
 
 
 @pytest.fixture(scope="module")
@@ -187,11 +186,11 @@ def test_text_1k_several_failures_per_connection(codec_lib, compact):
 
 
 def test_rejected_geometry_leaves_utf8_counters_consistent(codec_lib, monkeypatch):
-    """round-3 ADVICE (medium): a decode refused by the walk-geometry guard (WSC_WALK_MODE=16 with
+    """round-3 ADVICE (medium): a decode refused by the walk-geometry guard (walk_mode 16 with
     more segments than the look-back state holds) must not flip the UTF-8 item-counter parity nor
     commit its geometry -- the next decodes' chip-wide 1007 verdicts must stay exact"""
-    monkeypatch.setenv("WSC_WALK_MODE", "16")
-    monkeypatch.setenv("WSC_U8_INLINE_MAX", "0")
+    monkeypatch.setitem(K.CFG_DEFAULTS, "walk_mode", 16)
+    monkeypatch.setitem(K.CFG_DEFAULTS, "u8_inline_max", 0)
     c = K.Codec(0, max_batch_bytes=8 << 20, max_segs=1 << 15, max_frames=1 << 17)
     try:
         many = [synth.frame(2, b"x", mask=i) for i in range(1 << 15)]
@@ -253,5 +252,44 @@ def test_text_window_edges_alternating_layouts(codec_lib):
                 _check(c, streams, compact=compact)
         res = _check(c, _edge_batch(rng, bad=True))
         assert int((res.seg["status"] == K.SEG_ERROR).sum()) == 16
+    finally:
+        c.close()
+
+
+@pytest.mark.parametrize("compact", [False, True])
+@pytest.mark.parametrize("inline_max", [256, 0])
+def test_failed_single_piece_with_open_composite_zeroes_carried_state(codec_lib, compact, inline_max):
+    """round-5 ADVICE: a segment whose single-piece TEXT message fails (1007, decided by k_u8_check's
+    fast verdict) while composite items of the same segment are still open -- a TEXT fragment that
+    ends inside a 4-byte character (cont_utf8 would be 3) or a PONG under TEXT cut inside a
+    character (frame_utf8) -- must leave NO carried DFA state: status ERROR, cont_utf8 = frame_utf8 = 0.
+    Many such segments in one batch, the failing frame placed before, between and after the open
+    items, so the two verdict paths (per-item fail, per-segment compose) interleave every way."""
+    emoji = "\U0001F600".encode()
+    ok = ("ab" + "ü" * 300).encode()                      # > 256 B: deferred by default
+    bad = bytearray(("x" * 600).encode())
+    bad[333] = 0xFF
+    frag_open = synth.frame(1, ok + emoji[:1], fin=False, mask=0x01020304)   # ends 1 byte into U+1F600
+    pong_open = synth.frame(10, ok + emoji[:2], mask=0x0A0B0C0D)
+    streams = []
+    for k in range(96):
+        failing = synth.frame(1, bytes(bad), mask=0x11223344 + k)
+        if k % 3 == 0:
+            s = failing + frag_open
+        elif k % 3 == 1:
+            s = synth.frame(1, ok, fin=False, mask=5) + synth.frame(0, bytes(bad), mask=6 + k) + frag_open
+        else:
+            # a TEXT message open (fragment), a PONG inside it cut in a character, the failing frame first
+            s = failing + synth.frame(1, ok, fin=False, mask=7) + pong_open[:len(pong_open) - 3]
+        streams.append(s)
+    c = _with_inline_max(inline_max, lambda: K.Codec(0, max_batch_bytes=8 << 20, max_segs=256, max_frames=1 << 14))
+    try:
+        res = _check(c, streams, compact=compact)
+        for i in range(len(streams)):
+            st = res.state[i]
+            if int(res.seg[i]["status"]) == K.SEG_ERROR:
+                assert int(st["cont_utf8"]) == 0 and int(st["frame_utf8"]) == 0, (i, st)
+                assert int(st["frame_rem"]) == 0, (i, st)
+        assert int((res.seg["status"] == K.SEG_ERROR).sum()) == len(streams)
     finally:
         c.close()

@@ -1,5 +1,5 @@
 #!/bin/bash
-# An experiment build of libwscodec.so with extra -D flags, for A/B runs through WSC_LIB:
+# An experiment build of libwscodec.so with extra -D flags, for A/B runs (tools/lib_ab.py, ab_lib.sh):
 #   bash tools/build_variant.sh <name> -DFLAG ...   -> tools/_var/libwscodec_<name>.so
 set -e
 name=$1; shift

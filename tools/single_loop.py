@@ -30,8 +30,7 @@ def main():
            "t1": lambda: synth.text_batch(262144, 1024, 16, seed=synth.SEED_BASE + 8)}[which]()
     dev = torch.device("cuda:0")
     n = len(cfg["seg_off"]) - 1
-    kw = {"unmask_window": int(os.environ["WIN"])} if os.environ.get("WIN") else {}
-    c = K.Codec(0, max_batch_bytes=len(cfg["wire"]) + 4096, max_segs=n, max_frames=cfg["n_frames"] + 16, **kw)
+    c = K.Codec(0, max_batch_bytes=len(cfg["wire"]) + 4096, max_segs=n, max_frames=cfg["n_frames"] + 16)
     t = dict(wire=torch.from_numpy(cfg["wire"]).to(dev), seg_off=torch.from_numpy(cfg["seg_off"].view(np.int64)).to(dev),
              st=torch.zeros(n * K.STATE_BYTES, dtype=torch.uint8, device=dev), so=torch.zeros(n * 32, dtype=torch.uint8, device=dev),
              fr=torch.zeros((cfg["n_frames"] + 16) * 32, dtype=torch.uint8, device=dev), sm=torch.zeros(32, dtype=torch.uint8, device=dev))

@@ -1,14 +1,20 @@
-"""Where does the header walk spend its time?  Per-block s_memrealtime stamps (diagnostic build
-path: WSC_DEBUG_STAMPS=1) for a workload; prints count / look-back / emit phase durations."""
+"""Where does the header walk spend its time?  Per-block s_memrealtime stamps (wsc_config.walk_flags
+WSC_WALK_DEBUG_STAMPS) for a workload; prints count / look-back / emit phase durations.
+    python tools/walk_stamps.py <64k|1k|1k1|mixed|mixed1|frag> [walk_mode] [--lib path/to/libwscodec.so]"""
 import os
 import sys
-os.environ["WSC_DEBUG_STAMPS"] = "1"
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np
 import torch
 from netman_amd import codec as K, synth
 
-wl = sys.argv[1] if len(sys.argv) > 1 else "64k"
+args = sys.argv[1:]
+if "--lib" in args:   # an A/B variant build (tools/build_variant.sh)
+    i = args.index("--lib")
+    K.load_library(os.path.abspath(args[i + 1]))
+    del args[i:i + 2]
+wl = args[0] if args else "64k"
+mode = int(args[1]) if len(args) > 1 else 0
 cfg = {"64k": lambda: synth.uniform_batch(16384, 65536, 4, seed=synth.SEED_BASE + 1),
        "1k": lambda: synth.uniform_batch(1 << 20, 1024, 16, seed=synth.SEED_BASE + 1),
        "1k1": lambda: synth.uniform_batch(1 << 20, 1024, 1, seed=synth.SEED_BASE + 1),
@@ -18,7 +24,8 @@ cfg = {"64k": lambda: synth.uniform_batch(16384, 65536, 4, seed=synth.SEED_BASE 
 compact = wl == "frag"
 dev = torch.device("cuda:0")
 n = len(cfg["seg_off"]) - 1
-c = K.Codec(0, max_batch_bytes=len(cfg["wire"]) + 4096, max_segs=n, max_frames=cfg["n_frames"] + 16)
+c = K.Codec(0, max_batch_bytes=len(cfg["wire"]) + 4096, max_segs=n, max_frames=cfg["n_frames"] + 16,
+            walk_mode=mode, walk_flags=K.WALK_DEBUG_STAMPS)
 t = [torch.from_numpy(cfg["wire"]).to(dev), torch.from_numpy(cfg["seg_off"].view(np.int64)).to(dev),
      torch.zeros(n * K.STATE_BYTES, dtype=torch.uint8, device=dev), torch.zeros(n * 32, dtype=torch.uint8, device=dev),
      torch.zeros((cfg["n_frames"] + 16) * 32, dtype=torch.uint8, device=dev), torch.zeros(32, dtype=torch.uint8, device=dev)]
@@ -26,7 +33,6 @@ arena = torch.zeros(len(cfg["wire"]) + 64, dtype=torch.uint8, device=dev) if com
 fdst = torch.zeros(cfg["n_frames"] + 16, dtype=torch.int64, device=dev) if compact else None
 b = c.make_batch(t[0], t[1], None, t[2], t[3], t[4], t[5], compact=compact, arena=arena, frame_dst=fdst)
 n_cu = torch.cuda.get_device_properties(0).multi_processor_count
-mode = int(os.environ.get("WSC_WALK_MODE", "0"))
 if mode == 0:
     mode = 65 if n <= 64 * n_cu else (256 if n <= 256 * n_cu else 3)
 if mode == 3:   # the tiled walk (wsc_api.cpp): a persistent grid of 2 blocks per CU; stamps: start,

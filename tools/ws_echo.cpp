@@ -35,10 +35,10 @@ struct GpuDecoder : echo::Decoder {
     ~GpuDecoder() override { wsc_session_destroy(s); }
     int open() override {
         uint32_t id = 0;
-        wsc_session_open(s, &id);
+        check(wsc_session_open(s, &id), "wsc_session_open");
         return (int)id;
     }
-    void feed(int conn, const uint8_t* p, size_t n) override { wsc_session_feed(s, (uint32_t)conn, p, n); }
+    void feed(int conn, const uint8_t* p, size_t n) override { check(wsc_session_feed(s, (uint32_t)conn, p, n), "wsc_session_feed"); }
     // recv() straight into the session's pinned staging (the only host copy of inbound bytes)
     bool reserve(int conn, size_t max, uint8_t** p, size_t* avail) override {
         uint64_t a = 0;
@@ -46,7 +46,7 @@ struct GpuDecoder : echo::Decoder {
         *avail = (size_t)a;
         return true;
     }
-    void commit(int conn, size_t n) override { wsc_session_commit(s, (uint32_t)conn, n); }
+    void commit(int conn, size_t n) override { check(wsc_session_commit(s, (uint32_t)conn, n), "wsc_session_commit"); }
     bool pipelined() const override { return pipe; }
     void submit() override { check(wsc_session_submit(s), "wsc_session_submit"); }
     void complete() override { check(wsc_session_complete(s), "wsc_session_complete"); }
@@ -137,7 +137,13 @@ struct DeviceBatcher {
             }
             const uint64_t r = next_round++;
             requesting = 0;
-            while (true) {   // everything fed (a batch may leave spills: submit again)
+            // the bytes pending when the round starts (a batch may leave spills: submit again until
+            // they have all gone to the device) -- not what pollers that have not asked for this
+            // round keep feeding meanwhile, which would hold the waiting pollers (round-5 ADVICE)
+            uint64_t want = 0, sent0[2] = {0, 0};
+            check(wsc_session_pending(s, &want), "wsc_session_pending");
+            check(wsc_session_stats(s, sent0, 2), "wsc_session_stats");
+            while (true) {
                 check(wsc_session_submit(s), "wsc_session_submit");
                 while (true) {   // the device works; the pollers feed and read meanwhile
                     int ready = 0;
@@ -149,9 +155,10 @@ struct DeviceBatcher {
                 }
                 cv_req.wait(lk, [&] { return readers == 0; });   // the previous events are taken
                 check(wsc_session_complete(s), "wsc_session_complete");
-                uint64_t pend = 0;
+                uint64_t pend = 0, sent[2] = {0, 0};
                 check(wsc_session_pending(s, &pend), "wsc_session_pending");
-                if (!pend) break;
+                check(wsc_session_stats(s, sent, 2), "wsc_session_stats");
+                if (!pend || sent[1] - sent0[1] >= want) break;
             }
             done_round = r;
             cv_done.notify_all();
@@ -167,12 +174,12 @@ struct BatchedGpuDecoder : echo::Decoder {
     int open() override {
         std::lock_guard<std::mutex> lk(B.mu);
         uint32_t id = 0;
-        wsc_session_open(B.s, &id);
+        DeviceBatcher::check(wsc_session_open(B.s, &id), "wsc_session_open");
         return (int)id;
     }
     void feed(int conn, const uint8_t* p, size_t n) override {
         std::lock_guard<std::mutex> lk(B.mu);
-        wsc_session_feed(B.s, (uint32_t)conn, p, n);
+        DeviceBatcher::check(wsc_session_feed(B.s, (uint32_t)conn, p, n), "wsc_session_feed");
     }
     void eof(int conn) override {
         std::lock_guard<std::mutex> lk(B.mu);
@@ -231,7 +238,8 @@ int main(int argc, char** argv) {
     // --blocking-wait: the session sleeps on a blocking-sync event while the device works instead
     // of spinning in hipStreamSynchronize (WSC_SESSION_BLOCKING_WAIT): P pollers leave their cores
     // to the socket work
-    const uint32_t sflags = echo::has_flag(argc, argv, "--blocking-wait") ? WSC_SESSION_BLOCKING_WAIT : 0u;
+    const uint32_t sflags = (echo::has_flag(argc, argv, "--blocking-wait") ? WSC_SESSION_BLOCKING_WAIT : 0u) |
+                            (echo::has_flag(argc, argv, "--session-timing") ? WSC_SESSION_TIMING : 0u);
     int devices = 1;
     for (int i = 1; i + 1 < argc; ++i)
         if (std::string(argv[i]) == "--devices") devices = atoi(argv[i + 1]);
