@@ -751,7 +751,10 @@ def echo_configs(with_cpu=True):
     run is a separate process; msgs/s and GiB/s of echoed payload, every byte checked.  P pollers
     (netman runs NumCPU, eventloop/event.go:33-37): connection i on poller i % P, each poller its
     own decoder -- for the GPU its own wsc_session on the one device.  One read(2) takes at most
-    4 MiB per connection and round unless a row says otherwise (--read-bytes)."""
+    4 MiB per connection and round unless a row says otherwise (--read-bytes).  Every run also
+    reports the server's CPU seconds (the whole process minus the client threads: pollers plus the
+    HIP runtime's and any batching thread) and those per GiB echoed -- both servers are client-bound
+    on loopback from 4 pollers on, so GiB/s cannot tell them apart; the CPU the server spends can."""
     import subprocess
     gpu = os.path.join(ROOT, "tools", "ws_echo")
     cpu = os.path.join(ROOT, "oracle", "_build", "ws_echo_cpu")
@@ -760,7 +763,7 @@ def echo_configs(with_cpu=True):
     for P in (1, 4, 8):
         runs.append((f"64 conns x 200 x 64 KiB, {P} poller(s)", ["--conns", "64", "--frames", "200", "--size", "65536",
                                                                   "--client-threads", "4", "--pollers", str(P)],
-                     ["gpu", "gpu_blocking_wait", "cpu_port"] if P == 8 else ["gpu", "cpu_port"]))
+                     ["gpu", "gpu_blocking_wait", "cpu_port"]))
         # the same traffic with at most 512 KiB per read(2) (--read-bytes): more, smaller rounds.  The
         # echo is client-bound from 4 pollers on (ECHO_TIMING: the pollers' loops are busy ~1/3 of
         # the run), and how early the replies go out moves both servers by 10-40 %
@@ -783,7 +786,8 @@ def echo_configs(with_cpu=True):
             p = subprocess.run([exe] + args, capture_output=True, text=True, timeout=120)
             line = [x for x in p.stdout.splitlines() if x.startswith("{")]
             d = json.loads(line[-1]) if line else {"ok": False, "error": p.stderr[-300:]}
-            return {k: d.get(k) for k in ("ok", "gib_s", "msgs_per_s", "seconds", "rounds", "error")}
+            return {k: d.get(k) for k in ("ok", "gib_s", "msgs_per_s", "seconds", "rounds", "server_cpu_s",
+                                          "server_cpu_s_per_gib", "poller_cpu_s_per_gib", "client_cpu_s", "error")}
         except Exception as e:   # the echo lines are reported beside the metric, never fatal
             return {"ok": False, "error": repr(e)[:200]}
 
@@ -805,7 +809,10 @@ def echo_configs(with_cpu=True):
             if not good:
                 row[kind] = next((r for r in rs if r), None)
                 continue
-            row[kind] = dict(good[len(good) // 2], gib_s_runs=[r["gib_s"] for r in rs if r and r.get("ok")])
+            row[kind] = dict(good[len(good) // 2], gib_s_runs=[r["gib_s"] for r in rs if r and r.get("ok")],
+                             # what the server costs its host per GiB echoed, whatever the clients allow
+                             # through loopback: the median over the runs, beside the median run's rate
+                             server_cpu_s_per_gib_median=float(np.median([r["server_cpu_s_per_gib"] for r in good])))
             if len(good) < len(rs):
                 row[kind]["failed_runs"] = len(rs) - len(good)
         res[name] = row

@@ -27,6 +27,7 @@
 #include <netinet/in.h>
 #include <netinet/tcp.h>
 #include <sys/epoll.h>
+#include <sys/resource.h>
 #include <sys/socket.h>
 #include <sys/uio.h>
 #include <unistd.h>
@@ -42,6 +43,7 @@
 #include <memory>
 #include <mutex>
 #include <random>
+#include <ctime>
 #include <string>
 #include <thread>
 #include <vector>
@@ -82,9 +84,26 @@ struct Result {
     uint64_t messages = 0;
     uint64_t payload_bytes = 0;
     uint64_t rounds = 0;   // server epoll rounds that decoded something (= decode passes)
+    // CPU seconds over the timed run (CLOCK_THREAD_CPUTIME_ID / getrusage): what the server costs
+    // its host, beside what it delivers.  poller = the P poller threads; server = the whole process
+    // minus the client threads (the poller threads plus any helper thread the server starts: the HIP
+    // runtime's, the --batcher thread); client = the client threads (load generator, not the server)
+    double poller_cpu_s = 0, server_cpu_s = 0, client_cpu_s = 0;
     bool ok = false;
     std::string error;
 };
+
+inline double thread_cpu_s() {
+    timespec t{};
+    clock_gettime(CLOCK_THREAD_CPUTIME_ID, &t);
+    return (double)t.tv_sec + 1e-9 * (double)t.tv_nsec;
+}
+inline double process_cpu_s() {
+    rusage u{};
+    getrusage(RUSAGE_SELF, &u);
+    return (double)u.ru_utime.tv_sec + 1e-6 * (double)u.ru_utime.tv_usec + (double)u.ru_stime.tv_sec +
+           1e-6 * (double)u.ru_stime.tv_usec;
+}
 
 inline void set_nonblock(int fd) { fcntl(fd, F_SETFL, fcntl(fd, F_GETFL) | O_NONBLOCK); }
 
@@ -234,6 +253,8 @@ inline Result run(const DecoderFactory& make_decoder, int pollers, int conns, in
     std::atomic<uint64_t> client_msgs{0};
     std::atomic<bool> go{false};
     std::atomic<int> ready{0};   // clients whose wire images are built (not timed)
+    std::mutex cpu_mu;
+    double client_cpu = 0;       // CPU seconds of the client threads from `go` to their end
     std::vector<std::thread> clients;
     for (int t = 0; t < client_threads; ++t) {
         clients.emplace_back([&, t] {
@@ -253,6 +274,17 @@ inline Result run(const DecoderFactory& make_decoder, int pollers, int conns, in
             }
             ready++;
             while (!go.load()) std::this_thread::yield();
+            const double cpu0 = thread_cpu_s();
+            struct CpuTally {   // added at every exit of this thread
+                std::mutex& mu;
+                double& acc;
+                double c0;
+                ~CpuTally() {
+                    const double d = thread_cpu_s() - c0;
+                    std::lock_guard<std::mutex> g(mu);
+                    acc += d;
+                }
+            } tally{cpu_mu, client_cpu, cpu0};
             const int ep = epoll_create1(0);
             for (size_t i = 0; i < fds.size(); ++i) {
                 epoll_event e{};
@@ -338,6 +370,7 @@ inline Result run(const DecoderFactory& make_decoder, int pollers, int conns, in
         uint64_t served = 0, payload = 0, rounds = 0;
         std::string error;
         double t[6] = {0, 0, 0, 0, 0, 0};   // ECHO_TIMING=1: epoll_wait, reads, decode/submit, echo, complete, sends
+        double cpu = 0;                      // the thread's CPU seconds over its loop and final flush
     };
     const bool timing = [] { const char* e = std::getenv("ECHO_TIMING"); return e && e[0] == '1'; }();
     auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
@@ -369,10 +402,12 @@ inline Result run(const DecoderFactory& make_decoder, int pollers, int conns, in
     }
     while (ready.load() < client_threads && client_fail.load() == 0) std::this_thread::yield();
     const auto t0 = std::chrono::steady_clock::now();
+    const double proc0 = process_cpu_s();
     go = true;
     const auto deadline = t0 + std::chrono::seconds(timeout_s);
 
     auto poller_loop = [&](Poller& P) {
+        const double cpu0 = thread_cpu_s();
         Decoder& dec = *P.dec;
         std::vector<ServerConn>& sc = P.sc;
         std::vector<uint8_t> rb(g_read_bytes < 4096 ? 4096 : g_read_bytes);   // one read(2) per connection and round
@@ -527,6 +562,7 @@ inline Result run(const DecoderFactory& make_decoder, int pollers, int conns, in
                 if (c.out.send_some(c.fd) <= 0) std::this_thread::yield();
         }
         if (!P.error.empty()) client_fail++;   // release the client threads
+        P.cpu = thread_cpu_s() - cpu0;
     };
     std::vector<std::thread> server;
     if (res.error.empty())
@@ -536,7 +572,11 @@ inline Result run(const DecoderFactory& make_decoder, int pollers, int conns, in
     for (auto& t : server) t.join();
     for (auto& t : clients) t.join();
     const auto t1 = std::chrono::steady_clock::now();
+    const double proc1 = process_cpu_s();
     res.seconds = std::chrono::duration<double>(t1 - t0).count();
+    res.client_cpu_s = client_cpu;
+    res.server_cpu_s = (proc1 - proc0) - client_cpu;
+    for (auto& P : pl) res.poller_cpu_s += P.cpu;
     for (auto& P : pl) {
         res.messages += P.served;
         res.payload_bytes += P.payload;
@@ -558,12 +598,15 @@ inline void print_json(const char* codec, const Result& r, int pollers, int conn
                        int devices = 0, bool shutdown_wr = false) {
     printf("{\"codec\": \"%s\", \"devices\": %d, \"shutdown\": %s, \"ok\": %s, \"pollers\": %d, \"connections\": %d, \"frames_per_conn\": %d, \"frame_bytes\": %zu, "
            "\"seconds\": %.4f, \"messages\": %llu, \"msgs_per_s\": %.1f, \"gib_s\": %.3f, \"rounds\": %llu, "
-           "\"error\": \"%s\"}\n",
+           "\"poller_cpu_s\": %.4f, \"server_cpu_s\": %.4f, \"client_cpu_s\": %.4f, "
+           "\"server_cpu_s_per_gib\": %.4f, \"poller_cpu_s_per_gib\": %.4f, \"error\": \"%s\"}\n",
            codec, devices, shutdown_wr ? "true" : "false", r.ok ? "true" : "false", pollers, conns, frames, frame_bytes,
            r.seconds, (unsigned long long)r.messages,
            r.seconds > 0 ? (double)r.messages / r.seconds : 0.0,
            r.seconds > 0 ? (double)r.payload_bytes / r.seconds / 1073741824.0 : 0.0, (unsigned long long)r.rounds,
-           r.error.c_str());
+           r.poller_cpu_s, r.server_cpu_s, r.client_cpu_s,
+           r.payload_bytes ? r.server_cpu_s / ((double)r.payload_bytes / 1073741824.0) : 0.0,
+           r.payload_bytes ? r.poller_cpu_s / ((double)r.payload_bytes / 1073741824.0) : 0.0, r.error.c_str());
 }
 
 inline bool has_flag(int argc, char** argv, const char* flag) {
