@@ -73,6 +73,97 @@ __device__ __forceinline__ void hdr_bytes(const uint4& hd, uint32_t (&h)[14]) {
     for (int k = 0; k < 14; ++k) h[k] = (d[k >> 2] >> (8 * (k & 3))) & 0xFFu;
 }
 
+// ---- eager unmask (mode 65 helpers; see WalkArgs.eager) -----------------------------------------
+// A walking lane that has just found a complete plain BIN payload [src, src + plen) with key `key`
+// pushes the chunks of EAGER_WIN whole windows lying inside it (at most 127 per payload: the rest,
+// and the payload's edge windows, stay with k_unmask).  Any subset of the wave's lanes may call it
+// (the walk's control flow diverges): offsets come from bit-sliced ballots over the active lanes,
+// one queue atomic per wave.  Entries are two 8-byte agent-scope (sc1) stores, each tagged with
+// the decode's seq, so a reader never takes a stale or torn entry (MI355X_MICROARCH.md, granules).
+__device__ __forceinline__ void eager_push(const WalkArgs& a, uint64_t src, uint64_t plen, uint32_t key) {
+    const uint64_t A = (src + (1ull << a.win_shift) - 1) >> a.win_shift, B = (src + plen) >> a.win_shift;
+    uint32_t n = B > A ? (uint32_t)((B - A) / EAGER_WIN) : 0u;
+    if (n > 127) n = 127;
+    const uint64_t act = __ballot(true);
+    if (__ballot(n != 0) == 0) return;
+    uint32_t total = 0, below = 0;
+#pragma unroll
+    for (uint32_t b = 0; b < 7; ++b) {
+        const uint64_t m = __ballot((n >> b) & 1u);
+        total += (uint32_t)__builtin_popcountll(m) << b;
+        below += __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) << b;
+    }
+    const uint32_t leader = (uint32_t)__builtin_ctzll(act);
+    uint32_t base = 0;
+    if (lane_id() == leader) base = __hip_atomic_fetch_add(a.eager_q, total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)leader) + below;
+    const uint64_t tag = (uint64_t)a.seq << 32;
+    for (uint32_t k = 0; k < n; ++k) {
+        const uint32_t i = base + k;
+        if (i >= a.eager_cap) break;
+        __hip_atomic_store(a.eager_ent + 2ull * i, tag | (uint32_t)(A + (uint64_t)k * EAGER_WIN), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(a.eager_ent + 2ull * i + 1, tag | key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// A helper wave (mode 65: waves 1..3 of a block while wave 0 walks): claims queue entries in order
+// and unmasks each chunk in place -- EAGER_WIN windows inside one payload, one key, 16 B per lane
+// per 1 KiB, every load in flight at once -- then marks the windows done for k_unmask.  It stops at
+// its block's end of count (`stop`, set in LDS by the walking wave): a claimed entry that has not
+// been written by then is left to k_unmask (its windows are never marked), so no wave ever waits
+// on another block.
+__device__ __forceinline__ void eager_help(const WalkArgs& a, const uint32_t* stop) {
+    const uint32_t lane = lane_id();
+    const uint64_t seq = a.seq;
+    auto stopped = [&]() { return __hip_atomic_load(stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0u; };
+    auto rd = [&](const uint32_t* p) {
+        return (uint32_t)__builtin_amdgcn_readfirstlane(
+            (int)__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    };
+    // claim an entry only when one has been pushed and not yet claimed: an idle helper polls the
+    // two queue counters with long sleeps instead of hammering an empty slot (text batches push
+    // nothing); a claim that loses the race for the last entry waits for its slot like the others
+    auto claim = [&]() -> uint32_t {
+        for (uint32_t spin = 0; spin < (1u << 18); ++spin) {
+            if (stopped()) return a.eager_cap;
+            if (rd(a.eager_q + 1) < rd(a.eager_q)) {
+                uint32_t i = 0;
+                if (lane == 0) i = __hip_atomic_fetch_add(a.eager_q + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                return (uint32_t)__builtin_amdgcn_readfirstlane((int)i);
+            }
+            __builtin_amdgcn_s_sleep(16);
+        }
+        return a.eager_cap;
+    };
+    uint32_t i = claim();
+    while (i < a.eager_cap) {
+        uint64_t v0 = 0, v1 = 0;
+        bool ok = false;
+        for (uint32_t spin = 0; spin < (1u << 18); ++spin) {
+            v0 = __hip_atomic_load(a.eager_ent + 2ull * i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            v1 = __hip_atomic_load(a.eager_ent + 2ull * i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ok = (v0 >> 32) == seq && (v1 >> 32) == seq;
+            if (ok || stopped()) break;
+            __builtin_amdgcn_s_sleep(2);
+        }
+        ok = __builtin_amdgcn_readfirstlane((int)ok) != 0;
+        if (!ok) return;   // (claimed, never written before the stop: k_unmask does its windows)
+        const uint32_t w0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v0);
+        const uint32_t key = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v1);
+        constexpr uint32_t CH = EAGER_WIN * 4096u;
+        uint8_t* base = const_cast<uint8_t*>(a.wire) + ((uint64_t)w0 << a.win_shift);
+        const __amdgpu_buffer_rsrc_t rs = win_rsrc(base, CH);
+        u32x4 v[EAGER_WIN * 4];
+#pragma unroll
+        for (uint32_t k = 0; k < EAGER_WIN * 4; ++k) v[k] = ld16b<2>(rs, k * 1024u + lane * 16u);
+#pragma unroll
+        for (uint32_t k = 0; k < EAGER_WIN * 4; ++k) st16b<19>(rs, k * 1024u + lane * 16u, v[k] ^ key);
+        if (lane < EAGER_WIN) a.win_done[w0 + lane] = a.seq;
+        i = claim();
+    }
+}
+
 // Output side of the walk: everything a frame writes (record, arena offset, span, window index)
 // and what a segment writes at its end.  Shared by the LDS replay and the re-walking emitter so
 // both produce identical outputs.
@@ -813,6 +904,8 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
             sflags |= SEGF_UTF8;
             if constexpr (!EMIT) defer(pos + hl, plen, mask, false, false, hl);
         }
+        if constexpr (!EMIT && !PURE && !COMPACT)
+            if (a.eager && !text) eager_push(a, pos + hl, plen, rotr32(mask, 8u * ((uint32_t)(0u - (uint32_t)(pos + hl)) & 3u)));
         const bool have_span = plen > 0;
         if constexpr (EMIT) emit_frame<COMPACT>(a, e, fr, plen, have_span, 0);
         else record(fr, have_span, 0, plen);
@@ -1099,6 +1192,14 @@ __device__ __forceinline__ void quad_prefix(const WalkArgs& a, uint32_t s, uint3
                     bytes_x += pl[j];
                     lend_x = hp[j] + sz[j];
                 }
+            }
+        }
+        if (a.eager) {   // large payloads among the taken candidates: chunks for the helper waves
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const bool take = 4 * q + j < r && pl[j] != 0;
+                const uint64_t src = hp[j] + hlj[j];
+                if (take) eager_push(a, src, pl[j], rotr32(mk[j], 8u * ((uint32_t)(0u - (uint32_t)src) & 3u)));
             }
         }
         // the quad's state after the run: the last taken candidate's end and size
@@ -1510,10 +1611,12 @@ __global__ __launch_bounds__(NT) void k_walk_fused(WalkArgs a) {
     // (The pass loop below also serves PASSES > 1; a pass finding no plain BIN message at all --
     // fragmented or text traffic -- skips the rest.)
     constexpr bool PRE = G == 1 && SPREAD == 0 && NT == 4 * WL;
+    __shared__ uint32_t sh_counted, sh_looked;   // eager unmask: the walking wave has counted / looked back (helpers stop)
     if constexpr (PRE) {
         constexpr uint32_t NQ = NT / 4, PASSES = WL / NQ;
         __shared__ uint32_t sh_found;
         if (lane == 0) sh_found = 0;
+        if (lane == 0) sh_counted = sh_looked = 0;
         if (lane < WL) {   // (segments no pass reaches -- skipped passes -- keep these)
             L.pre[lane].nf = 0;
             L.pre[lane].full = false;
@@ -1538,12 +1641,27 @@ __global__ __launch_bounds__(NT) void k_walk_fused(WalkArgs a) {
     // walking column: in lane order, so the block scan over physical lanes stays in segment order
     const uint32_t col = SPREAD == 0 ? lane : (wl < SPREAD && wave < WL / (SPREAD ? SPREAD : 1)) ? wave * SPREAD + wl : WL + lane;
     const SegCount tot = tile_count<COMPACT, KR, NT, G>(a, L, (bid * WL + col) * G, a.n_segs, col, nrec, PRE);
+    if constexpr (PRE && !COMPACT) {
+        // eager unmask: while wave 0 walks, waves 1..3 unmask the large payloads the walkers found
+        if (a.eager) {
+            if (wave == 0) {
+                if (lane == 0) __hip_atomic_store(&sh_counted, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            } else {
+                eager_help(a, &sh_counted);
+            }
+        }
+    }
     SegCount btot;
     const SegCount excl = tile_scan<NT>(tot, L, wl, wave, btot);
     if (wave == 0) {
         if (a.dbg && wl == 0) t1 = __builtin_amdgcn_s_memrealtime();
         const SegCount prefix = block_lookback(a, bid, btot, wl);
         if (wl == 0) L.prefix = prefix;
+        if constexpr (PRE && !COMPACT)   // eager unmask: the helpers stop (second phase)
+            if (a.eager && wl == 0) __hip_atomic_store(&sh_looked, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    } else if constexpr (PRE && !COMPACT) {
+        // ... and while it waits on its predecessors in the look-back, the other waves go on helping
+        if (a.eager) eager_help(a, &sh_looked);
     }
     __syncthreads();
     if (a.dbg && lane == 0) t2 = __builtin_amdgcn_s_memrealtime();
@@ -1560,6 +1678,80 @@ __global__ __launch_bounds__(NT) void k_walk_fused(WalkArgs a) {
     if (bid == n_blocks - 1 && lane == 0) write_summary<COMPACT>(a, sc_add(L.prefix, btot));
 }
 
+// A segment that is exactly ONE complete plain masked FIN BIN frame of a connection with nothing
+// open (status OPEN, no fragmented message, no streamed frame): websocket.go:142-146 then
+// websocket_frame.go:52-91 -- Message{MsgID, Opcode 2}, messageMode 0, msgID + 1.  walk_segment's
+// `fast` path for it counts {1 frame, 1 span, plen bytes} and emits what emit_simple writes; the
+// tiled walk (one connection read per segment, the commonest shape at 1 M segments) takes it
+// without the state machine in both passes.  (plen > 0: a span; the segment < 4 GiB.)
+struct SimpleSeg {
+    uint32_t plen, mask, hl;
+};
+__device__ __forceinline__ bool simple_seg(const WalkArgs& a, const SegIn& x, SimpleSeg& o) {
+    if (x.st.status != WSC_SEG_OPEN || x.st.cont_len != 0 || x.st.frame_rem != 0) return false;
+    const uint4 hd = x.hdr;
+    const uint32_t b0 = hd.x & 0xFFu, b1 = (hd.x >> 8) & 0xFFu;
+    if (b0 != 0x82u || !(b1 & 0x80u)) return false;
+    const uint32_t len7 = b1 & 0x7Fu;
+    uint64_t plen;
+    if (len7 < 126) {
+        plen = len7;
+        o.mask = __builtin_amdgcn_alignbyte(hd.y, hd.x, 2);
+        o.hl = 6;
+    } else if (len7 == 126) {
+        plen = ((hd.x >> 8) & 0xFF00u) | (hd.x >> 24);
+        o.mask = hd.y;
+        o.hl = 8;
+    } else {
+        const uint64_t v = (uint64_t)__builtin_amdgcn_alignbyte(hd.y, hd.x, 2) |
+                           (uint64_t)__builtin_amdgcn_alignbyte(hd.z, hd.y, 2) << 32;
+        plen = __builtin_bswap64(v);
+        o.mask = __builtin_amdgcn_alignbyte(hd.w, hd.z, 2);
+        o.hl = 14;
+    }
+    if (plen == 0 || plen > 0xFFFFFFFFull || plen > a.max_frame_len) return false;
+    o.plen = (uint32_t)plen;
+    return x.end - x.start == (uint64_t)o.hl + plen;
+}
+
+// The outputs walk_segment<EMIT> writes for a simple segment s (frame fi, span si): its record, span,
+// window-index entries (windows starting inside the segment look the span up), result and carried
+// state -- consecutive lanes hold consecutive segments, so every store is coalesced.
+__device__ __forceinline__ void emit_simple(const WalkArgs& a, uint32_t s, const SegIn& x, const SimpleSeg& g,
+                                            uint32_t fi, uint32_t si) {
+    const uint32_t msg = x.st.msg_id;
+    if (fi < a.frames_cap) {
+        const uint4 r0 = make_uint4((uint32_t)x.start, (uint32_t)(x.start >> 32), g.plen, g.mask);
+        const uint4 r1 = make_uint4(s, msg, 2u | 1u << 8 | (uint32_t)WSC_FK_MESSAGE << 16 | 2u << 24,
+                                    (uint32_t)WSC_ERR_NONE | g.hl << 8 | (uint32_t)WSC_FF_UNMASKED << 16);
+        reinterpret_cast<uint4*>(a.frames + fi)[0] = r0;
+        reinterpret_cast<uint4*>(a.frames + fi)[1] = r1;
+    }
+    const uint64_t src = x.start + g.hl;
+    if (si < a.spans_cap) {
+        Span sp;
+        sp.src = src;
+        sp.dst = src;
+        sp.len = g.plen;
+        sp.key = rotr32(g.mask, 8u * ((uint32_t)(0u - (uint32_t)src) & 3u));
+        a.spans[si] = sp;
+    }
+    const uint64_t W = 1ull << a.win_shift;
+    for (uint64_t w = (x.start + W - 1) >> a.win_shift; (w << a.win_shift) < x.end; ++w) a.tile_first[w] = si;
+    wsc_seg_result r;
+    r.consumed = x.end - x.start;
+    r.frame_begin = fi;
+    r.frame_count = 1;
+    r.status = WSC_SEG_OPEN;
+    r.close_code = 0;
+    r.err = 0;
+    r.pad = 0;
+    a.seg_out[s] = r;
+    wsc_conn_state o{};
+    o.msg_id = msg + 1;
+    a.state_out[s] = o;
+}
+
 // Tiled walk for batches of many (short) segments (more than 256 per CU: one connection read per
 // segment, e.g. configs[1] with one frame per segment).  A persistent grid whose blocks are all
 // resident; block b (by ticket) owns the contiguous segments [b * per, (b + 1) * per) and walks
@@ -1568,7 +1760,9 @@ __global__ __launch_bounds__(NT) void k_walk_fused(WalkArgs a) {
 //            the block's total;
 //   look-back  the block's prefix (every block is running, so no block waits on one not started);
 //   phase 2  per tile: the count walk again with LDS records (headers now cache-warm), tile scan
-//            on top of the running prefix, cooperative emit from LDS.
+//            on top of the running prefix, cooperative emit from LDS -- or, for a tile whose
+//            segments are each one complete plain BIN frame (simple_seg), each lane's outputs
+//            written straight from its cached header (emit_simple).
 // One launch and no per-segment counts in HBM (the three-launch walk wrote and re-read 32 B of
 // counts per segment and re-walked every header in its emit pass).
 template <bool COMPACT, uint32_t KR, uint32_t NT>
@@ -1612,9 +1806,18 @@ __global__ __launch_bounds__(NT) void k_walk_tiled(WalkArgs a, uint32_t per_bloc
         for (uint32_t t = sb; t < se; t += NT) {
             if (t + NT < se) first_hdr(x1);
             bounds(t + 2 * NT, x2);
-            if (t + lane < se)
-                tot = sc_add(tot, walk_segment<false, COMPACT, NT, 4, true>(a, t + lane, zero, zero, nullptr, nullptr, nullptr, 0,
-                                                                            0, nullptr, &x0, a.hdr_cache));
+            if (t + lane < se) {
+                SimpleSeg g;
+                if (!COMPACT && simple_seg(a, x0, g)) {   // what walk_segment's count returns for it
+                    tot.frames += 1;
+                    tot.spans0 += 1;
+                    tot.bytes0 += g.plen;
+                    if (a.hdr_cache) a.hdr_cache[t + lane] = x0.hdr;
+                } else {
+                    tot = sc_add(tot, walk_segment<false, COMPACT, NT, 4, true>(a, t + lane, zero, zero, nullptr, nullptr,
+                                                                                nullptr, 0, 0, nullptr, &x0, a.hdr_cache));
+                }
+            }
             x0 = x1;
             x1 = x2;
         }
@@ -1641,6 +1844,35 @@ __global__ __launch_bounds__(NT) void k_walk_tiled(WalkArgs a, uint32_t per_bloc
     cached(sb, y0);
     for (uint32_t t = sb; t < se; t += NT) {
         cached(t + NT, y1);
+        if constexpr (!COMPACT) {
+            // a tile of simple segments only (one complete plain BIN frame each): frame and span
+            // ordinals are the lane's, so each lane writes its outputs straight from the cached
+            // header -- no second walk, no LDS records, no cooperative emit
+            const bool mine = t + lane < se;
+            SimpleSeg g{};
+            const bool simple = !mine || simple_seg(a, y0, g);
+            if (__syncthreads_and(simple)) {
+                const uint32_t n = se - t < NT ? se - t : NT;
+                uint64_t b = mine ? g.plen : 0u;
+#pragma unroll
+                for (int d = 32; d >= 1; d >>= 1) {
+                    const uint32_t lo = __shfl_xor((uint32_t)b, d), hi = __shfl_xor((uint32_t)(b >> 32), d);
+                    b += (uint64_t)hi << 32 | lo;
+                }
+                if (wl == 0) L.wave[wave].bytes0 = b;
+                if (mine) emit_simple(a, t + lane, y0, g, run.frames + lane, run.spans0 + run.spans1 + lane);
+                __syncthreads();
+                uint64_t bsum = 0;
+#pragma unroll
+                for (uint32_t w = 0; w < NT / 64; ++w) bsum += L.wave[w].bytes0;
+                run.frames += n;
+                run.spans0 += n;
+                run.bytes0 += bsum;
+                y0 = y1;
+                __syncthreads();   // (L.wave is reused by the next tile)
+                continue;
+            }
+        }
         uint32_t nrec;   // (lanes past the block's last segment count nothing)
         const SegCount c = tile_count<COMPACT, KR, NT, 1>(a, L, t + lane, se, lane, nrec, false, &y0);
         y0 = y1;

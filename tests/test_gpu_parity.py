@@ -722,3 +722,48 @@ def test_sharded_decode_equals_unsharded(codec, world):
     assert np.array_equal(merged_wire, whole_wire)
     for i, s in enumerate(streams):
         compare_segment(i, s, int(off[i]), whole, O.run(s), wire_after=whole_wire)
+
+
+@pytest.mark.parametrize("inline_max", [256, 0])
+def test_eager_unmask_during_walk(codec_lib, monkeypatch, inline_max):
+    """The eager unmask (an in-place, one-stream decode whose walk is mode 65 with >= 128 blocks):
+    while each block's walking wave counts and looks back, its other waves unmask the interiors of
+    large plain BIN payloads the walkers found (quad pre-pass and serial walk alike), and k_unmask
+    skips those windows.  9,000 connections: fuzz streams (text, errors, control frames), runs of
+    equal BIN frames, and one in 25 carrying payloads of 17 KiB .. 1 MiB -- whole, cut at the
+    segment's end (a streamed piece: never pushed), as a fragment (FIN=0: never pushed) or as TEXT
+    (deferred UTF-8: never pushed).  Every segment equals the oracle, record for record and byte
+    for byte; the wire outside payloads is untouched."""
+    monkeypatch.setitem(K.CFG_DEFAULTS, "u8_inline_max", inline_max)
+    rng = np.random.default_rng(2606)
+    streams = []
+    for i in range(9000):
+        if i % 25 == 7:
+            parts = [synth.frame(2, b"h" * int(rng.integers(0, 300)), rng=rng)]
+            for _ in range(int(rng.integers(1, 4))):
+                n = int(rng.choice([17 << 10, 64 << 10, 65535, 100003, 1 << 20]))
+                body = bytes(rng.integers(0, 256, n, dtype=np.uint8))
+                kind = rng.random()
+                if kind < 0.6:
+                    parts.append(synth.frame(2, body, rng=rng))
+                elif kind < 0.75:
+                    parts.append(synth.frame(2, body, fin=False, rng=rng) + synth.frame(0, b"end", rng=rng))
+                else:
+                    parts.append(synth.frame(1, ("é" * (n // 2)).encode(), rng=rng))
+            s = b"".join(parts)
+            if rng.random() < 0.3:   # the segment ends inside its last payload: a streamed piece
+                s = s[:len(s) - int(rng.integers(1, 9000))]
+            streams.append(s)
+        elif i % 3 == 0:
+            streams.append(b"".join(synth.frame(2, bytes(rng.integers(0, 256, 125, dtype=np.uint8)), rng=rng)
+                                    for _ in range(int(rng.integers(1, 17)))))
+        else:
+            streams.append(random_stream(26000 + i, n_units=int(1 + i % 12), text_p=0.3))
+    c = K.Codec(0, max_batch_bytes=512 << 20, max_segs=1 << 14, max_frames=1 << 18)
+    try:
+        res = _check_batch(c, streams)
+        mode, blocks = c.walk_info()
+        assert mode == 65 and blocks >= 128, (mode, blocks)
+        assert c.error_flags() == 0
+    finally:
+        c.close()

@@ -282,3 +282,53 @@ def test_session_h2d_once_for_streamed_payloads(codec_lib):
     st = sess.stats()
     assert st["read"] == len(s) and st["h2d"] == len(s) and st["resent"] == 0, st
     sess.close()
+
+
+@pytest.mark.parametrize("compact", [False, True])
+def test_tiled_walk_simple_segment_tiles(codec_lib, monkeypatch, compact):
+    """The tiled walk's simple-segment path (a segment that is exactly one complete plain BIN frame
+    of an idle connection: no second walk, outputs straight from the cached header).  2,000
+    connections over 4 device batches, cut at frame edges: connections 0..767 send one BIN frame per
+    batch (whole tiles of simple segments, carried msgIDs > 0 from the second batch on; payloads of
+    1..125 B, 126..65535 B and > 64 KiB: 6, 8 and 14-byte headers), the others mix in empty BIN
+    frames, two frames per segment, TEXT and fragmented messages, and cuts inside a frame -- so tiles
+    of the same batch take both paths.  Every connection equals the oracle on its whole stream."""
+    monkeypatch.setitem(K.CFG_DEFAULTS, "walk_mode", 3)
+    rng = np.random.default_rng(606)
+    sizes = [1, 5, 125, 126, 1000, 4093, 65535, 65536, 70001]
+    streams, cuts = [], []
+    for i in range(2000):
+        frames = []
+        for k in range(4):
+            if i < 768:
+                frames.append([synth.frame(2, bytes(rng.integers(0, 256, int(rng.choice(sizes)), dtype=np.uint8)), rng=rng)])
+                continue
+            r = rng.random()
+            if r < 0.2:
+                frames.append([synth.frame(2, b"", rng=rng)])
+            elif r < 0.4:
+                frames.append([synth.frame(2, b"ab", rng=rng), synth.frame(2, b"cde", rng=rng)])
+            elif r < 0.6:
+                frames.append([synth.frame(1, "ü".encode() * int(rng.integers(1, 200)), rng=rng)])
+            elif r < 0.8:
+                frames.append([synth.frame(2, b"x" * 300, fin=False, rng=rng), synth.frame(0, b"y" * 20, rng=rng)])
+            else:
+                frames.append([synth.frame(2, bytes(int(rng.integers(1, 3000))), rng=rng)])
+        parts = [b"".join(f) for f in frames]
+        s = b"".join(parts)
+        c = list(np.cumsum([len(p) for p in parts])[:-1])
+        if i >= 768 and rng.random() < 0.2:   # a cut inside a frame: that segment streams a piece
+            c[1] = c[1] - int(rng.integers(1, 5))
+        streams.append(s)
+        cuts.append(c)
+    c = K.Codec(0, max_batch_bytes=64 << 20, max_segs=1 << 12, max_frames=1 << 16)
+    try:
+        got = decode_in_parts(c, streams, cuts, compact=compact)
+        assert c.walk_info()[0] == 3
+        for i, (g, s) in enumerate(zip(got, streams)):
+            try:
+                check_against_oracle(s, g, O.run(s))
+            except AssertionError as e:
+                raise AssertionError(f"stream {i}: {e}") from None
+    finally:
+        c.close()
