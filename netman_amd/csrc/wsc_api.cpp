@@ -114,12 +114,6 @@ struct wsc_ctx {
     uint32_t max_walk_blocks = 0;       // look-back state allocated for this many walk blocks
     uint4* hdr_cache = nullptr;         // tiled walk: per segment, its first 16 header bytes (WSC_WALK_NO_HDR_CACHE: off)
     uint32_t* stride_hint = nullptr;    // quad pre-pass: the frame stride the last decode ended with
-    // eager unmask (WalkArgs.eager): queue counters, entries, per-window done tags, decode tag
-    uint32_t* eager_q = nullptr;
-    uint64_t* eager_ent = nullptr;
-    uint32_t eager_cap = 0;
-    uint32_t* win_done = nullptr;
-    uint32_t seq = 0;
     uint64_t tile_entries = 0;
     // host-staged path buffers (lazily allocated)
     uint8_t* d_wire = nullptr;
@@ -331,16 +325,9 @@ int wsc_create(int device, const wsc_config* cfg_in, wsc_ctx** out) {
     chk(hipMalloc(&c->win_flag, c->tile_entries * sizeof(uint32_t)), "hipMalloc win_flag");
     chk(hipMalloc(&c->win_map, c->tile_entries * sizeof(uint64_t)), "hipMalloc win_map");
     chk(hipMalloc(&c->u8ctr, 64 * sizeof(uint32_t)), "hipMalloc u8ctr");
-    c->eager_cap = (uint32_t)(c->tile_entries / EAGER_WIN + 64);
-    chk(hipMalloc(&c->eager_q, 2 * sizeof(uint32_t)), "hipMalloc eager_q");
-    chk(hipMalloc(&c->eager_ent, (uint64_t)c->eager_cap * 2 * sizeof(uint64_t)), "hipMalloc eager_ent");
-    chk(hipMalloc(&c->win_done, c->tile_entries * sizeof(uint32_t)), "hipMalloc win_done");
     if (rc == WSC_OK) {
         chk(hipMemsetAsync(c->win_flag, 0, c->tile_entries * sizeof(uint32_t), c->stream), "hipMemset win_flag");
         chk(hipMemsetAsync(c->u8ctr, 0, 64 * sizeof(uint32_t), c->stream), "hipMemset u8ctr");
-        chk(hipMemsetAsync(c->eager_q, 0, 2 * sizeof(uint32_t), c->stream), "hipMemset eager_q");
-        chk(hipMemsetAsync(c->eager_ent, 0, (uint64_t)c->eager_cap * 2 * sizeof(uint64_t), c->stream), "hipMemset eager_ent");
-        chk(hipMemsetAsync(c->win_done, 0, c->tile_entries * sizeof(uint32_t), c->stream), "hipMemset win_done");
         chk(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
     }
     c->quad_pre = !(cfg.walk_flags & WSC_WALK_NO_QUAD_PRE);
@@ -376,7 +363,7 @@ int wsc_destroy(wsc_ctx* c) {
                     c->d_seg_off, c->d_state_in, c->d_state_out, c->d_seg_out, c->d_frames,
                     c->d_frame_dst, c->d_summary, c->enc_lb_state, c->enc_lb_agg, c->enc_lb_incl, c->enc_tile,
                     c->d_enc_msgs, c->d_enc_src, c->d_enc_out, c->d_enc_off, c->u8items, c->u8maps, c->u8seg,
-                    c->win_flag, c->win_map, c->u8ctr, c->eager_q, c->eager_ent, c->win_done};
+                    c->win_flag, c->win_map, c->u8ctr};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -516,21 +503,6 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     const dim3 wblk(wnt), wgrid((n + spb - 1) / spb);
     if (phase != 2 && wgrid.x + 1 > c->max_walk_blocks)   // never index look-back state past its allocation
         return fail(WSC_E_INTERNAL, "walk geometry needs more look-back blocks than allocated");
-    // eager unmask: the one-stream decode of an in-place batch whose walk is mode 65 over the whole
-    // chip with at least 128 blocks (three helper waves per block; with fewer the queue would mostly
-    // fall through to k_unmask anyway).  The split / staged pipeline keeps the plain walk: its walk
-    // shares the chip with another batch's unmask.
-    const bool eager = !compact && !split && phase == 0 && mode == 65 && wgrid.x >= 128 &&
-                       stream_cus(c, st) >= (uint32_t)c->n_cu;
-    if (phase != 2) {
-        c->seq = c->seq + 1 ? c->seq + 1 : 1u;   // (never 0: the done tags start zeroed)
-    }
-    wa.eager = eager ? 1u : 0u;
-    wa.seq = c->seq;
-    wa.eager_cap = c->eager_cap;
-    wa.eager_q = c->eager_q;
-    wa.eager_ent = c->eager_ent;
-    wa.win_done = c->win_done;
     uint32_t rearm = 0;   // (after the launch below: the tiled walk sets walk_blocks)
     auto rec = [&](int i) {
         if (ev) (void)hipEventRecord(ev[i], st);
@@ -553,7 +525,6 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     if (stale) {   // ... and its look-back ticket / flags were not re-armed either
         HIP_TRY(hipMemsetAsync(c->u8ctr + 32 * par, 0, sizeof(uint32_t), ws));
         HIP_TRY(hipMemsetAsync(c->lb_state, 0, (c->max_walk_blocks + 3) * sizeof(uint32_t), ws));
-        HIP_TRY(hipMemsetAsync(c->eager_q, 0, 2 * sizeof(uint32_t), ws));
     }
     // fused: 16 frame records per lane in LDS (segments with more frames re-walk their headers)
     if (mode == 3) {
@@ -619,9 +590,6 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     U8Win uw{};
     uw.rearm = c->u8ctr + 32 * (c->u8par ^ 1u);
     uw.xcd_run = c->xcd_run;
-    uw.done = eager ? c->win_done : nullptr;
-    uw.seq = c->seq;
-    uw.eager_q = c->eager_q;
     if (need_u8) {
         uw.flag = c->win_flag;
         uw.map = c->win_map;

@@ -73,97 +73,6 @@ __device__ __forceinline__ void hdr_bytes(const uint4& hd, uint32_t (&h)[14]) {
     for (int k = 0; k < 14; ++k) h[k] = (d[k >> 2] >> (8 * (k & 3))) & 0xFFu;
 }
 
-// ---- eager unmask (mode 65 helpers; see WalkArgs.eager) -----------------------------------------
-// A walking lane that has just found a complete plain BIN payload [src, src + plen) with key `key`
-// pushes the chunks of EAGER_WIN whole windows lying inside it (at most 127 per payload: the rest,
-// and the payload's edge windows, stay with k_unmask).  Any subset of the wave's lanes may call it
-// (the walk's control flow diverges): offsets come from bit-sliced ballots over the active lanes,
-// one queue atomic per wave.  Entries are two 8-byte agent-scope (sc1) stores, each tagged with
-// the decode's seq, so a reader never takes a stale or torn entry (MI355X_MICROARCH.md, granules).
-__device__ __forceinline__ void eager_push(const WalkArgs& a, uint64_t src, uint64_t plen, uint32_t key) {
-    const uint64_t A = (src + (1ull << a.win_shift) - 1) >> a.win_shift, B = (src + plen) >> a.win_shift;
-    uint32_t n = B > A ? (uint32_t)((B - A) / EAGER_WIN) : 0u;
-    if (n > 127) n = 127;
-    const uint64_t act = __ballot(true);
-    if (__ballot(n != 0) == 0) return;
-    uint32_t total = 0, below = 0;
-#pragma unroll
-    for (uint32_t b = 0; b < 7; ++b) {
-        const uint64_t m = __ballot((n >> b) & 1u);
-        total += (uint32_t)__builtin_popcountll(m) << b;
-        below += __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) << b;
-    }
-    const uint32_t leader = (uint32_t)__builtin_ctzll(act);
-    uint32_t base = 0;
-    if (lane_id() == leader) base = __hip_atomic_fetch_add(a.eager_q, total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)leader) + below;
-    const uint64_t tag = (uint64_t)a.seq << 32;
-    for (uint32_t k = 0; k < n; ++k) {
-        const uint32_t i = base + k;
-        if (i >= a.eager_cap) break;
-        __hip_atomic_store(a.eager_ent + 2ull * i, tag | (uint32_t)(A + (uint64_t)k * EAGER_WIN), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(a.eager_ent + 2ull * i + 1, tag | key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-
-// A helper wave (mode 65: waves 1..3 of a block while wave 0 walks): claims queue entries in order
-// and unmasks each chunk in place -- EAGER_WIN windows inside one payload, one key, 16 B per lane
-// per 1 KiB, every load in flight at once -- then marks the windows done for k_unmask.  It stops at
-// its block's end of count (`stop`, set in LDS by the walking wave): a claimed entry that has not
-// been written by then is left to k_unmask (its windows are never marked), so no wave ever waits
-// on another block.
-__device__ __forceinline__ void eager_help(const WalkArgs& a, const uint32_t* stop) {
-    const uint32_t lane = lane_id();
-    const uint64_t seq = a.seq;
-    auto stopped = [&]() { return __hip_atomic_load(stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0u; };
-    auto rd = [&](const uint32_t* p) {
-        return (uint32_t)__builtin_amdgcn_readfirstlane(
-            (int)__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    };
-    // claim an entry only when one has been pushed and not yet claimed: an idle helper polls the
-    // two queue counters with long sleeps instead of hammering an empty slot (text batches push
-    // nothing); a claim that loses the race for the last entry waits for its slot like the others
-    auto claim = [&]() -> uint32_t {
-        for (uint32_t spin = 0; spin < (1u << 18); ++spin) {
-            if (stopped()) return a.eager_cap;
-            if (rd(a.eager_q + 1) < rd(a.eager_q)) {
-                uint32_t i = 0;
-                if (lane == 0) i = __hip_atomic_fetch_add(a.eager_q + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                return (uint32_t)__builtin_amdgcn_readfirstlane((int)i);
-            }
-            __builtin_amdgcn_s_sleep(16);
-        }
-        return a.eager_cap;
-    };
-    uint32_t i = claim();
-    while (i < a.eager_cap) {
-        uint64_t v0 = 0, v1 = 0;
-        bool ok = false;
-        for (uint32_t spin = 0; spin < (1u << 18); ++spin) {
-            v0 = __hip_atomic_load(a.eager_ent + 2ull * i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            v1 = __hip_atomic_load(a.eager_ent + 2ull * i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            ok = (v0 >> 32) == seq && (v1 >> 32) == seq;
-            if (ok || stopped()) break;
-            __builtin_amdgcn_s_sleep(2);
-        }
-        ok = __builtin_amdgcn_readfirstlane((int)ok) != 0;
-        if (!ok) return;   // (claimed, never written before the stop: k_unmask does its windows)
-        const uint32_t w0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v0);
-        const uint32_t key = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v1);
-        constexpr uint32_t CH = EAGER_WIN * 4096u;
-        uint8_t* base = const_cast<uint8_t*>(a.wire) + ((uint64_t)w0 << a.win_shift);
-        const __amdgpu_buffer_rsrc_t rs = win_rsrc(base, CH);
-        u32x4 v[EAGER_WIN * 4];
-#pragma unroll
-        for (uint32_t k = 0; k < EAGER_WIN * 4; ++k) v[k] = ld16b<2>(rs, k * 1024u + lane * 16u);
-#pragma unroll
-        for (uint32_t k = 0; k < EAGER_WIN * 4; ++k) st16b<19>(rs, k * 1024u + lane * 16u, v[k] ^ key);
-        if (lane < EAGER_WIN) a.win_done[w0 + lane] = a.seq;
-        i = claim();
-    }
-}
-
 // Output side of the walk: everything a frame writes (record, arena offset, span, window index)
 // and what a segment writes at its end.  Shared by the LDS replay and the re-walking emitter so
 // both produce identical outputs.
@@ -904,8 +813,6 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
             sflags |= SEGF_UTF8;
             if constexpr (!EMIT) defer(pos + hl, plen, mask, false, false, hl);
         }
-        if constexpr (!EMIT && !PURE && !COMPACT)
-            if (a.eager && !text) eager_push(a, pos + hl, plen, rotr32(mask, 8u * ((uint32_t)(0u - (uint32_t)(pos + hl)) & 3u)));
         const bool have_span = plen > 0;
         if constexpr (EMIT) emit_frame<COMPACT>(a, e, fr, plen, have_span, 0);
         else record(fr, have_span, 0, plen);
@@ -1192,14 +1099,6 @@ __device__ __forceinline__ void quad_prefix(const WalkArgs& a, uint32_t s, uint3
                     bytes_x += pl[j];
                     lend_x = hp[j] + sz[j];
                 }
-            }
-        }
-        if (a.eager) {   // large payloads among the taken candidates: chunks for the helper waves
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const bool take = 4 * q + j < r && pl[j] != 0;
-                const uint64_t src = hp[j] + hlj[j];
-                if (take) eager_push(a, src, pl[j], rotr32(mk[j], 8u * ((uint32_t)(0u - (uint32_t)src) & 3u)));
             }
         }
         // the quad's state after the run: the last taken candidate's end and size
@@ -1611,12 +1510,10 @@ __global__ __launch_bounds__(NT) void k_walk_fused(WalkArgs a) {
     // (The pass loop below also serves PASSES > 1; a pass finding no plain BIN message at all --
     // fragmented or text traffic -- skips the rest.)
     constexpr bool PRE = G == 1 && SPREAD == 0 && NT == 4 * WL;
-    __shared__ uint32_t sh_counted, sh_looked;   // eager unmask: the walking wave has counted / looked back (helpers stop)
     if constexpr (PRE) {
         constexpr uint32_t NQ = NT / 4, PASSES = WL / NQ;
         __shared__ uint32_t sh_found;
         if (lane == 0) sh_found = 0;
-        if (lane == 0) sh_counted = sh_looked = 0;
         if (lane < WL) {   // (segments no pass reaches -- skipped passes -- keep these)
             L.pre[lane].nf = 0;
             L.pre[lane].full = false;
@@ -1641,27 +1538,12 @@ __global__ __launch_bounds__(NT) void k_walk_fused(WalkArgs a) {
     // walking column: in lane order, so the block scan over physical lanes stays in segment order
     const uint32_t col = SPREAD == 0 ? lane : (wl < SPREAD && wave < WL / (SPREAD ? SPREAD : 1)) ? wave * SPREAD + wl : WL + lane;
     const SegCount tot = tile_count<COMPACT, KR, NT, G>(a, L, (bid * WL + col) * G, a.n_segs, col, nrec, PRE);
-    if constexpr (PRE && !COMPACT) {
-        // eager unmask: while wave 0 walks, waves 1..3 unmask the large payloads the walkers found
-        if (a.eager) {
-            if (wave == 0) {
-                if (lane == 0) __hip_atomic_store(&sh_counted, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            } else {
-                eager_help(a, &sh_counted);
-            }
-        }
-    }
     SegCount btot;
     const SegCount excl = tile_scan<NT>(tot, L, wl, wave, btot);
     if (wave == 0) {
         if (a.dbg && wl == 0) t1 = __builtin_amdgcn_s_memrealtime();
         const SegCount prefix = block_lookback(a, bid, btot, wl);
         if (wl == 0) L.prefix = prefix;
-        if constexpr (PRE && !COMPACT)   // eager unmask: the helpers stop (second phase)
-            if (a.eager && wl == 0) __hip_atomic_store(&sh_looked, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    } else if constexpr (PRE && !COMPACT) {
-        // ... and while it waits on its predecessors in the look-back, the other waves go on helping
-        if (a.eager) eager_help(a, &sh_looked);
     }
     __syncthreads();
     if (a.dbg && lane == 0) t2 = __builtin_amdgcn_s_memrealtime();

@@ -121,17 +121,7 @@ struct WalkArgs {
     uint4* hdr_cache;            // tiled walk: per segment, the 16 bytes at its first frame (null: off)
     uint32_t* stride_hint;       // quad pre-pass: the stride the last decode ended with (first speculation)
     uint32_t hdr_nt;             // non-temporal header loads (hdr_load): COMPACT batches (and WSC_WALK_HDR_NT)
-    // Eager unmask (mode 65, in place, whole chip): while the walking wave of a block counts, its
-    // three other waves unmask the interiors of large BIN payloads the walkers have found (chunks of
-    // EAGER_WIN windows, pushed to a chip-wide queue); k_unmask skips the windows they did
-    uint32_t eager;              // 1: push and help (host: in-place mode-65 decodes on all CUs)
-    uint32_t seq;                // this decode's tag (entries, done windows); never 0
-    uint32_t eager_cap;          // queue entries
-    uint32_t* eager_q;           // [0] entries pushed, [1] entries claimed (re-armed by k_unmask)
-    uint64_t* eager_ent;         // per entry: (seq << 32 | first window), (seq << 32 | key)
-    uint32_t* win_done;          // per unmask window: == seq once a helper has unmasked it
 };
-constexpr uint32_t EAGER_WIN = 4;   // windows (4 KiB each) per eager queue entry
 
 // k_u8_check runs AFTER the unmask: the unmask has already folded every text window that lies
 // inside an item (win_map), so the check reads only the items' partial windows at their ends --
@@ -172,9 +162,6 @@ struct U8Win {
     uint32_t* rearm;             // the next decode's item counter (zeroed by the unmask: always launched)
     uint32_t xcd_run;            // blocks per XCD run: consecutive logical blocks (windows) on one XCD
                                  // (0 / 1: the hardware's round-robin deal), see unmask_all
-    const uint32_t* done;        // eager decodes: per window, == seq when the walk's helpers unmasked it
-    uint32_t seq;
-    uint32_t* eager_q;           // the walk's eager queue counters, re-armed here (null: none)
 };
 
 

@@ -561,7 +561,6 @@ __device__ __forceinline__ void unmask_all(uint8_t* __restrict__ dst, const uint
     for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n_walk_blocks + 2; t += gridDim.x * blockDim.x)
         lb_state[t] = 0;
     if (blockIdx.x == 0 && threadIdx.x == 0 && u8w.rearm) *u8w.rearm = 0;
-    if (blockIdx.x == 0 && threadIdx.x < 2 && u8w.eager_q) u8w.eager_q[threadIdx.x] = 0;   // the walk's eager queue
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t waves_per_block = blockDim.x >> 6;
     // XCD runs of 4R consecutive windows (xcd_run_block, wsc_dev.hpp).  Measured: R = 8 streams the
@@ -577,9 +576,6 @@ __device__ __forceinline__ void unmask_all(uint8_t* __restrict__ dst, const uint
 
     for (uint64_t win = gw; win < n_win; win += nw) {
         const uint64_t wbase = win * WB;
-        // eager decodes: a window the walk's helper waves already unmasked (WB = 4 KiB windows: the
-        // walk's) -- never a partial one, which no payload interior holds whole
-        if (u8w.done && u8w.done[win] == u8w.seq) continue;
         if (wbase + WB > total) {   // the last, partial window
             const uint32_t r = tile_first[win];
             unmask_window_general<COMPACT, P, NT>(dst, src, src_bytes, total, spans, n_spans, r, wbase, lofs);

@@ -725,15 +725,13 @@ def test_sharded_decode_equals_unsharded(codec, world):
 
 
 @pytest.mark.parametrize("inline_max", [256, 0])
-def test_eager_unmask_during_walk(codec_lib, monkeypatch, inline_max):
-    """The eager unmask (an in-place, one-stream decode whose walk is mode 65 with >= 128 blocks):
-    while each block's walking wave counts and looks back, its other waves unmask the interiors of
-    large plain BIN payloads the walkers found (quad pre-pass and serial walk alike), and k_unmask
-    skips those windows.  9,000 connections: fuzz streams (text, errors, control frames), runs of
-    equal BIN frames, and one in 25 carrying payloads of 17 KiB .. 1 MiB -- whole, cut at the
-    segment's end (a streamed piece: never pushed), as a fragment (FIN=0: never pushed) or as TEXT
-    (deferred UTF-8: never pushed).  Every segment equals the oracle, record for record and byte
-    for byte; the wire outside payloads is untouched."""
+def test_mode65_many_blocks_large_payloads(codec_lib, monkeypatch, inline_max):
+    """The configs[2] geometry (mode 65: one walking wave and the quad pre-pass per block, >= 128
+    blocks over the whole chip) on 9,000 connections: fuzz streams (text, errors, control frames),
+    runs of equal BIN frames, and one in 25 carrying payloads of 17 KiB .. 1 MiB -- whole, cut at
+    the segment's end (a streamed piece), as a fragment (FIN=0) or as TEXT (deferred UTF-8).  Every
+    segment equals the oracle, record for record and byte for byte.  (It was written for the
+    round-6 eager-unmask experiment, DESIGN.md "Round 6", whose helper waves took those payloads.)"""
     monkeypatch.setitem(K.CFG_DEFAULTS, "u8_inline_max", inline_max)
     rng = np.random.default_rng(2606)
     streams = []
