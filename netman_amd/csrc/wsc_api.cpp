@@ -84,8 +84,7 @@ struct wsc_ctx {
     uint32_t* sticky = nullptr;      // error bits of every decode/encode (wsc_error_flags), never re-armed
     uint32_t* lb_state = nullptr;    // [0] ticket, [1] spin-timeout flag, [2] UTF-8 item count, [3..] per-block flags
     uint32_t* u8info = nullptr;      // per segment {utf8-failing frame ordinal, DFA state}
-    uint64_t* lb_agg = nullptr;
-    uint64_t* lb_incl = nullptr;
+    uint64_t* lb_rec = nullptr;      // per walk block: its look-back record (8 words)
     uint64_t* dbg = nullptr;         // WSC_WALK_DEBUG_STAMPS: per-block walk timestamps
     Span* spans = nullptr;
     uint32_t* tile = nullptr;
@@ -127,8 +126,7 @@ struct wsc_ctx {
     wsc_summary* d_summary = nullptr;
     // encode scratch: look-back state [ticket, timeout, flags...], aggregates, window index
     uint32_t* enc_lb_state = nullptr;
-    uint64_t* enc_lb_agg = nullptr;
-    uint64_t* enc_lb_incl = nullptr;
+    uint64_t* enc_lb_rec = nullptr;   // per scan block: its look-back word
     uint32_t enc_blocks = 0;
     uint32_t* enc_tile = nullptr;
     uint64_t enc_cap = 0;             // largest out_cap: max_batch_bytes + 16 * max_frames
@@ -304,12 +302,12 @@ int wsc_create(int device, const wsc_config* cfg_in, wsc_ctx** out) {
     c->max_walk_blocks = (uint32_t)max_blocks;
     chk(hipMalloc(&c->lb_state, (max_blocks + 3) * sizeof(uint32_t)), "hipMalloc lb_state");
     chk(hipMalloc(&c->u8info, (uint64_t)cfg.max_segs * 2 * sizeof(uint32_t)), "hipMalloc u8info");
-    chk(hipMalloc(&c->lb_agg, max_blocks * 4 * sizeof(uint64_t)), "hipMalloc lb_agg");
-    chk(hipMalloc(&c->lb_incl, max_blocks * 4 * sizeof(uint64_t)), "hipMalloc lb_incl");
+    chk(hipMalloc(&c->lb_rec, max_blocks * 8 * sizeof(uint64_t)), "hipMalloc lb_rec");
     if (cfg.walk_flags & WSC_WALK_DEBUG_STAMPS)
         chk(hipMalloc(&c->dbg, max_blocks * 8 * sizeof(uint64_t)), "hipMalloc dbg");
     if (rc == WSC_OK) {
         chk(hipMemsetAsync(c->lb_state, 0, (max_blocks + 3) * sizeof(uint32_t), c->stream), "hipMemset lb_state");
+        chk(hipMemsetAsync(c->lb_rec, 0, max_blocks * 8 * sizeof(uint64_t), c->stream), "hipMemset lb_rec");
         chk(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
     }
     chk(hipMalloc(&c->spans, (uint64_t)cfg.max_frames * sizeof(Span)), "hipMalloc spans");
@@ -339,11 +337,11 @@ int wsc_create(int device, const wsc_config* cfg_in, wsc_ctx** out) {
     c->enc_cap = cfg.max_batch_bytes + 16ull * cfg.max_frames;
     c->enc_tile_entries = c->enc_cap / ENC_WIN + 2;
     chk(hipMalloc(&c->enc_lb_state, (c->enc_blocks + 2) * sizeof(uint32_t)), "hipMalloc enc_lb_state");
-    chk(hipMalloc(&c->enc_lb_agg, c->enc_blocks * sizeof(uint64_t)), "hipMalloc enc_lb_agg");
-    chk(hipMalloc(&c->enc_lb_incl, c->enc_blocks * sizeof(uint64_t)), "hipMalloc enc_lb_incl");
+    chk(hipMalloc(&c->enc_lb_rec, (c->enc_blocks + 2) * sizeof(uint64_t)), "hipMalloc enc_lb_rec");
     chk(hipMalloc(&c->enc_tile, c->enc_tile_entries * sizeof(uint32_t)), "hipMalloc enc_tile");
     if (rc == WSC_OK) {
         chk(hipMemsetAsync(c->enc_lb_state, 0, (c->enc_blocks + 2) * sizeof(uint32_t), c->stream), "hipMemset enc_lb_state");
+        chk(hipMemsetAsync(c->enc_lb_rec, 0, (c->enc_blocks + 2) * sizeof(uint64_t), c->stream), "hipMemset enc_lb_rec");
         chk(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
     }
     if (rc != WSC_OK) {
@@ -359,9 +357,9 @@ int wsc_destroy(wsc_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     (void)fin_wait(c);
-    void* ptrs[] = {c->fin_ctr, c->dbg, c->sticky, c->hdr_cache, c->stride_hint, c->lb_state, c->u8info, c->lb_agg, c->lb_incl, c->spans, c->tile, c->d_wire, c->d_arena,
+    void* ptrs[] = {c->fin_ctr, c->dbg, c->sticky, c->hdr_cache, c->stride_hint, c->lb_state, c->u8info, c->lb_rec, c->spans, c->tile, c->d_wire, c->d_arena,
                     c->d_seg_off, c->d_state_in, c->d_state_out, c->d_seg_out, c->d_frames,
-                    c->d_frame_dst, c->d_summary, c->enc_lb_state, c->enc_lb_agg, c->enc_lb_incl, c->enc_tile,
+                    c->d_frame_dst, c->d_summary, c->enc_lb_state, c->enc_lb_rec, c->enc_tile,
                     c->d_enc_msgs, c->d_enc_src, c->d_enc_out, c->d_enc_off, c->u8items, c->u8maps, c->u8seg,
                     c->win_flag, c->win_map, c->u8ctr};
     for (void* p : ptrs)
@@ -459,10 +457,8 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     wa.state_in = b->state_in;
     wa.max_frame_len = c->cfg.max_frame_len;
     wa.lb_ticket = c->lb_state;
-    wa.lb_flag = c->lb_state + 3;
     wa.u8info = c->u8info;
-    wa.lb_agg = c->lb_agg;
-    wa.lb_incl = c->lb_incl;
+    wa.lb_rec = c->lb_rec;
     wa.lb_err = c->lb_state + 1;
     wa.dbg = c->dbg;
     wa.frames = b->frames;
@@ -525,6 +521,7 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     if (stale) {   // ... and its look-back ticket / flags were not re-armed either
         HIP_TRY(hipMemsetAsync(c->u8ctr + 32 * par, 0, sizeof(uint32_t), ws));
         HIP_TRY(hipMemsetAsync(c->lb_state, 0, (c->max_walk_blocks + 3) * sizeof(uint32_t), ws));
+        HIP_TRY(hipMemsetAsync(c->lb_rec, 0, (uint64_t)c->max_walk_blocks * 8 * sizeof(uint64_t), ws));
     }
     // fused: 16 frame records per lane in LDS (segments with more frames re-walk their headers)
     if (mode == 3) {
@@ -590,6 +587,7 @@ static int launch(wsc_ctx* c, const wsc_batch* b, hipStream_t st, hipEvent_t* ev
     U8Win uw{};
     uw.rearm = c->u8ctr + 32 * (c->u8par ^ 1u);
     uw.xcd_run = c->xcd_run;
+    uw.lb_rec = c->lb_rec;
     if (need_u8) {
         uw.flag = c->win_flag;
         uw.map = c->win_map;
@@ -826,9 +824,7 @@ static int launch_encode(wsc_ctx* c, const wsc_out_msg* msgs, uint32_t n, const 
     ea.tile_entries = c->enc_tile_entries;
     ea.lb_ticket = c->enc_lb_state;
     ea.lb_err = c->enc_lb_state + 1;
-    ea.lb_flag = c->enc_lb_state + 2;
-    ea.lb_agg = c->enc_lb_agg;
-    ea.lb_incl = c->enc_lb_incl;
+    ea.lb_rec = c->enc_lb_rec;
     ea.sticky = c->sticky;
     const uint32_t ipt = enc_scan_ipt(n);
     const uint32_t sblocks = (n + 256 * ipt - 1) / (256 * ipt);
@@ -847,6 +843,7 @@ static int launch_encode(wsc_ctx* c, const wsc_out_msg* msgs, uint32_t n, const 
     ca.tile = c->enc_tile;
     ca.tile_entries = c->enc_tile_entries;
     ca.lb_state = c->enc_lb_state;
+    ca.lb_rec = c->enc_lb_rec;
     ca.n_lb = sblocks + 2;
     ca.xcd_run = c->enc_xcd_run;
     uint64_t wins = (out_cap + ENC_WIN - 1) / ENC_WIN;   // the grid covers out_cap; waves past the total exit

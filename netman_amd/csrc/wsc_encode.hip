@@ -68,9 +68,8 @@ __device__ __forceinline__ void piece_mask(uint32_t bl, uint32_t bh, uint32_t (&
 }
 
 // ---------------------------------------------------------------------------------------------
-// Scan: frame sizes -> out_off (exclusive), window index.  Same look-back protocol as the
-// decoder's walk (wsc_kernels.hip): ticket block ids, agent-scope payload stores drained with
-// vmcnt(0) before the agent-scope flag store, readers poll with agent-scope atomics, bounded spin.
+// Scan: frame sizes -> out_off (exclusive), window index.  Decoupled look-back as in the decoder's
+// walk (wsc_kernels.hip): ticket block ids, self-tagged records (below), bounded spin.
 // IPT consecutive messages per thread: 1 M messages in 256 blocks instead of 4,096 -- the scan
 // went 68 -> 24 us at IPT 16 (8 per thread: 28 us, 32: 30 us).  The host picks the smallest IPT
 // that keeps the grid within 256 blocks (wsc_api.cpp enc_scan_ipt): with few, large messages the
@@ -116,17 +115,22 @@ __global__ __launch_bounds__(256) void k_encode_scan(EncArgs a) {
         btot += sh_wave[q];
     }
     if (wave == 0) {
-        if (lane == 0) {
-            __hip_atomic_store(bid == 0 ? a.lb_incl : a.lb_agg + bid, btot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __hip_atomic_store(a.lb_flag + bid, bid == 0 ? 2u : 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        // look-back records: one self-tagged word per block, kind (bits 62-63: 1 aggregate, 2
+        // inclusive prefix, 0 not yet -- k_encode_copy re-arms them) over the 62-bit value, one
+        // 8-byte agent-scope (sc1) store; a reader's one sc1 load gets status and value together
+        // (the decoder's walk does the same with 8-word records, wsc_kernels.hip lb_publish)
+        constexpr uint64_t VAL = (1ull << 62) - 1;
+        if (lane == 0)
+            __hip_atomic_store(a.lb_rec + bid, (bid == 0 ? 2ull : 1ull) << 62 | (btot & VAL), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
         uint64_t prefix = 0;
         int64_t j0 = (int64_t)bid - 1;
         uint32_t spins = 0;
         while (j0 >= 0) {
             const int64_t j = j0 - (int64_t)lane;
-            const uint32_t f = j >= 0 ? __hip_atomic_fetch_add(a.lb_flag + j, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 2u;
+            const uint64_t r = j >= 0 ? __hip_atomic_load(a.lb_rec + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                      : 2ull << 62;   // before block 0: an inclusive prefix of zero
+            const uint32_t f = (uint32_t)(r >> 62);
             const uint64_t m2 = __ballot(f == 2);
             const uint64_t m0 = __ballot(f == 0);
             const uint32_t first2 = m2 ? (uint32_t)__builtin_ctzll(m2) : 64u;
@@ -139,10 +143,7 @@ __global__ __launch_bounds__(256) void k_encode_scan(EncArgs a) {
                 __builtin_amdgcn_s_sleep(1);
                 continue;
             }
-            uint64_t v = 0;
-            if (lane <= first2 && j >= 0)
-                v = __hip_atomic_fetch_add((lane == first2 ? a.lb_incl : a.lb_agg) + j, 0ull, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
+            uint64_t v = lane <= first2 ? (r & VAL) : 0ull;
 #pragma unroll
             for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
             prefix += v;
@@ -150,11 +151,9 @@ __global__ __launch_bounds__(256) void k_encode_scan(EncArgs a) {
             j0 -= 64;
         }
         if (lane == 0) {
-            if (bid != 0) {
-                __hip_atomic_store(a.lb_incl + bid, prefix + btot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __hip_atomic_store(a.lb_flag + bid, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
+            if (bid != 0)
+                __hip_atomic_store(a.lb_rec + bid, 2ull << 62 | ((prefix + btot) & VAL), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
             sh_prefix = prefix;
         }
     }
@@ -436,7 +435,10 @@ __global__ __launch_bounds__(256) void k_encode_copy(EncCopyArgs a) {
     enc_pm_init(pm);
     __syncthreads();
     // re-arm the scan's look-back state for the next encode (this launch is ordered after it)
-    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < a.n_lb; t += gridDim.x * blockDim.x) a.lb_state[t] = 0;
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < a.n_lb; t += gridDim.x * blockDim.x) {
+        a.lb_state[t] = 0;
+        a.lb_rec[t] = 0;   // (n_lb = scan blocks + 2 >= the records written)
+    }
     const uint32_t n = a.n_msgs;
     if (n == 0) return;
     const uint32_t lane = threadIdx.x & 63;

@@ -933,23 +933,46 @@ __device__ __forceinline__ SegCount sc_shfl_up(const SegCount& v, int d) {
     return o;
 }
 
-__device__ __forceinline__ void lb_store(uint64_t* p, const SegCount& v) {
-    const uint64_t w0 = (uint64_t)v.frames | ((uint64_t)v.spans0 << 32);
-    const uint64_t w1 = (uint64_t)v.spans1 | ((uint64_t)v.flags << 32);
-    __hip_atomic_store(p + 0, w0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(p + 1, w1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(p + 2, v.bytes0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(p + 3, v.bytes1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// Look-back record of a block: 8 words, each (kind << 32 | one 32-bit field of its SegCount), kind
+// 1 = the block's aggregate, 2 = its inclusive prefix, 0 = nothing yet (k_unmask re-arms them).
+// Every word is one 8-byte agent-scope (sc1, write-through) store by its own lane and tells by
+// itself what it holds, so a reader needs no flag: ONE round of eight 8-byte sc1 loads per
+// predecessor gets both the status and the value, and a record read half-way through its
+// rewrite (aggregate words mixed with inclusive ones, or not all written) reads as not ready
+// (MI355X_MICROARCH.md: self-describing granules need no ordering).  Round 5 polled a flag and
+// then read the payload with atomic RMWs: two dependent round trips per look-back round.
+__device__ __forceinline__ uint32_t sc_word(const SegCount& v, uint32_t k) {
+    switch (k) {
+    case 0: return v.frames;
+    case 1: return v.spans0;
+    case 2: return v.spans1;
+    case 3: return v.flags;
+    case 4: return (uint32_t)v.bytes0;
+    case 5: return (uint32_t)(v.bytes0 >> 32);
+    case 6: return (uint32_t)v.bytes1;
+    default: return (uint32_t)(v.bytes1 >> 32);
+    }
 }
-__device__ __forceinline__ SegCount lb_load(uint64_t* p) {
-    const uint64_t w0 = __hip_atomic_fetch_add(p + 0, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint64_t w1 = __hip_atomic_fetch_add(p + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    SegCount v;
-    v.frames = (uint32_t)w0; v.spans0 = (uint32_t)(w0 >> 32);
-    v.spans1 = (uint32_t)w1; v.flags = (uint32_t)(w1 >> 32);
-    v.bytes0 = __hip_atomic_fetch_add(p + 2, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    v.bytes1 = __hip_atomic_fetch_add(p + 3, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return v;
+// lanes 0..7 of the wave each store one word
+__device__ __forceinline__ void lb_publish(uint64_t* rec, const SegCount& v, uint32_t kind, uint32_t wl) {
+    if (wl < 8) __hip_atomic_store(rec + wl, (uint64_t)kind << 32 | sc_word(v, wl), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// one lane reads a whole record: its kind (0 = not ready) and value
+__device__ __forceinline__ uint32_t lb_read(const uint64_t* rec, SegCount& v) {
+    uint64_t w[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) w[k] = __hip_atomic_load(rec + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t kind = (uint32_t)(w[0] >> 32);
+    bool same = true;
+#pragma unroll
+    for (int k = 1; k < 8; ++k) same = same && (uint32_t)(w[k] >> 32) == kind;
+    v.frames = (uint32_t)w[0];
+    v.spans0 = (uint32_t)w[1];
+    v.spans1 = (uint32_t)w[2];
+    v.flags = (uint32_t)w[3];
+    v.bytes0 = (uint64_t)(uint32_t)w[4] | (uint64_t)(uint32_t)w[5] << 32;
+    v.bytes1 = (uint64_t)(uint32_t)w[6] | (uint64_t)(uint32_t)w[7] << 32;
+    return same ? kind : 0u;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1241,27 +1264,18 @@ __device__ __forceinline__ SegCount tile_scan(const SegCount& tot, LDS& L, uint3
 }
 
 // Decoupled look-back by one wave (64 predecessors examined per round): publishes block bid's
-// total, returns the sum of every earlier block's total.  Look-back hand-off (MI355X_MICROARCH.md
-// "Valid forms", row 1): one lane stores the aggregate / inclusive prefix with agent-scope (sc1,
-// write-through) stores, drains them with s_waitcnt vmcnt(0), then publishes the flag with an
-// agent-scope atomic; readers poll the flag and read the payload with agent-scope atomic RMWs.
+// total, returns the sum of every earlier block's total.  Records: lb_publish / lb_read above.
 __device__ __forceinline__ SegCount block_lookback(const WalkArgs& a, uint32_t bid, const SegCount& btot, uint32_t wl) {
     const SegCount zero = {};
-    uint32_t* flag = a.lb_flag;
-    uint64_t* agg = a.lb_agg;      // [block][4]
-    uint64_t* incl = a.lb_incl;    // [block][4]
-    if (wl == 0) {
-        lb_store(bid == 0 ? incl : agg + 4ull * bid, btot);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(flag + bid, bid == 0 ? 2u : 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    uint64_t* rec = a.lb_rec;      // [block][8]
+    lb_publish(rec + 8ull * bid, btot, bid == 0 ? 2u : 1u, wl);
     SegCount prefix = zero;
     int64_t j0 = (int64_t)bid - 1;
     uint32_t spins = 0;
     while (j0 >= 0) {
         const int64_t j = j0 - (int64_t)wl;
-        const uint32_t f = j >= 0 ? __hip_atomic_fetch_add(flag + j, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                  : 2u;   // before block 0: an inclusive prefix of zero
+        SegCount v = zero;
+        const uint32_t f = j >= 0 ? lb_read(rec + 8ull * j, v) : 2u;   // before block 0: an inclusive prefix of zero
         const uint64_t m2 = __ballot(f == 2);
         const uint64_t m0 = __ballot(f == 0);
         const uint32_t first2 = m2 ? (uint32_t)__builtin_ctzll(m2) : 64u;
@@ -1274,8 +1288,7 @@ __device__ __forceinline__ SegCount block_lookback(const WalkArgs& a, uint32_t b
             __builtin_amdgcn_s_sleep(1);
             continue;
         }
-        SegCount v = zero;
-        if (wl <= first2 && j >= 0) v = lb_load((wl == first2 ? incl : agg) + 4ull * j);
+        if (!(wl <= first2 && j >= 0)) v = zero;   // lanes past the first inclusive prefix
 #pragma unroll
         for (int d = 32; d >= 1; d >>= 1) {
             SegCount o;
@@ -1291,11 +1304,7 @@ __device__ __forceinline__ SegCount block_lookback(const WalkArgs& a, uint32_t b
         if (first2 < 64) break;
         j0 -= 64;
     }
-    if (wl == 0 && bid != 0) {
-        lb_store(incl + 4ull * bid, sc_add(prefix, btot));
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(flag + bid, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (bid != 0) lb_publish(rec + 8ull * bid, sc_add(prefix, btot), 2u, wl);
     return prefix;
 }
 
@@ -1569,9 +1578,8 @@ __global__ __launch_bounds__(NT) void k_walk_fused(WalkArgs a) {
 struct SimpleSeg {
     uint32_t plen, mask, hl;
 };
-__device__ __forceinline__ bool simple_seg(const WalkArgs& a, const SegIn& x, SimpleSeg& o) {
-    if (x.st.status != WSC_SEG_OPEN || x.st.cont_len != 0 || x.st.frame_rem != 0) return false;
-    const uint4 hd = x.hdr;
+__device__ __forceinline__ bool simple_hdr(const WalkArgs& a, uint64_t start, uint64_t end, const uint4& hd,
+                                           SimpleSeg& o) {
     const uint32_t b0 = hd.x & 0xFFu, b1 = (hd.x >> 8) & 0xFFu;
     if (b0 != 0x82u || !(b1 & 0x80u)) return false;
     const uint32_t len7 = b1 & 0x7Fu;
@@ -1593,7 +1601,13 @@ __device__ __forceinline__ bool simple_seg(const WalkArgs& a, const SegIn& x, Si
     }
     if (plen == 0 || plen > 0xFFFFFFFFull || plen > a.max_frame_len) return false;
     o.plen = (uint32_t)plen;
-    return x.end - x.start == (uint64_t)o.hl + plen;
+    return end - start == (uint64_t)o.hl + plen;
+}
+__device__ __forceinline__ bool simple_state(uint32_t status, uint64_t cont_len, uint64_t frame_rem) {
+    return status == WSC_SEG_OPEN && cont_len == 0 && frame_rem == 0;
+}
+__device__ __forceinline__ bool simple_seg(const WalkArgs& a, const SegIn& x, SimpleSeg& o) {
+    return simple_state(x.st.status, x.st.cont_len, x.st.frame_rem) && simple_hdr(a, x.start, x.end, x.hdr, o);
 }
 
 // The outputs walk_segment<EMIT> writes for a simple segment s (frame fi, span si): its record, span,
@@ -1679,6 +1693,9 @@ __global__ __launch_bounds__(NT) void k_walk_tiled(WalkArgs a, uint32_t per_bloc
         x.hdr = x.end - x.start >= 2 ? hdr_load(a.wire, a.n_bytes, x.start, a.hdr_nt) : make_uint4(0, 0, 0, 0);
     };
     // ---- phase 1: the block's total ----
+    // (four tiles per step, every lane's inputs for all four in flight together, measured the same:
+    // 34.5-37.3 vs 35.6-39.2 us of count at 1 M one-frame segments -- the header lines, one per
+    // segment, are what this phase streams; profiles/r06/stamps_*.log)
     SegCount tot = zero;
     {
         SegIn x0, x1, x2;

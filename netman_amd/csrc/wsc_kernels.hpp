@@ -102,9 +102,7 @@ struct WalkArgs {
     wsc_seg_result* seg_out;
     wsc_summary* summary;
     uint32_t* lb_ticket;         // look-back: dynamic block id counter
-    uint32_t* lb_flag;           // per block: 0 none, 1 aggregate, 2 inclusive prefix
-    uint64_t* lb_agg;            // per block: SegCount as 4 x u64
-    uint64_t* lb_incl;
+    uint64_t* lb_rec;            // per block: its look-back record, 8 self-tagged words (block_lookback)
     uint32_t* lb_err;            // bounded-spin timeout
     uint64_t* dbg;               // optional per-block timestamps (WSC_WALK_DEBUG_STAMPS)
     uint32_t* u8info;            // per segment: {first utf8-failing frame ordinal, DFA state}
@@ -162,6 +160,7 @@ struct U8Win {
     uint32_t* rearm;             // the next decode's item counter (zeroed by the unmask: always launched)
     uint32_t xcd_run;            // blocks per XCD run: consecutive logical blocks (windows) on one XCD
                                  // (0 / 1: the hardware's round-robin deal), see unmask_all
+    uint64_t* lb_rec;            // the walk's look-back records, re-armed (zeroed) by this launch
 };
 
 
@@ -177,9 +176,7 @@ struct EncArgs {
     uint32_t* tile;              // per output window: the frame its first byte belongs to
     uint64_t tile_entries;
     uint32_t* lb_ticket;
-    uint32_t* lb_flag;
-    uint64_t* lb_agg;
-    uint64_t* lb_incl;
+    uint64_t* lb_rec;            // per scan block: its self-tagged look-back word
     uint32_t* lb_err;
     uint32_t* sticky;            // context error bits (bit2: encode look-back timeout)
 };
@@ -195,6 +192,7 @@ struct EncCopyArgs {
     const uint32_t* tile;
     uint64_t tile_entries;
     uint32_t* lb_state;          // the scan's look-back state, re-armed by this launch
+    uint64_t* lb_rec;            // ... and its records
     uint32_t n_lb;
     uint32_t xcd_run;            // blocks per XCD run (xcd_run_block)
 };

@@ -560,6 +560,9 @@ __device__ __forceinline__ void unmask_all(uint8_t* __restrict__ dst, const uint
     // this launch, and re-armed by the next decode's unmask)
     for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n_walk_blocks + 2; t += gridDim.x * blockDim.x)
         lb_state[t] = 0;
+    if (u8w.lb_rec)   // ... and its look-back records (8 words per block)
+        for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < 8 * n_walk_blocks; t += gridDim.x * blockDim.x)
+            u8w.lb_rec[t] = 0;
     if (blockIdx.x == 0 && threadIdx.x == 0 && u8w.rearm) *u8w.rearm = 0;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t waves_per_block = blockDim.x >> 6;
@@ -653,7 +656,7 @@ __global__ __launch_bounds__(256, (P == 4 ? WSC_UNMASK_WPE : 2) * MINW) void k_u
     if (fin_host == nullptr) return;
     __syncthreads();
     if (threadIdx.x == 0) {
-        if (blockIdx.x * blockDim.x < n_walk_blocks + 2) __threadfence();   // lb_state re-arm visible first
+        if (blockIdx.x * blockDim.x < 8 * n_walk_blocks + 2) __threadfence();   // lb_state re-arm visible first
         fin_signal(fin_ctr, fin_host, fin_seq);
     }
 }

@@ -32,6 +32,12 @@ def test_cpu_echo_roundtrip(cpu_echo, args):
     rc, d = _run(cpu_echo, *args)
     assert rc == 0 and d["ok"], d
     assert d["messages"] == int(args[1]) * int(args[3])
+    # what the server costs its host (round-5 VERDICT #3): poller threads, the whole process minus
+    # the client threads, and per GiB echoed
+    assert d["poller_cpu_s"] > 0 and d["server_cpu_s"] > 0 and d["client_cpu_s"] > 0, d
+    assert d["server_cpu_s"] >= 0.5 * d["poller_cpu_s"], d
+    gib = d["messages"] * int(args[5]) / 2**30
+    assert abs(d["server_cpu_s_per_gib"] * gib - d["server_cpu_s"]) <= 1e-4 + 0.01 * d["server_cpu_s"], d   # (%.4f)
 
 
 def test_poller_device_mapping():
@@ -80,6 +86,7 @@ def test_gpu_echo_roundtrip(codec_lib, args):
     assert rc == 0 and d["ok"], d
     assert d["messages"] == int(args[1]) * int(args[3])
     assert d["pollers"] == (int(args[args.index("--pollers") + 1]) if "--pollers" in args else 1)
+    assert d["server_cpu_s"] > 0 and d["server_cpu_s_per_gib"] > 0, d
 
 
 @pytest.mark.gpu
