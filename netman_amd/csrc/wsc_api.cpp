@@ -23,7 +23,6 @@ __global__ void k_unmask(uint8_t*, const uint8_t*, uint64_t, uint64_t, const Spa
                          const wsc_summary*, uint32_t*, uint32_t, uint32_t*, uint32_t*, uint32_t, U8Win);
 template <uint32_t IPT> __global__ void k_encode_scan(EncArgs);
 __global__ void k_kcopy(uint8_t*, const uint8_t*, uint64_t);
-template <int NT> __global__ void k_encode_small(EncCopyArgs);
 template <int NT> __global__ void k_encode_copy(EncCopyArgs);
 }  // namespace wsc
 
@@ -130,7 +129,6 @@ struct wsc_ctx {
     uint64_t* enc_lb_rec = nullptr;   // per scan block: its look-back word
     uint32_t enc_blocks = 0;
     uint32_t* enc_tile = nullptr;
-    uint8_t* enc_big = nullptr;       // per output window: a message above ENC_SMALL touches it
     uint64_t enc_cap = 0;             // largest out_cap: max_batch_bytes + 16 * max_frames
     uint64_t enc_tile_entries = 0;
     // host-staged encode buffers (lazily allocated)
@@ -341,11 +339,9 @@ int wsc_create(int device, const wsc_config* cfg_in, wsc_ctx** out) {
     chk(hipMalloc(&c->enc_lb_state, (c->enc_blocks + 2) * sizeof(uint32_t)), "hipMalloc enc_lb_state");
     chk(hipMalloc(&c->enc_lb_rec, (c->enc_blocks + 2) * sizeof(uint64_t)), "hipMalloc enc_lb_rec");
     chk(hipMalloc(&c->enc_tile, c->enc_tile_entries * sizeof(uint32_t)), "hipMalloc enc_tile");
-    chk(hipMalloc(&c->enc_big, c->enc_tile_entries), "hipMalloc enc_big");
     if (rc == WSC_OK) {
         chk(hipMemsetAsync(c->enc_lb_state, 0, (c->enc_blocks + 2) * sizeof(uint32_t), c->stream), "hipMemset enc_lb_state");
         chk(hipMemsetAsync(c->enc_lb_rec, 0, (c->enc_blocks + 2) * sizeof(uint64_t), c->stream), "hipMemset enc_lb_rec");
-        chk(hipMemsetAsync(c->enc_big, 0, c->enc_tile_entries, c->stream), "hipMemset enc_big");
         chk(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
     }
     if (rc != WSC_OK) {
@@ -363,7 +359,7 @@ int wsc_destroy(wsc_ctx* c) {
     (void)fin_wait(c);
     void* ptrs[] = {c->fin_ctr, c->dbg, c->sticky, c->hdr_cache, c->stride_hint, c->lb_state, c->u8info, c->lb_rec, c->spans, c->tile, c->d_wire, c->d_arena,
                     c->d_seg_off, c->d_state_in, c->d_state_out, c->d_seg_out, c->d_frames,
-                    c->d_frame_dst, c->d_summary, c->enc_lb_state, c->enc_lb_rec, c->enc_tile, c->enc_big,
+                    c->d_frame_dst, c->d_summary, c->enc_lb_state, c->enc_lb_rec, c->enc_tile,
                     c->d_enc_msgs, c->d_enc_src, c->d_enc_out, c->d_enc_off, c->u8items, c->u8maps, c->u8seg,
                     c->win_flag, c->win_map, c->u8ctr};
     for (void* p : ptrs)
@@ -830,7 +826,6 @@ static int launch_encode(wsc_ctx* c, const wsc_out_msg* msgs, uint32_t n, const 
     ea.lb_err = c->enc_lb_state + 1;
     ea.lb_rec = c->enc_lb_rec;
     ea.sticky = c->sticky;
-    ea.big = c->enc_big;
     const uint32_t ipt = enc_scan_ipt(n);
     const uint32_t sblocks = (n + 256 * ipt - 1) / (256 * ipt);
     if (ipt == 1) hipLaunchKernelGGL(k_encode_scan<1>, dim3(sblocks), dim3(256), 0, st, ea);
@@ -849,16 +844,13 @@ static int launch_encode(wsc_ctx* c, const wsc_out_msg* msgs, uint32_t n, const 
     ca.tile_entries = c->enc_tile_entries;
     ca.lb_state = c->enc_lb_state;
     ca.lb_rec = c->enc_lb_rec;
-    ca.big = c->enc_big;
     ca.n_lb = sblocks + 2;
     ca.xcd_run = c->enc_xcd_run;
     uint64_t wins = (out_cap + ENC_WIN - 1) / ENC_WIN;   // the grid covers out_cap; waves past the total exit
     if (wins > c->enc_tile_entries) wins = c->enc_tile_entries;
     if (wins == 0) wins = 1;
-    // messages up to ENC_SMALL: four per wave; the rest: the output windows they touch
-    hipLaunchKernelGGL(k_encode_small<3>, dim3((uint32_t)((n + 15ull) / 16)), dim3(256), 0, st, ca);
-    HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(k_encode_copy<3>, dim3((uint32_t)((wins + 3) / 4)), dim3(256), 0, st, ca);   // nt loads and stores
+    const dim3 cgrid((uint32_t)((wins + 3) / 4));
+    hipLaunchKernelGGL(k_encode_copy<3>, cgrid, dim3(256), 0, st, ca);   // nt loads and stores
     HIP_TRY(hipGetLastError());
     return WSC_OK;
 }

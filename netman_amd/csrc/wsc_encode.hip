@@ -169,13 +169,6 @@ __global__ __launch_bounds__(256) void k_encode_scan(EncArgs a) {
         uint64_t w_end = ((off + sz[j] - 1) >> ENC_WIN_SHIFT) + 1;
         if (w_end > a.tile_entries) w_end = a.tile_entries;
         for (; w < w_end; ++w) a.tile[w] = (uint32_t)i;
-        // a message above ENC_SMALL is framed by the window pass: mark every window it touches
-        // (small ones are framed message by message, k_encode_copy's first part)
-        if (sz[j] > ENC_SMALL + 4) {   // <=> len > ENC_SMALL (sz = len + 4 from len 126 to 65535)
-            uint64_t b = off >> ENC_WIN_SHIFT;
-            const uint64_t b_end = w_end;
-            for (; b < b_end; ++b) a.big[b] = 1;
-        }
         off += sz[j];
         if (i == a.n_msgs - 1) {
             uint64_t total = off;
@@ -432,178 +425,8 @@ __device__ __forceinline__ void enc_pm_init(u32x4* pm) {
     }
 }
 
-// Small messages (payload <= ENC_SMALL), four per wave: wave gw frames messages 4 gw .. 4 gw + 3.
-// Every 16-byte aligned output piece is owned by the frame holding its first byte; the pieces the
-// four frames own are numbered 0 .. C-1 in output order and lane l takes pieces l + 64 k -- 1 KiB
-// contiguous per store instruction, as in the window pass.  Pieces inside one payload are one
-// unaligned gather each; the others (a frame's header piece, its last piece, which also holds the
-// first bytes of the frames after it) are assembled from the five frames' descriptors (wave-
-// uniform, SGPRs) -- every store a full aligned 16 bytes, a byte run only at the output's end.
-// Two dependent rounds (descriptors + offsets, then payload gathers) where the window pass has
-// four (window index, its first frame, the window's frames, payload): at 1 KiB messages the
-// window pass waited on that chain 78 % of its cycles (round 5 PMC).  A window that also holds
-// bytes of a large message is framed by the window pass too, whose pieces carry these same bytes.
-struct GFrame {            // one frame, wave-uniform
-    uint64_t o, e, so, len;   // header start, frame end, payload source offset, payload length
-    uint32_t fb, hl;
-    bool ok;
-};
-__device__ __forceinline__ uint64_t readlane64(uint64_t v, int j) {
-    return (uint64_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), j) << 32 | __builtin_amdgcn_readlane((uint32_t)v, j);
-}
-// frame f's bytes inside the 16-byte piece at output offset x, ORed into acc
-__device__ __forceinline__ void frame_part(const EncCopyArgs& a, const GFrame& f, uint64_t x, const u32x4* __restrict__ pm,
-                                           uint4& acc) {
-    if (!f.ok || f.o >= x + 16 || f.e <= x) return;
-    const int64_t ho = (int64_t)f.o - (int64_t)x, po = ho + f.hl, fe = po + (int64_t)f.len;   // piece-relative
-    uint32_t msk[4];
-    int64_t lo = ho > 0 ? ho : 0, hi = po < 16 ? po : 16;
-    if (lo < hi) {   // header bytes (ho > -16 here: the header is at most 10 bytes)
-        uint32_t h[4];
-        enc_header(f.fb, f.len, h);
-        pm_mask(pm, (uint32_t)lo, (uint32_t)hi, msk);
-        const uint4 t = and4(enc_place(h, (int32_t)ho), msk);
-        acc.x |= t.x; acc.y |= t.y; acc.z |= t.z; acc.w |= t.w;
-    }
-    lo = po > 0 ? po : 0;
-    hi = fe < 16 ? fe : 16;
-    if (lo < hi) {
-        pm_mask(pm, (uint32_t)lo, (uint32_t)hi, msk);
-        const uint4 t = and4(load16_unaligned(a.src, (int64_t)f.so - po, a.src_bytes), msk);
-        acc.x |= t.x; acc.y |= t.y; acc.z |= t.z; acc.w |= t.w;
-    }
-}
-
-template <int NT>
-__device__ __forceinline__ void encode_small_group(const EncCopyArgs& a, uint64_t gw, uint64_t limit, uint32_t lane,
-                                                   const u32x4* __restrict__ pm) {
-#ifndef EXP_K
-#define EXP_K 4
-#endif
-    constexpr uint32_t K = EXP_K;   // pieces per lane per round
-    const uint64_t m0 = 4 * gw, n = a.n_msgs;
-    uint64_t lo_ = 0, ll = 0, ls = 0;
-    uint32_t lf = 0;
-    if (lane < 5 && m0 + lane < n) {   // frames m0 .. m0 + 4 (the fifth: the last piece's tail)
-        const wsc_out_msg mm = a.msgs[m0 + lane];
-        lo_ = a.out_off[m0 + lane];
-        ll = mm.len;
-        ls = mm.src_off;
-        lf = mm.first_byte;
-    }
-    // per frame j < 4 (wave-uniform): the pieces it owns -- aligned x in [o, min(e, limit)) --
-    // numbered P[j] .. P[j + 1] - 1, of which [F[j], L[j]) lie inside its payload; piece i sits
-    // at output base[j] + 16 i, its payload bytes at source sb[j] + 16 i
-    uint32_t P[5], F[4], L[4];
-    uint64_t base[4], sb[4];
-    uint32_t C = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const uint64_t o = readlane64(lo_, j), len = readlane64(ll, j), so = readlane64(ls, j);
-        const uint64_t p = o + enc_hlen(len), e = p + len;
-        P[j] = F[j] = L[j] = C;
-        base[j] = sb[j] = 0;
-        if (m0 + j < n && len <= ENC_SMALL && o < limit) {
-            const uint64_t end = e < limit ? e : limit, xf = (o + 15) & ~15ull;
-            const uint64_t xp = (p + 15) & ~15ull, xe = end & ~15ull;
-            const uint32_t c = xf < end ? (uint32_t)((end - xf + 15) >> 4) : 0u;
-            const uint32_t fa = (uint32_t)((xp - xf) >> 4), la = xe > xp ? (uint32_t)((xe - xf) >> 4) : fa;
-            F[j] = C + fa;
-            L[j] = C + la;
-            base[j] = xf - 16ull * C;
-            sb[j] = so - p + base[j];
-            C += c;
-        }
-    }
-    P[4] = C;
-    if (C == 0) return;
-    auto sel4 = [](uint32_t t, auto v0, auto v1, auto v2, auto v3) { return t == 0 ? v0 : t == 1 ? v1 : t == 2 ? v2 : v3; };
-    // ---- pieces inside a payload: K gathers issued together, then K stores ----
-    for (uint32_t i0 = lane; i0 < C; i0 += 64 * K) {
-        uint4 v[K];
-        bool fast[K];
-        uint64_t xs[K];
-#pragma unroll
-        for (uint32_t k = 0; k < K; ++k) {
-            const uint32_t i = i0 + 64 * k;
-            const uint32_t t = (uint32_t)(i >= P[1]) + (uint32_t)(i >= P[2]) + (uint32_t)(i >= P[3]);
-            fast[k] = i < C && i >= sel4(t, F[0], F[1], F[2], F[3]) && i < sel4(t, L[0], L[1], L[2], L[3]);
-            xs[k] = sel4(t, base[0], base[1], base[2], base[3]) + 16ull * i;
-            if (fast[k]) v[k] = load16_unaligned(a.src, (int64_t)(sel4(t, sb[0], sb[1], sb[2], sb[3]) + 16ull * i), a.src_bytes);
-        }
-#pragma unroll
-        for (uint32_t k = 0; k < K; ++k)
-            if (fast[k]) st16v<NT>(a.out + xs[k], u32x4{v[k].x, v[k].y, v[k].z, v[k].w});
-    }
-    // ---- the rest: per frame its header piece and its last piece (at most 8), lane 2 j + s ----
-    // assembled from frame j, frame j + 1 and, when that ends inside the piece (frames shorter
-    // than 16 B), the frames after it
-    const uint32_t j = lane < 8 ? lane >> 1 : 3u;
-    const uint32_t Pj = sel4(j, P[0], P[1], P[2], P[3]), Fj = sel4(j, F[0], F[1], F[2], F[3]);
-    const uint32_t Lj = sel4(j, L[0], L[1], L[2], L[3]), Pn = sel4(j, P[1], P[2], P[3], P[4]);
-    const uint32_t pi = (lane & 1) ? Pn - 1 : Pj;
-    const bool hdr_special = Fj > Pj;
-    bool act = lane < 8 && Pn > Pj && (pi < Fj || pi >= Lj);
-    if ((lane & 1) && pi == Pj && hdr_special) act = false;   // one piece, already lane 2 j's
-    const uint64_t x = sel4(j, base[0], base[1], base[2], base[3]) + 16ull * pi;
-    GFrame g0, g1;
-    g0.o = __shfl(lo_, (int)j);
-    g0.len = __shfl(ll, (int)j);
-    g0.so = __shfl(ls, (int)j);
-    g0.fb = __shfl(lf, (int)j);
-    g1.o = __shfl(lo_, (int)j + 1);
-    g1.len = __shfl(ll, (int)j + 1);
-    g1.so = __shfl(ls, (int)j + 1);
-    g1.fb = __shfl(lf, (int)j + 1);
-    g0.ok = true;
-    g1.ok = m0 + j + 1 < n;
-    g0.hl = enc_hlen(g0.len);
-    g1.hl = enc_hlen(g1.len);
-    g0.e = g0.o + g0.hl + g0.len;
-    g1.e = g1.o + g1.hl + g1.len;
-    if (!act) return;
-    uint4 acc = make_uint4(0, 0, 0, 0);
-    frame_part(a, g0, x, pm, acc);
-    frame_part(a, g1, x, pm, acc);
-    if (g1.ok) {
-        uint64_t oj = g1.e;
-        for (uint64_t m = m0 + j + 2; m < n && oj < x + 16; ++m) {
-            const wsc_out_msg mj = a.msgs[m];
-            GFrame g;
-            g.ok = true;
-            g.o = oj;
-            g.len = mj.len;
-            g.so = mj.src_off;
-            g.fb = mj.first_byte;
-            g.hl = enc_hlen(mj.len);
-            g.e = oj + g.hl + mj.len;
-            frame_part(a, g, x, pm, acc);
-            oj = g.e;
-        }
-    }
-    const u32x4 w = {acc.x, acc.y, acc.z, acc.w};
-    if (x + 16 <= limit) st16v<NT>(a.out + x, w);
-    else store_run<0>(a.out + x, w, 0u, (uint32_t)(limit - x));
-}
-
-// Small messages: wave gw frames messages 4 gw .. 4 gw + 3 (encode_small_group).  Its own launch,
-// before k_encode_copy: in one kernel with the window pass the two paths' registers added up
-// (82 VGPRs, 5 waves per SIMD) and the 1 KiB batch ran latency-bound at 0.58 ms.
-template <int NT>
-__global__ __launch_bounds__(256) void k_encode_small(EncCopyArgs a) {
-    __shared__ u32x4 pm[17];
-    enc_pm_init(pm);
-    __syncthreads();
-    const uint32_t n = a.n_msgs;
-    const uint64_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
-    if (n == 0 || 4 * gw >= n) return;
-    uint64_t limit = a.out_off[n];
-    if (limit > a.out_cap) limit = a.out_cap;
-    encode_small_group<NT>(a, gw, limit, threadIdx.x & 63, pm);
-}
-
 // ---------------------------------------------------------------------------------------------
-// Copy: one ENC_WIN-byte output window per wave, for the windows a large message touches.
+// Copy: one ENC_WIN-byte output window per wave.
 // ---------------------------------------------------------------------------------------------
 template <int NT>
 __global__ __launch_bounds__(256) void k_encode_copy(EncCopyArgs a) {
@@ -625,10 +448,7 @@ __global__ __launch_bounds__(256) void k_encode_copy(EncCopyArgs a) {
     if (limit > a.out_cap) limit = a.out_cap;
     const uint64_t wbase = gw << ENC_WIN_SHIFT;
     if (wbase >= limit || gw >= a.tile_entries) return;
-    const uint8_t big = a.big[gw];
     const uint32_t m = a.tile[gw];
-    if (big == 0) return;   // only small messages here: framed above
-    if (lane == 0) a.big[gw] = 0;  // (re-armed for the next encode)
     const wsc_out_msg mm = a.msgs[m];
     const uint64_t o = a.out_off[m];
     const uint64_t p0 = o + enc_hlen(mm.len), p1 = p0 + mm.len;
@@ -646,7 +466,6 @@ __global__ __launch_bounds__(256) void k_encode_copy(EncCopyArgs a) {
 template __global__ void k_encode_scan<1>(EncArgs);
 template __global__ void k_encode_scan<4>(EncArgs);
 template __global__ void k_encode_scan<16>(EncArgs);
-template __global__ void k_encode_small<3>(EncCopyArgs);
 template __global__ void k_encode_copy<3>(EncCopyArgs);
 
 }  // namespace wsc

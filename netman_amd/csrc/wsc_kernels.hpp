@@ -168,7 +168,6 @@ struct U8Win {
 constexpr uint32_t ENC_WIN_SHIFT = 12;                 // 4 KiB output windows
 constexpr uint32_t ENC_WIN = 1u << ENC_WIN_SHIFT;
 constexpr uint32_t ENC_IPT = 16;                       // encode scan: consecutive messages per thread
-constexpr uint32_t ENC_SMALL = 4000;                   // payloads up to this: framed message by message
 
 struct EncArgs {
     const wsc_out_msg* msgs;
@@ -180,7 +179,6 @@ struct EncArgs {
     uint64_t* lb_rec;            // per scan block: its self-tagged look-back word
     uint32_t* lb_err;
     uint32_t* sticky;            // context error bits (bit2: encode look-back timeout)
-    uint8_t* big;                // per output window: 1 = a message above ENC_SMALL touches it
 };
 
 struct EncCopyArgs {
@@ -195,7 +193,6 @@ struct EncCopyArgs {
     uint64_t tile_entries;
     uint32_t* lb_state;          // the scan's look-back state, re-armed by this launch
     uint64_t* lb_rec;            // ... and its records
-    uint8_t* big;                // the scan's large-message windows (re-armed by this launch)
     uint32_t n_lb;
     uint32_t xcd_run;            // blocks per XCD run (xcd_run_block)
 };

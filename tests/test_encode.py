@@ -117,11 +117,8 @@ def test_gpu_encode_edge_lengths(codec, seed):
 @pytest.mark.gpu
 @pytest.mark.parametrize("seed", range(3))
 def test_gpu_encode_small_and_large_mix(codec, seed):
-    """payloads up to ENC_SMALL (4000 B) are framed message by message, each aligned 16-byte piece
-    by the frame holding its first byte (with the frames after it); larger ones by the output
-    windows they touch (wsc_encode.hip encode_small_msgs, k_encode_copy).  Lengths either side of
-    the split, tiny frames between them, then an all-small batch in the same context (the window
-    flags the large frames set are re-armed)"""
+    """small and large frames mixed in one batch (windows holding frame edges of every kind),
+    then another batch in the same context"""
     lens = [0, 1, 9, 15, 16, 100, 1000, 1024, 3999, 4000, 4001, 4005, 4096, 9000, 70000]
     msgs, src = _batch(200 + seed, 3000, lens)
     _check(codec, msgs, src)

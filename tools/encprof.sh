@@ -1,4 +1,4 @@
-# Encode kernels alone (tools/enc_one.py), in-tree library vs an A/B build: kernel trace + SQ
+# Encode kernels alone (tools/enc_one.py), in-tree library vs an A/B build (tools/build_variant.sh): kernel trace + SQ
 # instruction / wave-cycle counters, one pass each.   bash tools/encprof.sh <lib_b.so> [1k|64k]
 set -e
 cd /tmp; export TMPDIR=/tmp; R=$GRAFT_REPO_ROOT; o=$R/gpurun_out/encprof; rm -rf $o; mkdir -p $o
