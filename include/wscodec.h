@@ -359,7 +359,7 @@ int wsc_profile(wsc_ctx* ctx, const wsc_batch* batch, int iters, double* out_ms)
 int wsc_debug_stamps(wsc_ctx* ctx, uint64_t* out, uint32_t max_blocks);
 
 /* Diagnostics: the header-walk geometry the context's last decode launched (*mode: 16, 32, 64, 65,
- * 66, 256, 257 = fused walks, 3 = tiled or three-launch; 0 before any decode) and its block count.
+ * 66, 256, 257 = fused walks, 3 = tiled; 0 before any decode) and its block count.
  * Tests use it to check that a geometry pinned with wsc_config.walk_mode really ran.            */
 int wsc_walk_info(wsc_ctx* ctx, uint32_t* mode, uint32_t* blocks);
 

@@ -141,7 +141,7 @@ struct wsc_ctx {
 extern "C" {
 
 // walk geometry (see launch): 64 = fused walk with 64-lane blocks, 256 = fused with 256-lane
-// blocks, 3 = the three-launch walk (count / scan / emit)
+// blocks, 3 = the tiled walk
 // CUs of the streams made by wsc_stream_create with a CU mask (any context of the process may
 // launch on them): the walk's geometry must fit the CUs it actually runs on -- a fused walk whose
 // blocks cannot all be resident serialises on its look-back (a 65 k-segment walk on 16 CUs ran
@@ -161,7 +161,7 @@ static uint32_t walk_mode(const wsc_ctx* c, uint32_t n_segs, uint32_t cus) {
     // a CU-masked walk stream whose CUs hold every segment in 4 resident 64-lane blocks per CU:
     // 64-lane blocks (headline pipeline, 16 CUs: 2,941 vs 2,842 GiB/s with 256-lane blocks).
     // Larger batches keep the whole-chip choice: measured, a fused walk whose blocks are not all
-    // resident still beat the three-launch walk there (configs[1] on 32 CUs: 0.435 vs 0.497 ms)
+    // resident still beat the (since removed) three-launch walk there (configs[1] on 32 CUs: 0.435 vs 0.497 ms)
     if (cus < (uint32_t)c->n_cu && n_segs <= 256u * cus) return 64;
     const uint32_t all = (uint32_t)c->n_cu;
     // up to one wave of segments per CU: one walking wave per CU, four emitting (mode 65)

@@ -1659,7 +1659,7 @@ __device__ __forceinline__ void emit_simple(const WalkArgs& a, uint32_t s, const
 //            on top of the running prefix, cooperative emit from LDS -- or, for a tile whose
 //            segments are each one complete plain BIN frame (simple_seg), each lane's outputs
 //            written straight from its cached header (emit_simple).
-// One launch and no per-segment counts in HBM (the three-launch walk wrote and re-read 32 B of
+// One launch and no per-segment counts in HBM (round 2's three-launch walk wrote and re-read 32 B of
 // counts per segment and re-walked every header in its emit pass).
 template <bool COMPACT, uint32_t KR, uint32_t NT>
 __global__ __launch_bounds__(NT) void k_walk_tiled(WalkArgs a, uint32_t per_block) {
