@@ -1,5 +1,5 @@
 """Back-to-back decodes of one device batch on one stream (one batch in flight), for kernel-trace
-gap analysis:  python tools/single_loop.py <config> [iters]
+gap analysis:  python tools/single_loop.py <config> [iters] [--lib libwscodec.so]
 config: head (16384 x 64 KiB, 4/seg) | c1 (1M x 1 KiB, 16/seg) | c2 (256k mixed, 16/seg) |
 c4 (64k fragmented messages, COMPACT) | c4i (the same batch unmasked in place) |
 t64 / t1 (TEXT 16384 x 64 KiB / 262144 x 1 KiB; wire restored before each decode, wall time includes the copy)"""
@@ -17,8 +17,13 @@ from netman_amd import synth  # noqa: E402
 
 
 def main():
-    which = sys.argv[1] if len(sys.argv) > 1 else "c1"
-    iters = int(sys.argv[2]) if len(sys.argv) > 2 else 30
+    args = sys.argv[1:]
+    if "--lib" in args:   # an A/B build (tools/build_variant.sh) instead of the in-tree library
+        i = args.index("--lib")
+        K.load_library(os.path.abspath(args[i + 1]))
+        del args[i:i + 2]
+    which = args[0] if len(args) > 0 else "c1"
+    iters = int(args[1]) if len(args) > 1 else 30
     cfg = {"head": lambda: synth.uniform_batch(16384, 65536, 4, seed=synth.SEED_BASE + 1),
            "c1": lambda: synth.uniform_batch(1 << 20, 1024, 16, seed=synth.SEED_BASE + 1),
            "c11": lambda: synth.uniform_batch(1 << 20, 1024, 1, seed=synth.SEED_BASE + 1),
