@@ -268,7 +268,12 @@ __device__ __forceinline__ bool encode_window_lanes(const EncCopyArgs& a, const 
         }
     };
     // ---- pass 1: pieces inside one payload ----
+    // all P gathers issued before the first store: one memory round trip for the window (with a
+    // load and its store in one iteration the compiler waited on each load in turn -- the branchy
+    // edge path of load16_unaligned keeps it from hoisting the next load over the store)
     uint32_t n_edge = 0;
+    uint4 v[P];
+    bool ins[P];
 #pragma unroll
     for (uint32_t k = 0; k < P; ++k) {
         const int32_t pr = (int32_t)(k * 1024 + lane * 16);
@@ -277,11 +282,8 @@ __device__ __forceinline__ bool encode_window_lanes(const EncCopyArgs& a, const 
         const int32_t fp = __shfl(rp, t & 63), fe = __shfl(re, t & 63);
         const uint32_t sl = __shfl(so_lo, t & 63), sh = __shfl(so_hi, t & 63);
         const bool inside = t < (int32_t)nl && fp <= pr && pr + 16 <= fe && pa + 16 <= limit;
-        if (inside) {
-            const int64_t sof = (int64_t)((uint64_t)sh << 32 | sl) + (int64_t)pa;
-            const uint4 v = load16_unaligned(a.src, sof, a.src_bytes);
-            enc_st<NT>(a.out, wbase, pa, u32x4{v.x, v.y, v.z, v.w});
-        }
+        ins[k] = inside;
+        if (inside) v[k] = load16_unaligned(a.src, (int64_t)((uint64_t)sh << 32 | sl) + (int64_t)pa, a.src_bytes);
         const bool edge = !inside && pa < limit;
         const uint64_t em = __ballot(edge);
         if (edge)
@@ -289,33 +291,61 @@ __device__ __forceinline__ bool encode_window_lanes(const EncCopyArgs& a, const 
                 (uint16_t)(k * 64 + lane);
         n_edge += (uint32_t)__builtin_popcountll(em);
     }
+#pragma unroll
+    for (uint32_t k = 0; k < P; ++k) {
+        const uint64_t pa = wbase + k * 1024u + lane * 16u;
+        if (ins[k]) enc_st<NT>(a.out, wbase, pa, u32x4{v[k].x, v[k].y, v[k].z, v[k].w});
+    }
     if (n_edge == 0) return true;
     __builtin_amdgcn_wave_barrier();
     // ---- pass 2: pieces holding headers / frame edges, one per lane ----
     // one frame's contribution to a piece: header bytes from registers, payload by a gather
-    auto part = [&](int32_t t, int32_t pr, uint4& acc, bool& ends_inside) {
-        const int32_t fo = __shfl(ro, t & 63), fp = __shfl(rp, t & 63), fe = __shfl(re, t & 63);
-        const uint32_t hh[4] = {__shfl(h[0], t & 63), __shfl(h[1], t & 63), __shfl(h[2], t & 63), 0u};
-        const uint32_t sl = __shfl(so_lo, t & 63), sh = __shfl(so_hi, t & 63);
-        ends_inside = false;
-        if (t >= (int32_t)nl) return;
-        uint32_t msk[4];
-        int32_t lo = fo > pr ? fo : pr, hi = fp < pr + 16 ? fp : pr + 16;
-        if (lo < hi) {
-            pm_mask(pm, (uint32_t)(lo - pr), (uint32_t)(hi - pr), msk);
-            const uint4 t4 = and4(enc_place(hh, fo - pr), msk);
-            acc.x |= t4.x; acc.y |= t4.y; acc.z |= t4.z; acc.w |= t4.w;
-        }
-        lo = fp > pr ? fp : pr;
-        hi = fe < pr + 16 ? fe : pr + 16;
-        if (lo < hi) {
-            pm_mask(pm, (uint32_t)(lo - pr), (uint32_t)(hi - pr), msk);
-            const int64_t sof = (int64_t)((uint64_t)sh << 32 | sl) + (int64_t)wbase + pr;
-            const uint4 t4 = and4(load16_unaligned(a.src, sof, a.src_bytes), msk);
-            acc.x |= t4.x; acc.y |= t4.y; acc.z |= t4.z; acc.w |= t4.w;
-        }
-        ends_inside = fe < pr + 16;
+    // (split in two: the payload gathers of a piece's two frames are issued together, then the
+    // piece is assembled -- with the gather and its use in one step, the two waited in turn)
+    struct Part {
+        int32_t fo, fp, fe;
+        uint32_t hh[3];
+        bool ok;
+        uint4 pay;   // the 16 source bytes under the piece (when the payload meets it)
     };
+    auto part_load = [&](int32_t t, int32_t pr) -> Part {
+        Part q;
+        q.fo = __shfl(ro, t & 63);
+        q.fp = __shfl(rp, t & 63);
+        q.fe = __shfl(re, t & 63);
+        q.hh[0] = __shfl(h[0], t & 63);
+        q.hh[1] = __shfl(h[1], t & 63);
+        q.hh[2] = __shfl(h[2], t & 63);
+        const uint32_t sl = __shfl(so_lo, t & 63), sh = __shfl(so_hi, t & 63);
+        q.ok = t < (int32_t)nl;
+        q.pay = make_uint4(0, 0, 0, 0);
+        const int32_t lo = q.fp > pr ? q.fp : pr, hi = q.fe < pr + 16 ? q.fe : pr + 16;
+        if (q.ok && lo < hi)
+            q.pay = load16_unaligned(a.src, (int64_t)((uint64_t)sh << 32 | sl) + (int64_t)wbase + pr, a.src_bytes);
+        return q;
+    };
+    // one frame's contribution to a piece: header bytes from registers, payload from the gather
+    auto part_add = [&](const Part& q, int32_t pr, uint4& acc, bool& ends_inside) {
+        ends_inside = false;
+        if (!q.ok) return;
+        uint32_t msk[4];
+        int32_t lo = q.fo > pr ? q.fo : pr, hi = q.fp < pr + 16 ? q.fp : pr + 16;
+        if (lo < hi) {
+            const uint32_t hh[4] = {q.hh[0], q.hh[1], q.hh[2], 0u};
+            pm_mask(pm, (uint32_t)(lo - pr), (uint32_t)(hi - pr), msk);
+            const uint4 t4 = and4(enc_place(hh, q.fo - pr), msk);
+            acc.x |= t4.x; acc.y |= t4.y; acc.z |= t4.z; acc.w |= t4.w;
+        }
+        lo = q.fp > pr ? q.fp : pr;
+        hi = q.fe < pr + 16 ? q.fe : pr + 16;
+        if (lo < hi) {
+            pm_mask(pm, (uint32_t)(lo - pr), (uint32_t)(hi - pr), msk);
+            const uint4 t4 = and4(q.pay, msk);
+            acc.x |= t4.x; acc.y |= t4.y; acc.z |= t4.z; acc.w |= t4.w;
+        }
+        ends_inside = q.fe < pr + 16;
+    };
+    auto part = [&](int32_t t, int32_t pr, uint4& acc, bool& ends_inside) { part_add(part_load(t, pr), pr, acc, ends_inside); };
     for (uint32_t base = 0; base < n_edge; base += 64) {
         const bool act = base + lane < n_edge;
         const uint32_t pid = act ? elist[base + lane] : 0u;
@@ -323,8 +353,9 @@ __device__ __forceinline__ bool encode_window_lanes(const EncCopyArgs& a, const 
         const int32_t ta = find(pr);
         uint4 acc = make_uint4(0, 0, 0, 0);
         bool ea, eb;
-        part(ta, pr, acc, ea);
-        part(ta + 1, pr, acc, eb);
+        const Part qa = part_load(ta, pr), qb = part_load(ta + 1, pr);
+        part_add(qa, pr, acc, ea);
+        part_add(qb, pr, acc, eb);
         // rare: frames shorter than 16 B -> a third, fourth ... frame in a piece
         int32_t t = ta + 2;
         bool more = act && ea && eb && t < (int32_t)nl;
