@@ -347,7 +347,6 @@ __device__ __forceinline__ SegCount walk_segment(const WalkArgs& a, uint32_t s, 
             if (i < a.u8items_cap) {
                 U8Item d{};
                 d.seg = U8_DEAD;
-                d.first = d.last = 1;   // (a whole message of length 0 to k_u8_check's unit_self)
                 d.next = 0xFFFFFFFFu;
                 a.u8items[i] = d;
             }
@@ -1811,9 +1810,8 @@ template <uint32_t NCH, uint32_t WPB>
 #endif
 __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(WSC_CHECK_WPE))) void k_u8_check(U8Args a) {
     __shared__ U8Lds T;
-    __shared__ uint8_t tab8r[9 * 256];   // u8_self_chunk's resync table
     __shared__ uint4 stage[WPB][U8_STAGE];
-    u8_check_run<NCH, WPB>(a, T, tab8r, stage, blockIdx.x, gridDim.x);
+    u8_check_run<NCH, WPB>(a, T, stage, blockIdx.x, gridDim.x);
     // staged pipeline: the decode's last kernel tells the host its scratch is free
     if (a.fin_host) {
         __syncthreads();

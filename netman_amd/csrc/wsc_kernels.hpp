@@ -1,6 +1,5 @@
 // wsc_kernels.hpp -- device-side types shared by the gfx950 kernels and the host launch code.
 #pragma once
-#include <cstddef>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "../../include/wscodec.h"
@@ -56,7 +55,7 @@ struct U8Item {
     uint8_t s_in;       // DFA state entering a chain frame, 0xFF = the previous chain item's result
     uint8_t first, last;   // first / last piece of its frame
 };
-static_assert(sizeof(U8Item) == 32 && offsetof(U8Item, kind) == 28, "U8Item layout (k_u8_check reads kind..last as dword 7)");
+static_assert(sizeof(U8Item) == 32, "U8Item layout");
 struct U8Seg {          // per segment with deferred items (written by the walk)
     uint32_t head, n, done;
     uint32_t pending_end;  // bit 0: a text chain with a deferred part is still open; bit 1: composite items;

@@ -238,64 +238,4 @@ __device__ __forceinline__ uint64_t u8_chunk_map(const U8Lds& t, const V (&v)[4]
     return plain ? trivial() : m;
 }
 
-// ---- single-piece messages from a known entry state ------------------------------------------
-// A whole TEXT message (one piece) starts in state 0, and in a stream that is valid up to some
-// byte the state after it follows from the last 3 bytes alone: a lead or ASCII byte among them
-// restarts the count, and three continuation bytes end any character that is still valid.  So a
-// chain that starts 3 bytes early in state 0, with continuation bytes in state 0 tolerated for
-// those 3 bytes (tab8r: tab8 with row 0 sending 0x80..0xBF to 0), enters its own bytes in the
-// state the stream really has there -- whenever the bytes before it are valid, which the chain
-// before it checks.  Each chain then needs no transition maps (no 8-entry composition of its first
-// bytes, no map composition across chains, lanes and rows): the message is valid iff no chain
-// rejects and the chain holding its last byte ends in state 0.
-// tab8r fill (every thread of a 256-thread workgroup its byte; caller syncs)
-__device__ __forceinline__ void u8_tables_init_resync(uint8_t* tab8r, uint32_t byte) {
-    for (uint32_t st = 0; st < 9; ++st) {
-        const uint32_t ns = st == 8 ? 8u : u8_step(st, byte);
-        tab8r[st * 256 + byte] = (uint8_t)(st == 0 && byte >= 0x80 && byte <= 0xBF ? 0u : ns);
-    }
-}
-// One lane's 64-byte chunk of a single-piece message as 4 chains of 16 bytes: true when the chunk
-// makes the message fail.  `prev` = the 4 bytes before the chunk, unmasked (0 -- ASCII -- when the
-// chunk starts the message); nk = valid bytes (0..64); `last`: the chunk holds the message's last
-// byte.  PART: some lane of the wave holds 0 < nk < 64 (steps past nk are predicated off).
-template <bool PART, typename V>
-__device__ __forceinline__ bool u8_self_chunk(const U8Lds& t, const uint8_t* tab8r, const V (&v)[4], uint32_t mask,
-                                              uint32_t prev, uint32_t nk, bool last) {
-    auto dw = [&](uint32_t j) -> uint32_t { return (uint32_t)v[j >> 2][j & 3] ^ mask; };
-    // st << 8 | byte i of d (the table index; bytes 2-3 zero)
-    auto idx = [](uint32_t st, uint32_t d, uint32_t i) {
-        return __builtin_amdgcn_perm(st, d, i | 4u << 8 | 0x0Cu << 16 | 0x0Cu << 24);
-    };
-    uint32_t st[4];
-#pragma unroll
-    for (uint32_t c = 0; c < 4; ++c) {
-        const uint32_t p = c == 0 ? prev : dw(4 * c - 1);
-        uint32_t s = 0;
-#pragma unroll
-        for (uint32_t i = 1; i < 4; ++i) s = tab8r[idx(s, p, i)];
-        st[c] = s;
-    }
-#pragma unroll
-    for (uint32_t j = 0; j < 4; ++j) {
-#pragma unroll
-        for (uint32_t i = 0; i < 4; ++i) {
-#pragma unroll
-            for (uint32_t c = 0; c < 4; ++c) {
-                const uint32_t ns = t.tab8[idx(st[c], dw(4 * c + j), i)];
-                st[c] = (!PART || 16 * c + 4 * j + i < nk) ? ns : st[c];
-            }
-        }
-    }
-    bool bad = false;
-#pragma unroll
-    for (uint32_t c = 0; c < 4; ++c) bad |= 16 * c < nk && st[c] == 8;
-    if (last) {
-        const uint32_t k = (nk - 1) >> 4;
-        const uint32_t fin = k == 0 ? st[0] : k == 1 ? st[1] : k == 2 ? st[2] : st[3];
-        bad |= fin != 0;
-    }
-    return bad;
-}
-
 }  // namespace wsc

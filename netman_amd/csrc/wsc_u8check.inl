@@ -169,8 +169,8 @@ __device__ __forceinline__ void u8_remask(const U8Args& a, uint32_t seg, uint64_
 // WPB: waves per workgroup (4: 256-thread workgroups; 16: one 1024-thread workgroup per CU, a
 // quarter of the workgroups to dispatch for the same waves)
 template <uint32_t NCH, uint32_t WPB = 4>
-__device__ __forceinline__ void u8_check_run(const U8Args& a, U8Lds& T, uint8_t* tab8r, uint4 (*stage)[U8_STAGE],
-                                             uint32_t bid, uint32_t nblk) {
+__device__ __forceinline__ void u8_check_run(const U8Args& a, U8Lds& T, uint4 (*stage)[U8_STAGE], uint32_t bid,
+                                             uint32_t nblk) {
     // (items past the capacity were dropped by the walk: only a batch whose records overflowed
     // allocates that many, and its verdicts are skipped below)
     const uint32_t n_items = *a.count < a.items_cap ? *a.count : a.items_cap;
@@ -205,10 +205,7 @@ __device__ __forceinline__ void u8_check_run(const U8Args& a, U8Lds& T, uint8_t*
         fail_settle(ord != 0xFFFFFFFFu, seg, ord);
     };
     if (bid * WPB < n_items) {   // (nothing deferred, or fewer units than waves: only the signal)
-    if (threadIdx.x < 256) {
-        u8_tables_init(T, threadIdx.x);
-        u8_tables_init_resync(tab8r, threadIdx.x);
-    }
+    if (threadIdx.x < 256) u8_tables_init(T, threadIdx.x);
     __syncthreads();
     const uint32_t gw = __builtin_amdgcn_readfirstlane(bid * WPB + (threadIdx.x >> 6));
     const uint32_t nw = nblk * WPB;
@@ -321,43 +318,21 @@ __device__ __forceinline__ void u8_check_run(const U8Args& a, U8Lds& T, uint8_t*
     const uint32_t n_units = (n_items + 3) / 4;
     // A small unit's 4 items as the step needs them (uniform, scalar loads); entries past the last
     // item have len 0.
-    // self: every item a whole TEXT message (SELF, first and last piece; dead slots say so too)
-    struct UnitS { uint64_t src[4]; uint32_t len[4], mask[4]; bool self; };
+    struct UnitS { uint64_t src[4]; uint32_t len[4], mask[4]; };
     auto unit_items = [&](uint32_t u, UnitS& x) {
         const uint32_t i0 = 4 * u, cnt = n_items - i0 < 4 ? n_items - i0 : 4u;
-        x.self = true;
 #pragma unroll
         for (uint32_t k = 0; k < 4; ++k) {
             const U8Item it = a.items[i0 + (k < cnt ? k : 0u)];
             x.src[k] = it.src;
             x.len[k] = k < cnt ? it.len : 0u;
             x.mask[k] = it.mask;
-            // kind, s_in, first, last as one dword (a scalar load; the byte fields would be vector loads)
-            const uint32_t fl = reinterpret_cast<const uint32_t*>(a.items + i0 + (k < cnt ? k : 0u))[7];
-            x.self = x.self && (fl & 0xFFFF00FFu) == (U8K_SELF | 1u << 16 | 1u << 24);
         }
     };
     auto unit_small = [](const UnitS& x) -> bool {
         return x.len[0] <= 1024 && x.len[1] <= 1024 && x.len[2] <= 1024 && x.len[3] <= 1024;
     };
-    // units of whole TEXT messages <= 1 KiB whose 1 KiB reads stay inside the wire: pass 1
-    // (u8_self_chunk), skipped by pass 2
-    auto unit_fast = [&](const UnitS& x) -> bool {
-        return x.self && unit_small(x) && x.src[0] + 1024 <= a.n_bytes && x.src[1] + 1024 <= a.n_bytes &&
-               x.src[2] + 1024 <= a.n_bytes && x.src[3] + 1024 <= a.n_bytes;
-    };
-    // a fast unit's data: plain 16-byte loads, every lane, the address clamped into the wire (only
-    // called when it holds >= 1 KiB; bytes past an item are never looked at).  No edge path and no
-    // condition: load16_unaligned's byte loads, or a conditional prefetch, made the compiler wait
-    // for every load in flight -- the next unit's prefetch too -- before the restage.
-    auto unit_data_fast = [&](const UnitS& x, u32x4 (&q)[4]) {
-#pragma unroll
-        for (uint32_t k = 0; k < 4; ++k) {
-            const uint64_t o = x.src[k] + 16u * lane;
-            const u32x4u_ld t = *reinterpret_cast<const u32x4u_ld*>(a.wire + (o + 16 <= a.n_bytes ? o : a.n_bytes - 16));
-            q[k] = u32x4{t.x, t.y, t.z, t.w};
-        }
-    };
+    // piece k of a small unit's step = item k's KiB (16 B per lane, coalesced)
     auto unit_data = [&](const UnitS& x, u32x4 (&q)[4]) {
 #pragma unroll
         for (uint32_t k = 0; k < 4; ++k) {
@@ -366,64 +341,6 @@ __device__ __forceinline__ void u8_check_run(const U8Args& a, U8Lds& T, uint8_t*
             q[k] = u32x4{t.x, t.y, t.z, t.w};
         }
     };
-    // Pass 1: units of whole TEXT messages <= 1 KiB (text frames), every lane its 64-byte chunk as
-    // chains from known states (u8_self_chunk), the verdict by one ballot.  Its own loop (the
-    // registers of pass 2's large items are not live here): a unit's descriptors are loaded two
-    // units ahead and its data one unit ahead, and row r's length and mask come from the scalar
-    // descriptors -- the item record is read only on a failure.
-    if (a.n_bytes >= 1024) {   // (no unit is fast otherwise)
-        UnitS xc, xn;
-        u32x4 qc[4], qn[4];
-        bool cf = false;
-        if (gw < n_units) {
-            unit_items(gw, xc);
-            cf = unit_fast(xc);
-            unit_data_fast(xc, qc);
-        }
-        xn = xc;
-        if (gw + nw < n_units) unit_items(gw + nw, xn);
-        for (uint32_t u = gw; u < n_units; u += nw) {
-            const uint32_t i0 = 4 * u;
-            const uint32_t cnt = n_items - i0 < 4 ? n_items - i0 : 4u;
-            const uint32_t un = u + nw;
-            const bool nf = un < n_units && unit_fast(xn);
-            unit_data_fast(xn, qn);   // (every iteration: a constant count of loads in flight)
-            if (cf) {
-                const uint32_t r = lane >> 4;
-                const uint32_t rlen = r == 0 ? xc.len[0] : r == 1 ? xc.len[1] : r == 2 ? xc.len[2] : xc.len[3];
-                const uint32_t rmask = r == 0 ? xc.mask[0] : r == 1 ? xc.mask[1] : r == 2 ? xc.mask[2] : xc.mask[3];
-                u8_restage(sw, qc, lane);
-                const uint32_t off = (lane & 15) * 64;
-                const uint32_t rmk = a.unmasked ? 0u : rmask;
-                const uint32_t nk = chunk_len(rlen, off);
-                // the 4 bytes before the chunk: the previous lane's last dword (0 at a row's start)
-                const uint32_t pv = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)qc[3][3], 0x111, 0xF, 0xF, true);
-                const uint32_t prev = (lane & 15) ? pv ^ rmk : 0u;
-                uint32_t hib = 0;
-#pragma unroll
-                for (uint32_t j = 0; j < 16; ++j) hib |= (uint32_t)qc[j >> 2][j & 3] ^ rmk;
-                const bool last = nk != 0 && off + nk == rlen;
-                uint64_t badm = 0;
-                if (__ballot(nk > 0 && (hib & 0x80808080u) != 0) != 0) {   // (ASCII everywhere: all pass)
-                    const bool bad = __ballot(nk > 0 && nk < 64) != 0 ? u8_self_chunk<true>(T, tab8r, qc, rmk, prev, nk, last)
-                                                                      : u8_self_chunk<false>(T, tab8r, qc, rmk, prev, nk, last);
-                    badm = __ballot(bad);
-                }
-                // row r's message fails when any of its lanes says so; applied by the row's first lane
-                const bool f = (lane & 15) == 0 && r < cnt && ((badm >> (16 * r)) & 0xFFFFull) != 0;
-                if (__ballot(f)) {
-                    const U8Item xr = a.items[i0 + (r < cnt ? r : 0u)];
-                    fail_settle(f && xr.seg != U8_DEAD, xr.seg, xr.ordinal);
-                }
-            }
-            xc = xn;
-#pragma unroll
-            for (uint32_t k = 0; k < 4; ++k) qc[k] = qn[k];
-            cf = nf;
-            if (un + nw < n_units) unit_items(un + nw, xn);
-        }
-    }
-    // Pass 2: the other units.
     // Software pipeline over a wave's units: the next unit's items are loaded one unit ahead, and
     // (small units) its data loads go out before this unit's verdict atomics, so the dependent
     // round trips of consecutive units overlap (1 KiB text: 4 per unit otherwise)
@@ -436,7 +353,7 @@ __device__ __forceinline__ void u8_check_run(const U8Args& a, U8Lds& T, uint8_t*
     uint32_t pret = 0, pn = 0, pseg = 0, pcnt = 0;
     if (gw < n_units) {
         unit_items(gw, xc);
-        cur_small = unit_small(xc) && !xc.self;
+        cur_small = unit_small(xc);
         if (cur_small && WSC_CHECK_PREFETCH) unit_data(xc, qc);
     }
     if (gw + nw < n_units) unit_items(gw + nw, xn);
@@ -461,7 +378,7 @@ __device__ __forceinline__ void u8_check_run(const U8Args& a, U8Lds& T, uint8_t*
             const uint64_t pm = u8_chunk_map<NCH, U8P_LANE>(T, qc, a.unmasked ? 0u : rmask, chunk_len(rlen, off), plain);
             const uint64_t rm = u8_row_maps(pm, lane);
             if (un < n_units) {
-                nsmall = unit_small(xn) && !xn.self;
+                nsmall = unit_small(xn);
                 if (nsmall && WSC_CHECK_PREFETCH) unit_data(xn, qn);
             }
             settle(pact && pret + pcnt == pn, pseg);
@@ -493,13 +410,11 @@ __device__ __forceinline__ void u8_check_run(const U8Args& a, U8Lds& T, uint8_t*
             }
             pseg = xr.seg;
         } else {
-            if (!unit_fast(xc)) {   // (a fast unit was done by pass 1)
-                settle(pact && pret + pcnt == pn, pseg);
-                pact = false;
-                unit_large(i0, cnt);
-            }
+            settle(pact && pret + pcnt == pn, pseg);
+            pact = false;
+            unit_large(i0, cnt);
             if (un < n_units) {
-                nsmall = unit_small(xn) && !xn.self;
+                nsmall = unit_small(xn);
                 if (nsmall && WSC_CHECK_PREFETCH) unit_data(xn, qn);
             }
         }
