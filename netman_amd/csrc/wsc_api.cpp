@@ -846,6 +846,8 @@ static int launch_encode(wsc_ctx* c, const wsc_out_msg* msgs, uint32_t n, const 
     ca.lb_rec = c->enc_lb_rec;
     ca.n_lb = sblocks + 2;
     ca.xcd_run = c->enc_xcd_run;
+    // small messages (src bytes per message < two windows): most windows hold frame edges
+    ca.hoist = src_bytes < (uint64_t)n * 2 * ENC_WIN ? 1u : 0u;
     uint64_t wins = (out_cap + ENC_WIN - 1) / ENC_WIN;   // the grid covers out_cap; waves past the total exit
     if (wins > c->enc_tile_entries) wins = c->enc_tile_entries;
     if (wins == 0) wins = 1;

@@ -373,6 +373,159 @@ __device__ __forceinline__ bool encode_window_lanes(const EncCopyArgs& a, const 
     return true;
 }
 
+// The same window in one memory round trip, when it can: every gather of both passes -- the
+// pieces inside one payload and the two frames' payload bytes under each edge piece -- is issued
+// before any is waited on, as plain 16-byte loads (a lane with nothing to gather reads src + 0).
+// Taken when the window has at most 64 edge pieces (a piece meeting a third frame -- frames under
+// 16 B -- gathers it in the loop at the end) and every gather lies inside src (a wave-uniform test; load16_unaligned's byte path for the ends
+// of src made the compiler wait on each gather in turn).  Returns false, having written nothing,
+// when it cannot: encode_window_lanes then takes the window.
+template <int NT>
+__device__ __forceinline__ bool encode_window_direct(const EncCopyArgs& a, const EncLanes& L, uint32_t base, uint64_t wbase,
+                                                     uint64_t limit, uint32_t lane, const u32x4* __restrict__ pm,
+                                                     uint16_t* __restrict__ elist) {
+    constexpr uint32_t P = ENC_WIN / 1024;
+    constexpr int64_t WB = ENC_WIN;
+    if (a.src_bytes < 16) return false;
+    const int64_t smax = (int64_t)a.src_bytes - 16;
+    auto clip = [](uint64_t x, uint64_t wb) -> int32_t {   // as in encode_window_lanes
+        if (x == ~0ull || x > wb + (uint64_t)(WB + 64)) return (int32_t)WB + 64;
+        return x + (1ull << 30) < wb ? -(1 << 30) : (int32_t)((int64_t)x - (int64_t)wb);
+    };
+    const int32_t ro = clip(L.o, wbase), rp = clip(L.p, wbase), re = clip(L.e, wbase);
+    const uint32_t h[4] = {L.h[0], L.h[1], L.h[2], 0u};
+    const uint32_t so_lo = (uint32_t)L.so, so_hi = (uint32_t)((uint64_t)L.so >> 32);
+    const uint32_t nl = (uint32_t)__builtin_popcountll(__ballot(ro < (int32_t)WB));
+    if (nl == 64 && __shfl(re, 63) < (int32_t)WB && base + 64 < a.n_msgs) return false;
+    const int32_t st0 = nl == 0 ? 0 : (nl >= 32 ? 32 : (int32_t)((1u << (32 - __builtin_clz(nl))) >> 1));
+    auto find = [&](int32_t pr) -> int32_t {
+        int32_t lo = -1;
+        for (int32_t st = st0; st >= 1; st >>= 1) {
+            const int32_t c = lo + st;
+            const int32_t dv = __shfl(ro, c & 63);
+            if (c < (int32_t)nl && dv <= pr) lo = c;
+        }
+        return lo < 0 ? 0 : lo;
+    };
+    auto src_of = [&](int32_t t) -> int64_t {   // frame t's source offset of output byte x: so + x
+        const uint32_t sl = __shfl(so_lo, t & 63), sh = __shfl(so_hi, t & 63);
+        return (int64_t)((uint64_t)sh << 32 | sl);
+    };
+    bool safe = true;
+    // pass 1's pieces: inside one payload -> gather address; otherwise listed as an edge piece
+    uint32_t n_edge = 0;
+    int64_t g1[P];
+    bool ins[P];
+#pragma unroll
+    for (uint32_t k = 0; k < P; ++k) {
+        const int32_t pr = (int32_t)(k * 1024 + lane * 16);
+        const uint64_t pa = wbase + (uint64_t)pr;
+        const int32_t t = find(pr);
+        const int32_t fp = __shfl(rp, t & 63), fe = __shfl(re, t & 63);
+        const int64_t g = src_of(t) + (int64_t)pa;
+        const bool inside = t < (int32_t)nl && fp <= pr && pr + 16 <= fe && pa + 16 <= limit;
+        ins[k] = inside;
+        g1[k] = inside ? g : 0;
+        safe = safe && (!inside || (g >= 0 && g <= smax));
+        const bool edge = !inside && pa < limit;
+        const uint64_t em = __ballot(edge);
+        if (edge)
+            elist[n_edge + __builtin_amdgcn_mbcnt_hi((uint32_t)(em >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)em, 0u))] =
+                (uint16_t)(k * 64 + lane);
+        n_edge += (uint32_t)__builtin_popcountll(em);
+    }
+    if (n_edge > 64) return false;
+    __builtin_amdgcn_wave_barrier();
+    // pass 2's pieces, one per lane: the frame holding the piece's first byte (a) and the next (b)
+    const bool act = lane < n_edge;
+    const uint32_t pid = act ? elist[lane] : 0u;
+    const int32_t pr2 = (int32_t)((pid >> 6) * 1024 + (pid & 63) * 16);
+    const int32_t ta = find(pr2);
+    struct Meta { int32_t fo, fp, fe; uint32_t hh[3]; bool ok; int64_t g; };
+    auto meta = [&](int32_t t) -> Meta {
+        Meta q;
+        q.fo = __shfl(ro, t & 63);
+        q.fp = __shfl(rp, t & 63);
+        q.fe = __shfl(re, t & 63);
+        q.hh[0] = __shfl(h[0], t & 63);
+        q.hh[1] = __shfl(h[1], t & 63);
+        q.hh[2] = __shfl(h[2], t & 63);
+        q.ok = act && t < (int32_t)nl;
+        const int32_t lo = q.fp > pr2 ? q.fp : pr2, hi = q.fe < pr2 + 16 ? q.fe : pr2 + 16;
+        const int64_t g = src_of(t) + (int64_t)wbase + pr2;
+        const bool need = q.ok && lo < hi;
+        q.g = need ? g : 0;
+        safe = safe && (!need || (g >= 0 && g <= smax));
+        return q;
+    };
+    const Meta qa = meta(ta), qb = meta(ta + 1);
+    if (__ballot(!safe)) return false;
+    // every gather at once
+    auto ld = [&](int64_t g) -> uint4 {
+        const u32x4u_ld t = *reinterpret_cast<const u32x4u_ld*>(a.src + g);
+        return make_uint4(t.x, t.y, t.z, t.w);
+    };
+    uint4 v[P];
+#pragma unroll
+    for (uint32_t k = 0; k < P; ++k) v[k] = ld(g1[k]);
+    const uint4 pay_a = ld(qa.g), pay_b = ld(qb.g);
+#pragma unroll
+    for (uint32_t k = 0; k < P; ++k) {
+        const uint64_t pa = wbase + k * 1024u + lane * 16u;
+        if (ins[k]) enc_st<NT>(a.out, wbase, pa, u32x4{v[k].x, v[k].y, v[k].z, v[k].w});
+    }
+    if (n_edge == 0) return true;
+    // assemble the edge pieces: header bytes from registers, payload bytes from the gathers
+    auto add = [&](const Meta& q, const uint4& pay, uint4& acc) -> bool {
+        if (!q.ok) return false;
+        uint32_t msk[4];
+        int32_t lo = q.fo > pr2 ? q.fo : pr2, hi = q.fp < pr2 + 16 ? q.fp : pr2 + 16;
+        if (lo < hi) {
+            const uint32_t hh[4] = {q.hh[0], q.hh[1], q.hh[2], 0u};
+            pm_mask(pm, (uint32_t)(lo - pr2), (uint32_t)(hi - pr2), msk);
+            const uint4 t4 = and4(enc_place(hh, q.fo - pr2), msk);
+            acc.x |= t4.x; acc.y |= t4.y; acc.z |= t4.z; acc.w |= t4.w;
+        }
+        lo = q.fp > pr2 ? q.fp : pr2;
+        hi = q.fe < pr2 + 16 ? q.fe : pr2 + 16;
+        if (lo < hi) {
+            pm_mask(pm, (uint32_t)(lo - pr2), (uint32_t)(hi - pr2), msk);
+            const uint4 t4 = and4(pay, msk);
+            acc.x |= t4.x; acc.y |= t4.y; acc.z |= t4.z; acc.w |= t4.w;
+        }
+        return q.fe < pr2 + 16;
+    };
+    uint4 acc = make_uint4(0, 0, 0, 0);
+    const bool ea = add(qa, pay_a, acc);
+    const bool eb = add(qb, pay_b, acc);
+    // rare: frames shorter than 16 B -> a third, fourth ... frame in a piece (one gather each)
+    int32_t t = ta + 2;
+    bool more = act && ea && eb && t < (int32_t)nl;
+    while (__ballot(more)) {
+        const int32_t fo = __shfl(ro, t & 63);
+        more = more && t < (int32_t)nl && fo < pr2 + 16;
+        Meta q = meta(t);
+        q.ok = q.ok && more;
+        const uint4 pay = load16_unaligned(a.src, q.g, a.src_bytes);   // (q.g = 0 when unused: a harmless read)
+        uint4 tmp = make_uint4(0, 0, 0, 0);
+        add(q, pay, tmp);
+        acc.x |= tmp.x; acc.y |= tmp.y; acc.z |= tmp.z; acc.w |= tmp.w;
+        ++t;
+    }
+    if (act) {
+        const uint64_t pa = wbase + (uint64_t)pr2;
+        if (pa + 16 <= limit) {
+            enc_st<NT>(a.out, wbase, pa, u32x4{acc.x, acc.y, acc.z, acc.w});
+        } else {   // the tail piece: never write at or past the total / out_cap
+            const uint32_t d[4] = {acc.x, acc.y, acc.z, acc.w};
+#pragma unroll
+            for (uint32_t b = 0; b < 16; ++b)
+                if (pa + b < limit) a.out[pa + b] = (uint8_t)(d[b >> 2] >> (8 * (b & 3)));
+        }
+    }
+    return true;
+}
+
 // A window with more than 64 frames: frame by frame from m, every lane assembling its P pieces.
 template <int NT>
 __device__ __forceinline__ void encode_window_serial(const EncCopyArgs& a, uint32_t m, uint64_t wbase, uint64_t limit,
@@ -482,14 +635,21 @@ __global__ __launch_bounds__(256) void k_encode_copy(EncCopyArgs a) {
     const uint32_t m = a.tile[gw];
     const wsc_out_msg mm = a.msgs[m];
     const uint64_t o = a.out_off[m];
+    // the frames from m in lanes: with small messages (most windows hold frame edges: a.hoist)
+    // loaded beside m's own descriptor -- the general path's next round trip; with large ones only
+    // when the window is not inside one payload (1 KiB encode 0.4325 -> 0.4279 ms hoisted, 64 KiB
+    // 0.3508 -> 0.3446 ms not: interleaved A/B, profiles/r06/enc_direct_ab.log)
+    EncLanes L;
+    if (a.hoist) L = enc_lanes_load(a, m, lane);
     const uint64_t p0 = o + enc_hlen(mm.len), p1 = p0 + mm.len;
     if (p0 <= wbase && p1 >= wbase + ENC_WIN && wbase + ENC_WIN <= limit) {
         encode_window_inside<NT>(a, (int64_t)mm.src_off - (int64_t)p0, wbase, lane);
         return;
     }
+    if (!a.hoist) L = enc_lanes_load(a, m, lane);
     // general path: frame edges in the window -> lane-parallel frame lookup (serial walk over the
     // frames only when more than 64 of them overlap the window)
-    const EncLanes L = enc_lanes_load(a, m, lane);
+    if (encode_window_direct<NT>(a, L, m, wbase, limit, lane, pm, elist[threadIdx.x >> 6])) return;
     if (encode_window_lanes<NT>(a, L, m, wbase, limit, lane, pm, elist[threadIdx.x >> 6])) return;
     encode_window_serial<NT>(a, m, wbase, limit, lane);
 }

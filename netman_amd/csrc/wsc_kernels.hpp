@@ -195,6 +195,7 @@ struct EncCopyArgs {
     uint64_t* lb_rec;            // ... and its records
     uint32_t n_lb;
     uint32_t xcd_run;            // blocks per XCD run (xcd_run_block)
+    uint32_t hoist;              // load the window's frames before the inside-one-payload test (small messages)
 };
 
 }  // namespace wsc
