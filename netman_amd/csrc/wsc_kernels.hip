@@ -1610,30 +1610,6 @@ __device__ __forceinline__ bool simple_seg(const WalkArgs& a, const SegIn& x, Si
     return simple_state(x.st.status, x.st.cont_len, x.st.frame_rem) && simple_hdr(a, x.start, x.end, x.hdr, o);
 }
 
-// The tiled walk's header cache, in place (round 6): phase 1 leaves in each segment's slot what
-// phase 2 needs to emit a simple segment -- {start bits 0..31; start bits 32..35 | header-length
-// code << 4 | plen << 6; mask; msg_id}, code 0 / 1 / 2 = a 6 / 8 / 14-byte header, 3 = not a simple
-// segment (or one the record cannot hold: start >= 2^36, plen >= 2^26) -- so a tile of simple
-// segments is emitted from these 16 bytes alone, without reading seg_off and the 40-byte carried
-// state again.  A tile with any other segment reads its inputs afresh (bounds, wire headers).
-constexpr uint32_t PK_NOT_SIMPLE = 3u << 4;
-__device__ __forceinline__ uint4 pack_simple(const SegIn& x, const SimpleSeg& g) {
-    if (x.start >> 36 || g.plen >> 26) return make_uint4(0, PK_NOT_SIMPLE, 0, 0);
-    const uint32_t code = g.hl == 6 ? 0u : (g.hl == 8 ? 1u : 2u);
-    return make_uint4((uint32_t)x.start, (uint32_t)(x.start >> 32) | code << 4 | g.plen << 6, g.mask, x.st.msg_id);
-}
-__device__ __forceinline__ bool pack_is_simple(const uint4& p) { return (p.y & PK_NOT_SIMPLE) != PK_NOT_SIMPLE; }
-__device__ __forceinline__ void unpack_simple(const uint4& p, SegIn& x, SimpleSeg& g) {
-    const uint32_t code = (p.y >> 4) & 3u;
-    g.hl = code == 0 ? 6u : (code == 1 ? 8u : 14u);
-    g.plen = p.y >> 6;
-    g.mask = p.z;
-    x.start = p.x | (uint64_t)(p.y & 0xFu) << 32;
-    x.end = x.start + g.hl + g.plen;
-    x.st = wsc_conn_state{};
-    x.st.msg_id = p.w;
-}
-
 // The outputs walk_segment<EMIT> writes for a simple segment s (frame fi, span si): its record, span,
 // window-index entries (windows starting inside the segment look the span up), result and carried
 // state -- consecutive lanes hold consecutive segments, so every store is coalesced.
@@ -1735,14 +1711,10 @@ __global__ __launch_bounds__(NT) void k_walk_tiled(WalkArgs a, uint32_t per_bloc
                     tot.frames += 1;
                     tot.spans0 += 1;
                     tot.bytes0 += g.plen;
-                    if (a.hdr_cache) a.hdr_cache[t + lane] = pack_simple(x0, g);
+                    if (a.hdr_cache) a.hdr_cache[t + lane] = x0.hdr;
                 } else {
-                    // (in place the slot says "not simple" and phase 2 reads this tile afresh;
-                    // COMPACT caches the raw header for its phase-2 walk)
-                    if (!COMPACT && a.hdr_cache) a.hdr_cache[t + lane] = make_uint4(0, PK_NOT_SIMPLE, 0, 0);
                     tot = sc_add(tot, walk_segment<false, COMPACT, NT, 4, true>(a, t + lane, zero, zero, nullptr, nullptr,
-                                                                                nullptr, 0, 0, nullptr, &x0,
-                                                                                COMPACT ? a.hdr_cache : nullptr));
+                                                                                nullptr, 0, 0, nullptr, &x0, a.hdr_cache));
                 }
             }
             x0 = x1;
@@ -1767,65 +1739,9 @@ __global__ __launch_bounds__(NT) void k_walk_tiled(WalkArgs a, uint32_t per_bloc
         x.hdr = (t < se && s < se && a.hdr_cache) ? a.hdr_cache[s] : make_uint4(0, 0, 0, 0);
         if (!a.hdr_cache) first_hdr(x);
     };
-    // the simple-tile emit (one lane per segment, outputs straight from its inputs): returns false
-    // (nothing written) unless every segment of the tile is simple
-    auto simple_tile = [&](uint32_t t, bool simple, const SegIn& x, const SimpleSeg& g) -> bool {
-        if (!__syncthreads_and(simple)) return false;
-        const bool mine = t + lane < se;
-        const uint32_t n = se - t < NT ? se - t : NT;
-        uint64_t b = mine ? g.plen : 0u;
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) {
-            const uint32_t lo = __shfl_xor((uint32_t)b, d), hi = __shfl_xor((uint32_t)(b >> 32), d);
-            b += (uint64_t)hi << 32 | lo;
-        }
-        if (wl == 0) L.wave[wave].bytes0 = b;
-        if (mine) emit_simple(a, t + lane, x, g, run.frames + lane, run.spans0 + run.spans1 + lane);
-        __syncthreads();
-        uint64_t bsum = 0;
-#pragma unroll
-        for (uint32_t w = 0; w < NT / 64; ++w) bsum += L.wave[w].bytes0;
-        run.frames += n;
-        run.spans0 += n;
-        run.bytes0 += bsum;
-        __syncthreads();   // (L.wave is reused by the next tile)
-        return true;
-    };
-    bool phase2_done = false;
-    if constexpr (!COMPACT) {
-        if (a.hdr_cache) {
-            // packed slots (pack_simple), the next tile's in flight while a tile is emitted
-            auto slot = [&](uint32_t t) -> uint4 {
-                const uint32_t s = t + lane;
-                return (t < se && s < se) ? a.hdr_cache[s] : make_uint4(0, 0, 0, 0);   // (past the end: "simple")
-            };
-            uint4 p0 = slot(sb);
-            for (uint32_t t = sb; t < se; t += NT) {
-                const uint4 p1 = slot(t + NT);
-                SegIn x;
-                SimpleSeg g;
-                unpack_simple(p0, x, g);
-                if (!simple_tile(t, pack_is_simple(p0), x, g)) {
-                    // a tile with other segments: its inputs afresh, the walk with LDS records
-                    SegIn y;
-                    bounds(t, y);
-                    first_hdr(y);
-                    uint32_t nrec;
-                    const SegCount c = tile_count<COMPACT, KR, NT, 1>(a, L, t + lane, se, lane, nrec, false, &y);
-                    SegCount ttot;
-                    const SegCount excl = tile_scan<NT>(c, L, wl, wave, ttot);
-                    tile_emit<COMPACT, KR, NT, 1>(a, L, sc_add(run, excl), nrec, t, se, lane);
-                    run = sc_add(run, ttot);
-                    __syncthreads();   // (the tile's LDS is reused by the next tile)
-                }
-                p0 = p1;
-            }
-            phase2_done = true;
-        }
-    }
     SegIn y0, y1;
-    if (!phase2_done) cached(sb, y0);
-    for (uint32_t t = sb; t < se && !phase2_done; t += NT) {
+    cached(sb, y0);
+    for (uint32_t t = sb; t < se; t += NT) {
         cached(t + NT, y1);
         if constexpr (!COMPACT) {
             // a tile of simple segments only (one complete plain BIN frame each): frame and span
@@ -1834,8 +1750,25 @@ __global__ __launch_bounds__(NT) void k_walk_tiled(WalkArgs a, uint32_t per_bloc
             const bool mine = t + lane < se;
             SimpleSeg g{};
             const bool simple = !mine || simple_seg(a, y0, g);
-            if (simple_tile(t, simple, y0, g)) {
+            if (__syncthreads_and(simple)) {
+                const uint32_t n = se - t < NT ? se - t : NT;
+                uint64_t b = mine ? g.plen : 0u;
+#pragma unroll
+                for (int d = 32; d >= 1; d >>= 1) {
+                    const uint32_t lo = __shfl_xor((uint32_t)b, d), hi = __shfl_xor((uint32_t)(b >> 32), d);
+                    b += (uint64_t)hi << 32 | lo;
+                }
+                if (wl == 0) L.wave[wave].bytes0 = b;
+                if (mine) emit_simple(a, t + lane, y0, g, run.frames + lane, run.spans0 + run.spans1 + lane);
+                __syncthreads();
+                uint64_t bsum = 0;
+#pragma unroll
+                for (uint32_t w = 0; w < NT / 64; ++w) bsum += L.wave[w].bytes0;
+                run.frames += n;
+                run.spans0 += n;
+                run.bytes0 += bsum;
                 y0 = y1;
+                __syncthreads();   // (L.wave is reused by the next tile)
                 continue;
             }
         }
