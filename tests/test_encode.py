@@ -147,6 +147,27 @@ def test_gpu_encode_scan_widths(codec_lib, n):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("src_bytes", [1, 7, 15, 16, 17, 40, 4096])
+def test_gpu_encode_gathers_at_the_ends_of_src(codec, src_bytes):
+    """the copy's one-round-trip window (encode_window_direct) reads plain 16-byte pieces only when
+    every gather of the window lies inside src, else the window takes the two-pass path: sources
+    shorter than 16 bytes, and messages starting at src byte 0 or ending at its last byte (their
+    pieces' 16-byte reads cross the ends of src), equal the oracle either way"""
+    from netman_amd import codec as K
+    rng = np.random.default_rng(5000 + src_bytes)
+    src = rng.integers(0, 256, src_bytes, dtype=np.uint8)
+    n = 3000
+    lens = rng.integers(0, src_bytes + 1, n).astype(np.uint64)
+    at = rng.integers(0, 3, n)   # 0: from src byte 0, 1: ending at its last byte, 2: anywhere
+    offs = np.where(at == 0, 0, np.where(at == 1, src_bytes - lens,
+                                         [rng.integers(0, src_bytes - int(L) + 1) for L in lens])).astype(np.uint64)
+    msgs = np.zeros(n, K.OUT_MSG_DTYPE)
+    msgs["src_off"], msgs["len"] = offs, lens
+    msgs["first_byte"] = rng.choice(np.array([0x81, 0x82], np.uint8), size=n)
+    _check(codec, msgs, src)
+
+
+@pytest.mark.gpu
 def test_gpu_encode_large_frames(codec):
     msgs, src = _batch(8, 24, [1 << 20, (1 << 20) + 3, 3 * 65536 + 7, 131], src_bytes=8 << 20)
     _check(codec, msgs, src)
