@@ -388,6 +388,8 @@ __device__ __forceinline__ bool encode_window_direct(const EncCopyArgs& a, const
     constexpr int64_t WB = ENC_WIN;
     if (a.src_bytes < 16) return false;
     const int64_t smax = (int64_t)a.src_bytes - 16;
+    // (clip and find repeat encode_window_lanes' on purpose: shared as __device__ helpers the kernel
+    // compiled to 82 VGPRs, 5 waves per SIMD, and the 1 KiB encode ran 0.429 -> 0.437 ms)
     auto clip = [](uint64_t x, uint64_t wb) -> int32_t {   // as in encode_window_lanes
         if (x == ~0ull || x > wb + (uint64_t)(WB + 64)) return (int32_t)WB + 64;
         return x + (1ull << 30) < wb ? -(1 << 30) : (int32_t)((int64_t)x - (int64_t)wb);
